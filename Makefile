@@ -1,0 +1,29 @@
+# Builds the product library (HIP, gfx950) and the test-only oracle.
+#   make            -> pollnet_amd/libpollnet_amd.so + oracle/liboracle.so (+ oracle/_ref when /root/reference exists)
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+CFLAGS_ORACLE = -O3 -march=x86-64-v3 -fPIC -Wall -std=c11
+
+LIB = pollnet_amd/libpollnet_amd.so
+SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
+HDRS = include/pollnet_amd.h
+
+ORACLE = oracle/liboracle.so
+REFDIR ?= /root/reference
+
+all: $(LIB) $(ORACLE) ref
+
+$(LIB): $(SRCS) $(HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lpthread
+
+$(ORACLE): oracle/pn_oracle.c oracle/pn_oracle.h $(HDRS)
+	gcc $(CFLAGS_ORACLE) -shared -o $@ oracle/pn_oracle.c -lpthread
+
+ref:
+	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
+
+clean:
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so
+
+.PHONY: all ref clean

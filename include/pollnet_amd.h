@@ -1,0 +1,174 @@
+/*
+ * pollnet_amd.h — C-ABI of the MI355X receive-path per-frame transform.
+ *
+ * This is the drop-in seam for efvitcp's RX hot path.  In the reference every
+ * raw frame taken off the ef_vi ring goes through `Core::pollNet`
+ * (/root/reference/efvitcp/Core.h:494-552): header pointers (:503-507),
+ * `connHashKey` (:508 -> :167-172), `findConnEntry` (:509 -> :558-562), the
+ * TIME_WAIT test (:510), and then `recv_handler(key, entry, eth)` (:526) whose
+ * stateless part is `TcpConn::onPack`'s payload arithmetic
+ * (/root/reference/efvitcp/TcpConn.h:469-473).  The IP/TCP one's-complement
+ * verification is `Core::checksum` (Core.h:448-472, EFVITCP_DEBUG only in the
+ * reference) built on `CSum` (Core.h:89-138).
+ *
+ * Here that per-frame work runs as one batched HIP kernel over frames resident
+ * in HBM and produces one 16-byte `pn_result` per frame.  Everything stateful
+ * (TCP state machine, TIME_WAIT bookkeeping, timers, TX) stays on the host.
+ *
+ * Conventions (mirroring the reference's error style, Core.h:253-383 returns
+ * `const char*`, Socket.h:47 `getLastError()`):
+ *   - every function returns 0 on success and a negative PN_E* code on error;
+ *   - `pn_last_error(ctx)` returns a static/ctx-owned message for the last error;
+ *   - no C++ types, no exceptions cross this ABI; pointers + sizes only;
+ *   - device pointers are plain `void*` from hipMalloc (or torch), streams are
+ *     `hipStream_t` passed as `void*` (NULL = the null stream).
+ */
+#ifndef POLLNET_AMD_H
+#define POLLNET_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PN_ABI_VERSION 1
+
+/* ---- constants taken from the reference (Core.h) ---- */
+#define PN_RECV_BUF_SIZE 2048u         /* RecvBufSize, Core.h:45 (ring slot stride) */
+#define PN_RECV_MSS 1460u              /* RecvMSS, Core.h:44 */
+#define PN_EMPTY_KEY (1ull << 63)      /* EmptyKey, Core.h:49 */
+#define PN_MISS 0xFFFFFFFFu            /* pn_result.conn_id when findConnEntry misses */
+
+/* ---- error codes ---- */
+#define PN_OK 0
+#define PN_EINVAL -1    /* bad argument (shape/alignment contract violated) */
+#define PN_EHIP -2      /* a HIP runtime call failed (see pn_last_error) */
+#define PN_ENOMEM -3    /* allocation failed */
+#define PN_ENOTABLE -4  /* pn_classify before pn_set_conn_table */
+#define PN_EFULL -5     /* conn table full */
+#define PN_ENOENT -6    /* key not in conn table */
+
+/* ---- per-frame output record (16 bytes, written coalesced) ---- */
+typedef struct pn_result {
+  uint32_t conn_id;     /* entry->conn_id on hit (Core.h:510/TcpServer.h:96), PN_MISS on miss.
+                           conn_id >= max_conn_cnt means TIME_WAIT (tw_id = conn_id - max_conn_cnt) */
+  uint32_t seq;         /* ntohl(tcp->seq_num) + tcp->syn                 (TcpConn.h:473) */
+  uint16_t payload_off; /* (tcp + doff*4) - eth, tcp = ip + 20            (TcpConn.h:471, Core.h:507) */
+  int16_t payload_len;  /* ip + min(tot_len,1500) - (tcp + doff*4)        (TcpConn.h:472, signed) */
+  uint16_t flags;       /* PN_F_* below */
+  uint16_t tcp_fold;    /* CSum::fold() of the reference TCP sum (Core.h:459-466); 0 <=> valid.
+                           0xFFFF when PN_F_TRUNC (segment runs past the slot). */
+} pn_result;
+
+/* flags */
+#define PN_F_IP_OK 0x0001u      /* CSum.add<20>(ip).fold() == 0            (Core.h:451-453) */
+#define PN_F_TCP_OK 0x0002u     /* pseudo-header + segment fold == 0      (Core.h:459-466) */
+#define PN_F_HIT 0x0004u        /* findConnEntry(key)->key == key          (Core.h:510, TcpServer.h:81) */
+#define PN_F_TW 0x0008u         /* hit && conn_id >= MaxConnCnt            (Core.h:510) */
+#define PN_F_FIN 0x0010u        /* TcpHeader bitfields                     (Core.h:80) */
+#define PN_F_SYN 0x0020u
+#define PN_F_RST 0x0040u
+#define PN_F_PSH 0x0080u
+#define PN_F_ACK 0x0100u
+#define PN_F_IHL_NE_5 0x0200u   /* ip->header_len != 5 (reference assumes 5: Core.h:507, TcpConn.h:469) */
+#define PN_F_RFC_IP_OK 0x0400u  /* RFC 791 header checksum over header_len*4 bytes */
+#define PN_F_RFC_TCP_OK 0x0800u /* RFC 793 checksum: TCP at ip+IHL*4, odd tail zero-padded */
+#define PN_F_NOT_TCP 0x1000u    /* ether_type != 0x0800 || ip_ver != 4 || protocol != 6
+                                   (TcpStream.h:45-46; efvitcp itself trusts the NIC filter, Core.h:375-383) */
+#define PN_F_TRUNC 0x2000u      /* ip+20+tcp_len(+pad) exceeds the slot: the reference would read past
+                                   the frame (undefined); TCP_OK/RFC_TCP_OK cleared, tcp_fold=0xFFFF */
+
+/* ---- 16-byte conn-table entry, identical layout to ConnHashEntry (Core.h:178-182) ---- */
+typedef struct pn_conn_entry {
+  uint64_t key;     /* connHashKey(), or PN_EMPTY_KEY */
+  uint32_t conn_id;
+  uint32_t _pad;
+} pn_conn_entry;
+
+/* ======================= host conn table (control plane) =======================
+ * Restates Core's ordered-linear-probe table so the host builds the exact
+ * `conn_tbl`/`tbl_mask` bytes the GPU reads.  Sizing as Core.h:235-236, initial
+ * mask as Core.h:322.  Not thread-safe (reference: single thread). */
+typedef struct pn_conn_table pn_conn_table;
+
+/* connHashKey(ip, port) with ip/port in network byte order (Core.h:167-172). */
+uint64_t pn_conn_hash_key(uint32_t ip_be, uint16_t port_be);
+
+int pn_table_create(uint32_t max_conn_cnt, uint32_t max_tw_cnt, pn_conn_table** out);
+void pn_table_destroy(pn_conn_table* t);
+/* findConnEntry (Core.h:558-562): index of the entry the probe stops at; *hit = key matched. */
+int pn_table_find(const pn_conn_table* t, uint64_t key, uint32_t* entry_idx, int* hit, uint32_t* conn_id);
+/* findConnEntry + addConnEntry + tryExpandConnTbl (Core.h:566-576, 650-682).
+ * The reference's callers only add keys that missed; PN_EINVAL if key present. */
+int pn_table_add(pn_conn_table* t, uint64_t key, uint32_t conn_id);
+/* delConnEntry (Core.h:578-605): backward-shift delete. */
+int pn_table_del(pn_conn_table* t, uint64_t key);
+/* enterTW relabel (Core.h:612-627): conn_id -> max_conn_cnt + tw_id. */
+int pn_table_set_conn_id(pn_conn_table* t, uint64_t key, uint32_t conn_id);
+/* Snapshot view: entries (TotalTableSize of them), current tbl_mask, sizing. */
+const pn_conn_entry* pn_table_entries(const pn_conn_table* t, uint32_t* n_entries, uint64_t* tbl_mask);
+uint32_t pn_table_max_conn_cnt(const pn_conn_table* t);
+uint32_t pn_table_size(const pn_conn_table* t); /* getTblSize() (Core.h:564) */
+/* How many expansions hit the reference's rehash defect (Core.h:665-669 debug
+ * exit) and were rebuilt canonically instead of losing keys. */
+uint32_t pn_table_repairs(const pn_conn_table* t);
+
+/* ======================= device context =======================
+ * One ctx per (host thread, device).  Owns the device copy of the conn table. */
+typedef struct pn_ctx pn_ctx;
+
+int pn_open(int device, pn_ctx** out);
+void pn_close(pn_ctx* ctx);
+const char* pn_last_error(const pn_ctx* ctx); /* ctx may be NULL: last global error */
+int pn_device_count(int* n);
+
+/* Snapshot the conn table into device memory (synchronous H2D, ≤160 KiB for
+ * 1024+1024 conns).  `entries` is host memory laid out as pn_conn_entry[n]. */
+int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entries, uint64_t tbl_mask,
+                      uint32_t max_conn_cnt);
+
+/* Classify n frames resident in device memory (asynchronous on `stream`).
+ *   frames_dev : base of n slots, 16-byte aligned; frame i's Ethernet header is at
+ *                frames_dev + i*slot_stride + frame_off (Core.h:503-505: slot +
+ *                sizeof(RecvBuf) + receive_prefix_len).
+ *   slot_stride: multiple of 16, >= frame_off + 96 (the header window), <= 65536.
+ *   frame_off  : even; (frame_off + 14) % 16 selects a specialised kernel.
+ *   results_dev: n pn_result records (16-byte aligned).
+ * Frame length is taken from ip->tot_len only, as the reference does (Core.h:463, TcpConn.h:472). */
+int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                void* results_dev, void* stream);
+
+/* Wait for the last stream used by this ctx. */
+int pn_sync(pn_ctx* ctx);
+
+/* HBM streaming-read calibration kernel (used by bench/profiling only): reads
+ * `bytes` (multiple of 16) from src and writes one u32 per workgroup to sink. */
+int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream);
+
+/* ======================= synthetic frame generator =======================
+ * Deterministic (seed, frame index) generator for the BASELINE configs; writes
+ * slots into host memory with bytes after each frame zero-filled.  Multi-threaded.
+ *   cfg: 2 = C2 (1514-B frames, 1 flow), 3 = C3 (64..1514-B mixed, 1024 flows,
+ *        TW + miss flows), 4 = C4 (1514-B frames over 1024 flows), 5 = C5
+ *        (IPv4 options + odd lengths + bad-checksum + adversarial cluster).
+ * first_index lets ranks generate disjoint shards of one global batch. */
+typedef struct pn_gen_params {
+  uint32_t cfg;
+  uint32_t n_flows;       /* flows with a conn entry (conn_id = flow index) */
+  uint32_t n_tw_flows;    /* of those, how many are moved to TIME_WAIT */
+  uint32_t max_conn_cnt;  /* Conf::MaxConnCnt (= MaxTimeWaitConnCnt) */
+  uint64_t seed;
+} pn_gen_params;
+
+int pn_gen_frames(const pn_gen_params* p, uint64_t first_index, uint32_t n, void* slots_host, uint32_t slot_stride,
+                  uint32_t frame_off, int n_threads);
+/* Build the conn table the generator's flows imply (add in flow order, TW relabel). */
+int pn_gen_conn_table(const pn_gen_params* p, pn_conn_table* t);
+/* Wire bytes (14 + tot_len) summed over the n generated frames (metric numerator). */
+uint64_t pn_wire_bytes(const void* slots_host, uint32_t slot_stride, uint32_t frame_off, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLLNET_AMD_H */

@@ -1,0 +1,72 @@
+/*
+ * pn_oracle.h — CPU restatement of efvitcp's RX per-frame transform.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load or call this code, and only as the
+ * checker / the timed CPU baseline — never as the product path.
+ *
+ * Parity pinning: the reference's Core.h cannot be
+ * compiled here (it needs the absent ef_vi headers <etherfabric/...> headers, and
+ * writing stand-ins for them is not allowed), so this restatement is pinned by
+ *   - RFC 1071 known answers (tests/golden/known_answers.json),
+ *   - the survey's probe of the real Core::pollNet (connHashKey of
+ *     10.0.0.2:40000 == 146235046566976; tbl_mask 4095 after 1024 inserts),
+ *   - the reference's own TcpStream.h compiled from /root/reference
+ *     (oracle/_ref, ethertype/protocol filter and IHL=5 payload split),
+ *   - real kernel-generated IPv4 headers captured on loopback.
+ * Every function cites the reference line it restates.
+ */
+#ifndef PN_ORACLE_H
+#define PN_ORACLE_H
+#include <stdint.h>
+#include "../include/pollnet_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* CSum (Core.h:89-138): u32 accumulator of host-order u16 words. */
+typedef struct orc_csum { uint32_t sum; } orc_csum;
+uint16_t orc_csum_fold(orc_csum s);                               /* Core.h:94-98 */
+void orc_csum_add16(orc_csum* s, uint16_t a);                     /* Core.h:100 */
+void orc_csum_add32(orc_csum* s, uint32_t a);                     /* Core.h:101-104 */
+void orc_csum_add_bytes(orc_csum* s, const void* p, uint32_t len); /* Core.h:106-117 (reads ceil(len/2) words) */
+
+uint64_t orc_conn_hash_key(uint32_t ip_be, uint16_t port_be); /* Core.h:167-172 */
+
+/* Ordered linear-probe conn table (Core.h:178-182, 235-236, 321-322, 558-682). */
+typedef struct orc_table {
+  pn_conn_entry* tbl;
+  uint32_t total;          /* TotalTableSize */
+  uint32_t max_table_size; /* MaxTableSize */
+  uint32_t max_conn, max_tw;
+  uint64_t mask;           /* tbl_mask */
+  uint32_t size;           /* conn_cnt + tw_cnt */
+} orc_table;
+int orc_table_init(orc_table* t, uint32_t max_conn, uint32_t max_tw);
+void orc_table_free(orc_table* t);
+uint32_t orc_table_find(const orc_table* t, uint64_t key);               /* Core.h:558-562 (bounded) */
+int orc_table_add(orc_table* t, uint64_t key, uint32_t conn_id);         /* Core.h:566-576 + 650-682 */
+int orc_table_del(orc_table* t, uint64_t key);                           /* Core.h:578-605 */
+
+/* One frame: eth points at the Ethernet header; `avail` = readable bytes from eth
+ * to the end of its slot.  Table may be described by raw entries + mask. */
+void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
+                        uint64_t mask, uint32_t max_conn, pn_result* out);
+
+/* Batch over strided slots; n_threads <= 1 runs single-threaded (pthreads otherwise). */
+void orc_classify_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                        const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
+                        pn_result* out, int n_threads);
+
+/* The reference's *release* RX path only (no checksum): parse + key + probe +
+ * onPack payload math (Core.h:503-509, TcpConn.h:469-473).  Timed as the second
+ * CPU-baseline variant.  Writes the same records with the two *_OK bits clear. */
+void orc_release_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                       const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
+                       pn_result* out, int n_threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,170 @@
+"""ctypes wrapper over oracle/liboracle.so (plain-C restatement) and oracle/_ref
+(the reference's own TcpStream.h compiled from /root/reference).
+
+TEST INFRASTRUCTURE ONLY — the checker and the timed CPU baseline ("port").
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_tcpstream.so")
+
+RESULT_DTYPE = np.dtype(
+    [("conn_id", "<u4"), ("seq", "<u4"), ("payload_off", "<u2"), ("payload_len", "<i2"), ("flags", "<u2"), ("tcp_fold", "<u2")]
+)
+ENTRY_DTYPE = np.dtype([("key", "<u8"), ("conn_id", "<u4"), ("_pad", "<u4")])
+
+_lib = C.CDLL(ORACLE_SO)
+_vp, _u32, _u64, _i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+
+
+class _Csum(C.Structure):
+    _fields_ = [("sum", _u32)]
+
+
+class _Table(C.Structure):
+    _fields_ = [("tbl", _vp), ("total", _u32), ("max_table_size", _u32), ("max_conn", _u32), ("max_tw", _u32),
+                ("mask", _u64), ("size", _u32)]
+
+
+def _sig(name, res, *args):
+    f = getattr(_lib, name)
+    f.restype, f.argtypes = res, list(args)
+    return f
+
+
+_fold = _sig("orc_csum_fold", C.c_uint16, _Csum)
+_add16 = _sig("orc_csum_add16", None, C.POINTER(_Csum), C.c_uint16)
+_add32 = _sig("orc_csum_add32", None, C.POINTER(_Csum), _u32)
+_addb = _sig("orc_csum_add_bytes", None, C.POINTER(_Csum), _vp, _u32)
+_key = _sig("orc_conn_hash_key", _u64, _u32, C.c_uint16)
+_tinit = _sig("orc_table_init", _i32, C.POINTER(_Table), _u32, _u32)
+_tfree = _sig("orc_table_free", None, C.POINTER(_Table))
+_tfind = _sig("orc_table_find", _u32, C.POINTER(_Table), _u64)
+_tadd = _sig("orc_table_add", _i32, C.POINTER(_Table), _u64, _u32)
+_tdel = _sig("orc_table_del", _i32, C.POINTER(_Table), _u64)
+_frame = _sig("orc_classify_frame", None, _vp, _u32, _vp, _u32, _u64, _u32, _vp)
+_batch = _sig("orc_classify_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
+_release = _sig("orc_release_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
+
+
+class Csum:
+    """CSum (Core.h:89-138)."""
+
+    def __init__(self, s=0):
+        self.c = _Csum(s)
+
+    def add16(self, v):
+        _add16(C.byref(self.c), v)
+
+    def add32(self, v):
+        _add32(C.byref(self.c), v)
+
+    def add_bytes(self, b: bytes, n=None):
+        buf = C.create_string_buffer(bytes(b) + b"\0\0", len(b) + 2)
+        _addb(C.byref(self.c), buf, len(b) if n is None else n)
+
+    @property
+    def sum(self):
+        return self.c.sum
+
+    def fold(self):
+        return int(_fold(self.c))
+
+
+def conn_hash_key(ip_be: int, port_be: int) -> int:
+    return int(_key(ip_be, port_be))
+
+
+class Table:
+    """Ordered linear-probe conn table restated in C (Core.h:558-682)."""
+
+    def __init__(self, max_conn, max_tw):
+        self.t = _Table()
+        assert _tinit(C.byref(self.t), max_conn, max_tw) == 0
+
+    def __del__(self):
+        _tfree(C.byref(self.t))
+
+    def find(self, key):
+        return int(_tfind(C.byref(self.t), key))
+
+    def add(self, key, cid):
+        return int(_tadd(C.byref(self.t), key, cid))
+
+    def delete(self, key):
+        return int(_tdel(C.byref(self.t), key))
+
+    def set_conn_id(self, key, cid):
+        e = self.find(key)
+        arr = self.entries(copy=False)
+        assert arr[e]["key"] == key
+        arr[e]["conn_id"] = cid
+
+    @property
+    def mask(self):
+        return int(self.t.mask)
+
+    @property
+    def size(self):
+        return int(self.t.size)
+
+    def entries(self, copy=True):
+        buf = (C.c_uint8 * (self.t.total * 16)).from_address(self.t.tbl)
+        a = np.frombuffer(buf, dtype=ENTRY_DTYPE)
+        return a.copy() if copy else a
+
+
+def classify_frame(eth: bytes, avail: int, entries: np.ndarray, mask: int, max_conn: int) -> np.void:
+    buf = C.create_string_buffer(bytes(eth).ljust(avail, b"\0"), avail)
+    out = np.zeros(1, RESULT_DTYPE)
+    ent = np.ascontiguousarray(entries, dtype=ENTRY_DTYPE)
+    _frame(buf, avail, ent.ctypes.data, len(ent), mask, max_conn, out.ctypes.data)
+    return out[0]
+
+
+def classify_batch(slots: np.ndarray, stride: int, frame_off: int, n: int, entries: np.ndarray, mask: int,
+                   max_conn: int, threads: int = 1, release: bool = False) -> np.ndarray:
+    assert slots.dtype == np.uint8 and slots.flags.c_contiguous and slots.size >= n * stride
+    ent = np.ascontiguousarray(entries, dtype=ENTRY_DTYPE)
+    out = np.zeros(n, RESULT_DTYPE)
+    fn = _release if release else _batch
+    fn(slots.ctypes.data, stride, frame_off, n, ent.ctypes.data, len(ent), mask, max_conn, out.ctypes.data, threads)
+    return out
+
+
+# ---------------- the reference itself: TcpStream.h (oracle/_ref) ----------------
+_ref = None
+
+
+def ref_available() -> bool:
+    return os.path.exists(REF_SO)
+
+
+def _ref_lib():
+    global _ref
+    if _ref is None:
+        _ref = C.CDLL(REF_SO)
+        _ref.ref_filter_packet.restype = _i32
+        _ref.ref_filter_packet.argtypes = [_vp, _u32, C.c_char_p, C.c_uint16, C.c_char_p, C.c_uint16]
+        _ref.ref_handle_packet.restype = _i32
+        _ref.ref_handle_packet.argtypes = [_vp, _u32, C.POINTER(_u32), C.POINTER(_u32)]
+    return _ref
+
+
+def ref_filter_packet(eth: bytes) -> bool:
+    b = C.create_string_buffer(bytes(eth), len(eth))
+    return bool(_ref_lib().ref_filter_packet(b, len(eth), None, 0, None, 0))
+
+
+def ref_handle_packet(eth: bytes):
+    """(payload_off, payload_len) as TcpStream::handlePacket hands them over, or None."""
+    b = C.create_string_buffer(bytes(eth), len(eth))
+    off, ln = _u32(), _u32()
+    ok = _ref_lib().ref_handle_packet(b, len(eth), C.byref(off), C.byref(ln))
+    return (off.value, ln.value) if ok else None

@@ -1,0 +1,49 @@
+// Test-only harness: compiles the reference's own TcpStream.h
+// (/root/reference/TcpStream.h, header-only, no external deps) into
+// oracle/_ref/libref_tcpstream.so so the oracle's parse rules can be checked
+// against the reference itself:
+//   - TcpStream::filterPacket (TcpStream.h:39-52): ether_type == 0x0800 (LE
+//     0x0008) && protocol == 6, 4-tuple wildcard filter;
+//   - TcpStream::handlePacket (TcpStream.h:54-142): the IHL=5 payload split
+//     header_len = 20 + doff*4 (:72-74), zero-copy payload pointer (:115).
+// Nothing here is shipped or used by the product path.
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <utility>
+
+#include "TcpStream.h"
+
+namespace {
+using Stream = TcpStream<true, (1u << 20)>;
+}
+
+extern "C" {
+
+// Wildcard filter ("0.0.0.0", port 0) unless given; returns filterPacket().
+int ref_filter_packet(const uint8_t* eth, uint32_t size, const char* src_ip, uint16_t src_port, const char* dst_ip,
+                      uint16_t dst_port) {
+  std::unique_ptr<Stream> s(new Stream());
+  s->initFilter(src_ip ? src_ip : "0.0.0.0", src_port, dst_ip ? dst_ip : "0.0.0.0", dst_port);
+  return s->filterPacket(eth, size) ? 1 : 0;
+}
+
+// First packet of a fresh stream: handlePacket() hands the whole payload to the
+// handler zero-copy.  Returns 1 and the payload offset/size the reference
+// computed, 0 if the reference dropped it (obsolete/empty or too large).
+int ref_handle_packet(const uint8_t* eth, uint32_t size, uint32_t* payload_off, uint32_t* payload_len) {
+  std::unique_ptr<Stream> s(new Stream());
+  const uint8_t* got = nullptr;
+  uint32_t got_size = 0;
+  bool ok = s->handlePacket(eth, size, [&](const uint8_t* data, uint32_t n) -> uint32_t {
+    got = data;
+    got_size = n;
+    return 0;
+  });
+  if (!ok || !got) return 0;
+  *payload_off = (uint32_t)(got - eth);
+  *payload_len = got_size;
+  return 1;
+}
+}

@@ -1,0 +1,283 @@
+"""ctypes bindings for libpollnet_amd.so (C-ABI: include/pollnet_amd.h).
+
+Names follow the reference: ``conn_hash_key`` is ``connHashKey`` (efvitcp/Core.h:167-172),
+``ConnTable.find/add/delete`` are ``findConnEntry/addConnEntry/delConnEntry``
+(Core.h:558-605), ``RxContext.classify`` is the per-frame part of ``Core::pollNet``
+(Core.h:494-552) plus ``TcpConn::onPack``'s payload split (TcpConn.h:469-473).
+Errors surface as ``PollnetError`` carrying ``pn_last_error()`` (the reference's
+``const char*`` / ``getLastError()`` convention, Core.h:253-383, Socket.h:47).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpollnet_amd.so")
+
+PN_EMPTY_KEY = 1 << 63
+PN_MISS = 0xFFFFFFFF
+PN_RECV_BUF_SIZE = 2048
+
+
+class F:
+    """pn_result.flags bits (include/pollnet_amd.h)."""
+
+    IP_OK = 0x0001
+    TCP_OK = 0x0002
+    HIT = 0x0004
+    TW = 0x0008
+    FIN = 0x0010
+    SYN = 0x0020
+    RST = 0x0040
+    PSH = 0x0080
+    ACK = 0x0100
+    IHL_NE_5 = 0x0200
+    RFC_IP_OK = 0x0400
+    RFC_TCP_OK = 0x0800
+    NOT_TCP = 0x1000
+    TRUNC = 0x2000
+
+
+RESULT_DTYPE = np.dtype(
+    [("conn_id", "<u4"), ("seq", "<u4"), ("payload_off", "<u2"), ("payload_len", "<i2"), ("flags", "<u2"), ("tcp_fold", "<u2")]
+)
+ENTRY_DTYPE = np.dtype([("key", "<u8"), ("conn_id", "<u4"), ("_pad", "<u4")])
+assert RESULT_DTYPE.itemsize == 16 and ENTRY_DTYPE.itemsize == 16
+
+
+class PollnetError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built: run `make` (or __graft_entry__.build()); there is no CPU fallback for the RX path"
+        )
+    return ctypes.CDLL(LIB_PATH)
+
+
+_lib = _load()
+_c = ctypes
+_vp, _u32, _u64, _i32, _u16 = _c.c_void_p, _c.c_uint32, _c.c_uint64, _c.c_int, _c.c_uint16
+
+
+class _GenParams(_c.Structure):
+    _fields_ = [("cfg", _u32), ("n_flows", _u32), ("n_tw_flows", _u32), ("max_conn_cnt", _u32), ("seed", _u64)]
+
+
+def _sig(name, res, *args):
+    fn = getattr(_lib, name)
+    fn.restype = res
+    fn.argtypes = list(args)
+    return fn
+
+
+_pn_conn_hash_key = _sig("pn_conn_hash_key", _u64, _u32, _u16)
+_pn_table_create = _sig("pn_table_create", _i32, _u32, _u32, _c.POINTER(_vp))
+_pn_table_destroy = _sig("pn_table_destroy", None, _vp)
+_pn_table_find = _sig("pn_table_find", _i32, _vp, _u64, _c.POINTER(_u32), _c.POINTER(_i32), _c.POINTER(_u32))
+_pn_table_add = _sig("pn_table_add", _i32, _vp, _u64, _u32)
+_pn_table_del = _sig("pn_table_del", _i32, _vp, _u64)
+_pn_table_set_conn_id = _sig("pn_table_set_conn_id", _i32, _vp, _u64, _u32)
+_pn_table_entries = _sig("pn_table_entries", _vp, _vp, _c.POINTER(_u32), _c.POINTER(_u64))
+_pn_table_max_conn_cnt = _sig("pn_table_max_conn_cnt", _u32, _vp)
+_pn_table_size = _sig("pn_table_size", _u32, _vp)
+_pn_table_repairs = _sig("pn_table_repairs", _u32, _vp)
+_pn_open = _sig("pn_open", _i32, _i32, _c.POINTER(_vp))
+_pn_close = _sig("pn_close", None, _vp)
+_pn_last_error = _sig("pn_last_error", _c.c_char_p, _vp)
+_pn_device_count = _sig("pn_device_count", _i32, _c.POINTER(_i32))
+_pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
+_pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
+_pn_sync = _sig("pn_sync", _i32, _vp)
+_pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
+_pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
+_pn_gen_conn_table = _sig("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)
+_pn_wire_bytes = _sig("pn_wire_bytes", _u64, _vp, _u32, _u32, _u32)
+
+
+def _check(rc, ctx=None, what=""):
+    if rc != 0:
+        msg = _pn_last_error(ctx).decode(errors="replace")
+        raise PollnetError(f"{what} failed ({rc}): {msg}")
+
+
+def conn_hash_key(ip_be: int, port_be: int) -> int:
+    """connHashKey(ip, port) with network-byte-order inputs (Core.h:167-172)."""
+    return int(_pn_conn_hash_key(ip_be & 0xFFFFFFFF, port_be & 0xFFFF))
+
+
+def device_count() -> int:
+    n = _i32(0)
+    _pn_device_count(_c.byref(n))
+    return n.value
+
+
+class ConnTable:
+    """Core's ordered linear-probe conn table (Core.h:178-182, 235-236, 558-682)."""
+
+    def __init__(self, max_conn_cnt: int, max_tw_cnt: int):
+        h = _vp()
+        _check(_pn_table_create(max_conn_cnt, max_tw_cnt, _c.byref(h)), None, "pn_table_create")
+        self._h = h
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _pn_table_destroy(self._h)
+            self._h = None
+
+    @property
+    def handle(self):
+        return self._h
+
+    def find(self, key: int):
+        """findConnEntry: (entry_idx, hit, conn_id or PN_MISS)."""
+        idx, hit, cid = _u32(), _i32(), _u32()
+        _check(_pn_table_find(self._h, key, _c.byref(idx), _c.byref(hit), _c.byref(cid)), None, "pn_table_find")
+        return idx.value, bool(hit.value), cid.value
+
+    def add(self, key: int, conn_id: int):
+        _check(_pn_table_add(self._h, key, conn_id), None, "pn_table_add")
+
+    def delete(self, key: int):
+        _check(_pn_table_del(self._h, key), None, "pn_table_del")
+
+    def set_conn_id(self, key: int, conn_id: int):
+        _check(_pn_table_set_conn_id(self._h, key, conn_id), None, "pn_table_set_conn_id")
+
+    @property
+    def max_conn_cnt(self) -> int:
+        return int(_pn_table_max_conn_cnt(self._h))
+
+    @property
+    def size(self) -> int:
+        return int(_pn_table_size(self._h))
+
+    @property
+    def repairs(self) -> int:
+        return int(_pn_table_repairs(self._h))
+
+    def snapshot(self):
+        """(entries as an ENTRY_DTYPE numpy copy, tbl_mask)."""
+        n, mask = _u32(), _u64()
+        p = _pn_table_entries(self._h, _c.byref(n), _c.byref(mask))
+        buf = (_c.c_uint8 * (n.value * 16)).from_address(p)
+        return np.frombuffer(bytes(buf), dtype=ENTRY_DTYPE).copy(), int(mask.value)
+
+    @property
+    def mask(self) -> int:
+        return self.snapshot()[1]
+
+
+def _ptr(x):
+    """Raw address of a torch tensor / numpy array / int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(f"cannot take the address of {type(x)}")
+
+
+def _stream_handle(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+class RxContext:
+    """A device context (pn_ctx): owns the device copy of the conn table."""
+
+    def __init__(self, device: int = 0):
+        h = _vp()
+        _check(_pn_open(device, _c.byref(h)), None, "pn_open")
+        self._h = h
+        self.device = device
+        self.max_conn_cnt = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _pn_close(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def set_conn_table(self, table: ConnTable):
+        entries, mask = table.snapshot()
+        self.set_conn_entries(entries, mask, table.max_conn_cnt)
+
+    def set_conn_entries(self, entries: np.ndarray, mask: int, max_conn_cnt: int):
+        entries = np.ascontiguousarray(entries, dtype=ENTRY_DTYPE)
+        _check(
+            _pn_set_conn_table(self._h, entries.ctypes.data, len(entries), mask, max_conn_cnt), self._h, "pn_set_conn_table"
+        )
+        self.max_conn_cnt = max_conn_cnt
+
+    def classify(self, frames_dev, slot_stride: int, frame_off: int, n: int, results_dev, stream=None):
+        """Asynchronous launch on `stream` (torch.cuda.Stream, raw handle, or None = null stream)."""
+        _check(
+            _pn_classify(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(results_dev), _stream_handle(stream)),
+            self._h,
+            "pn_classify",
+        )
+
+    def sync(self):
+        _check(_pn_sync(self._h), self._h, "pn_sync")
+
+    def calib_stream_read(self, src_dev, nbytes: int, sink_dev, stream=None):
+        _check(_pn_calib(self._h, _ptr(src_dev), nbytes, _ptr(sink_dev), _stream_handle(stream)), self._h, "pn_calib")
+
+
+@dataclass
+class GenParams:
+    cfg: int
+    n_flows: int = 1024
+    n_tw_flows: int = 0
+    max_conn_cnt: int = 1024
+    seed: int = 0
+
+    @staticmethod
+    def for_config(cfg: int) -> "GenParams":
+        """C2 1 flow; C3 1024 flows / 32 TW; C4 1024 flows; C5 1024 flows / 32 TW."""
+        seeds = {2: 0x5EED0002, 3: 0x5EED0003, 4: 0x5EED0004, 5: 0x5EED0005}
+        if cfg == 2:
+            return GenParams(2, 1, 0, 1024, seeds[2])
+        if cfg == 4:
+            return GenParams(4, 1024, 0, 1024, seeds[4])
+        return GenParams(cfg, 1024, 32, 1024, seeds[cfg])
+
+    def _c(self):
+        return _GenParams(self.cfg, self.n_flows, self.n_tw_flows, self.max_conn_cnt, self.seed)
+
+
+def gen_frames(params: GenParams, n: int, slot_stride: int = PN_RECV_BUF_SIZE, frame_off: int = 2, first_index: int = 0,
+               threads: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+    """Deterministic synthetic ring slots (n, slot_stride) uint8 in host memory."""
+    if out is None:
+        out = np.empty((n, slot_stride), dtype=np.uint8)
+    assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= n * slot_stride
+    threads = threads or min(16, os.cpu_count() or 1)
+    p = params._c()
+    _check(_pn_gen_frames(_c.byref(p), first_index, n, out.ctypes.data, slot_stride, frame_off, threads), None, "pn_gen_frames")
+    return out
+
+
+def gen_conn_table(params: GenParams, max_tw_cnt: int | None = None) -> ConnTable:
+    t = ConnTable(params.max_conn_cnt, params.max_conn_cnt if max_tw_cnt is None else max_tw_cnt)
+    p = params._c()
+    _check(_pn_gen_conn_table(_c.byref(p), t.handle), None, "pn_gen_conn_table")
+    return t
+
+
+def wire_bytes(slots: np.ndarray, slot_stride: int, frame_off: int, n: int) -> int:
+    """Σ(14 + tot_len): the metric's numerator (wire frame bytes without FCS)."""
+    return int(_pn_wire_bytes(slots.ctypes.data, slot_stride, frame_off, n))

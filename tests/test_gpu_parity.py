@@ -1,0 +1,238 @@
+"""HIP path (libpollnet_amd.so, gfx950) vs the oracle and the committed golden
+fixtures: bit-exact on every pn_result field (integer work, no tolerance)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import pollnet_amd as pa
+from oracle import pyoracle as orc
+
+from frames import FRAME_OFF, STRIDE, make_frame, to_slots
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch_cuda):
+    c = pa.RxContext(0)
+    yield c
+    c.close()
+
+
+def gpu_classify(torch, ctx, slots, stride, off, n, entries, mask, max_conn, canary=0):
+    ctx.set_conn_entries(entries, mask, max_conn)
+    frames = torch.from_numpy(np.ascontiguousarray(slots).reshape(-1)).cuda()
+    res = torch.full(((n + canary) * 16,), 0xAB, dtype=torch.uint8, device="cuda")
+    ctx.classify(frames, stride, off, n, res, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    out = res.cpu().numpy()
+    if canary:
+        assert (out[n * 16:] == 0xAB).all(), "kernel wrote past n records"
+    return out[: n * 16].view(pa.RESULT_DTYPE).copy()
+
+
+def assert_same(got, exp, names=None):
+    if np.array_equal(got, exp):
+        return
+    bad = np.nonzero(got != exp)[0]
+    i = int(bad[0])
+    nm = names[i] if names is not None else i
+    raise AssertionError(f"{len(bad)} records differ; first #{i} ({nm}): gpu={got[i]} oracle={exp[i]}")
+
+
+def test_edge_frames_bit_exact(torch_cuda, ctx, golden_dir):
+    d = np.load(os.path.join(golden_dir, "edge_frames.npz"))
+    n = len(d["expected"])
+    got = gpu_classify(torch_cuda, ctx, d["slots"], int(d["stride"]), int(d["frame_off"]), n, d["entries"], int(d["mask"]),
+                       int(d["max_conn"]), canary=17)
+    assert_same(got, d["expected"], d["names"])
+
+
+def test_loopback_frames_bit_exact(torch_cuda, ctx, golden_dir):
+    d = np.load(os.path.join(golden_dir, "loopback_frames.npz"))
+    n = len(d["lengths"])
+    ents = np.zeros(16, pa.ENTRY_DTYPE)
+    ents["key"] = pa.PN_EMPTY_KEY
+    exp = orc.classify_batch(d["slots"], int(d["stride"]), int(d["frame_off"]), n, ents, 15, 8)
+    got = gpu_classify(torch_cuda, ctx, d["slots"], int(d["stride"]), int(d["frame_off"]), n, ents, 15, 8)
+    assert_same(got, exp)
+    assert np.all(got["flags"] & pa.F.IP_OK)
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_config_slices_vs_committed(torch_cuda, ctx, golden_dir, cfg):
+    d = np.load(os.path.join(golden_dir, "config_slices.npz"))
+    p = pa.rx.GenParams.for_config(cfg)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    s = pa.gen_frames(p, 4096, STRIDE, FRAME_OFF)
+    assert hashlib.sha256(s.tobytes()).hexdigest() == str(d[f"c{cfg}_slots_sha256"])
+    got = gpu_classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, 4096, e, m, t.max_conn_cnt)
+    assert_same(got, d[f"c{cfg}_expected"])
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 5, 4])
+def test_full_size_digest(torch_cuda, ctx, golden_dir, cfg):
+    """BASELINE sizes (C2/C3/C5: 1 Mi frames; C4: one 2 Mi-frame shard of 8): the sha256
+    of the GPU's records equals the oracle's (computed when the fixtures were made),
+    plus size-independent counts."""
+    with open(os.path.join(golden_dir, "full_digests.json")) as f:
+        ref = json.load(f)[f"c{cfg}"]
+    p = pa.rx.GenParams.for_config(cfg)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = ref["n"]
+    s = pa.gen_frames(p, n, STRIDE, FRAME_OFF)
+    assert pa.wire_bytes(s, STRIDE, FRAME_OFF, n) == ref["wire_bytes"]
+    got = gpu_classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt)
+    counts = [int(((got["flags"] >> b) & 1).sum()) for b in range(14)]
+    assert counts == ref["flag_bit_counts"]
+    assert hashlib.sha256(got.tobytes()).hexdigest() == ref["records_sha256"]
+    if cfg in (2, 4):  # every 1024th frame carries a flipped payload bit
+        assert counts[1] == n - n // 1024
+
+
+@pytest.mark.parametrize("frame_off", [0, 2, 4, 6, 8, 10, 12, 14, 16, 24, 34, 38])
+def test_every_alignment_specialisation(torch_cuda, ctx, frame_off):
+    """(frame_off + 14) % 16 selects one of 8 kernel specialisations; ef_vi's layout is
+    frame_off = 10 + receive_prefix_len (Core.h:505)."""
+    p = pa.rx.GenParams.for_config(5)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = 3000
+    s = pa.gen_frames(p, n, STRIDE, frame_off)
+    exp = orc.classify_batch(s, STRIDE, frame_off, n, e, m, t.max_conn_cnt, threads=8)
+    got = gpu_classify(torch_cuda, ctx, s, STRIDE, frame_off, n, e, m, t.max_conn_cnt, canary=3)
+    assert_same(got, exp)
+
+
+@pytest.mark.parametrize("stride,frame_off", [(112, 2), (128, 2), (256, 10), (1536, 2), (4096, 2), (9216, 8), (65536, 2)])
+def test_slot_strides(torch_cuda, ctx, stride, frame_off):
+    p = pa.rx.GenParams.for_config(3)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = 700 if stride < 65536 else 64
+    s = pa.gen_frames(p, n, stride, frame_off)
+    exp = orc.classify_batch(s, stride, frame_off, n, e, m, t.max_conn_cnt)
+    got = gpu_classify(torch_cuda, ctx, s, stride, frame_off, n, e, m, t.max_conn_cnt)
+    assert_same(got, exp)
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 4099])
+def test_ragged_batch_sizes(torch_cuda, ctx, n):
+    p = pa.rx.GenParams.for_config(3)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    s = pa.gen_frames(p, n)
+    exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt)
+    got = gpu_classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, canary=65)
+    assert_same(got, exp)
+
+
+def test_empty_batch_is_noop(torch_cuda, ctx):
+    p = pa.rx.GenParams.for_config(2)
+    t = pa.gen_conn_table(p)
+    ctx.set_conn_table(t)
+    frames = torch_cuda.zeros(4096, dtype=torch_cuda.uint8, device="cuda")
+    res = torch_cuda.full((64,), 7, dtype=torch_cuda.uint8, device="cuda")
+    ctx.classify(frames, STRIDE, FRAME_OFF, 0, res)
+    torch_cuda.cuda.synchronize()
+    assert (res.cpu().numpy() == 7).all()
+
+
+def test_random_bytes_fuzz(torch_cuda, ctx):
+    """Arbitrary slot contents (garbage headers, any tot_len/IHL/doff, stale bytes after
+    the frame): the kernel must agree with the oracle on every record."""
+    rng = np.random.default_rng(1234)
+    n = 20000
+    s = rng.integers(0, 256, size=(n, STRIDE), dtype=np.uint8)
+    # make a third of them plausible IPv4/TCP so checksums and lookups see structure
+    p = pa.rx.GenParams.for_config(5)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    plaus = pa.gen_frames(p, n // 3)
+    s[: n // 3] = plaus
+    # random small tot_len on some, to land near the TRUNC/odd boundaries
+    idx = rng.integers(0, n, 3000)
+    tl = rng.integers(0, 2100, 3000).astype(np.uint16)
+    s[idx, FRAME_OFF + 16] = (tl >> 8).astype(np.uint8)
+    s[idx, FRAME_OFF + 17] = (tl & 255).astype(np.uint8)
+    exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, threads=8)
+    got = gpu_classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt)
+    assert_same(got, exp)
+
+
+def test_probe_runs_to_array_end_and_tiny_tables(torch_cuda, ctx):
+    """A run that reaches the last entry with no EmptyKey sentinel (the reference would
+    walk off the array; both sides stop at n_entries), an all-empty table, a 1-conn Conf."""
+    frames, keys = [], []
+    for j in range(40):
+        ip = f"10.7.{j}.1"
+        frames.append(make_frame(ip, 33333, payload=bytes(50)))
+        keys.append(pa.conn_hash_key(int.from_bytes(bytes([10, 7, j, 1]), "little"),
+                                     int.from_bytes((33333).to_bytes(2, "big"), "little")))
+    slots = to_slots(frames)
+    n = len(frames)
+    # same home slot for all (mask 0), sorted, filling the array to the end
+    ents = np.zeros(24, pa.ENTRY_DTYPE)
+    ks = sorted(keys)[:24]
+    ents["key"] = ks
+    ents["conn_id"] = np.arange(24)
+    for e, m, mc in ((ents, 0, 16), (ents, 7, 16)):
+        exp = orc.classify_batch(slots, STRIDE, FRAME_OFF, n, e, m, mc)
+        got = gpu_classify(torch_cuda, ctx, slots, STRIDE, FRAME_OFF, n, e, m, mc)
+        assert_same(got, exp)
+    empty = np.zeros(8, pa.ENTRY_DTYPE)
+    empty["key"] = pa.PN_EMPTY_KEY
+    got = gpu_classify(torch_cuda, ctx, slots, STRIDE, FRAME_OFF, n, empty, 7, 1)
+    assert (got["conn_id"] == pa.PN_MISS).all() and not (got["flags"] & pa.F.HIT).any()
+    tiny = pa.ConnTable(1, 1)
+    tiny.add(keys[3], 0)
+    e, m = tiny.snapshot()
+    got = gpu_classify(torch_cuda, ctx, slots, STRIDE, FRAME_OFF, n, e, m, 1)
+    assert got[3]["conn_id"] == 0 and (got["flags"] & pa.F.HIT).sum() == 1
+
+
+def test_boundary_errors(torch_cuda, ctx):
+    c = pa.RxContext(0)
+    frames = torch_cuda.zeros(8192, dtype=torch_cuda.uint8, device="cuda")
+    res = torch_cuda.zeros(64, dtype=torch_cuda.uint8, device="cuda")
+    with pytest.raises(pa.PollnetError, match="conn table"):
+        c.classify(frames, STRIDE, FRAME_OFF, 1, res)
+    c.set_conn_table(pa.gen_conn_table(pa.rx.GenParams.for_config(2)))
+    with pytest.raises(pa.PollnetError, match="aligned"):
+        c.classify(frames.data_ptr() + 2, STRIDE, FRAME_OFF, 1, res)
+    with pytest.raises(pa.PollnetError, match="layout"):
+        c.classify(frames, 100, FRAME_OFF, 1, res)
+    with pytest.raises(pa.PollnetError, match="layout"):
+        c.classify(frames, STRIDE, 3, 1, res)
+    c.close()
+
+
+def test_side_stream_and_sync(torch_cuda, ctx):
+    p = pa.rx.GenParams.for_config(3)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = 5000
+    s = pa.gen_frames(p, n)
+    exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, threads=8)
+    ctx.set_conn_entries(e, m, t.max_conn_cnt)
+    frames = torch_cuda.from_numpy(s.reshape(-1)).cuda()
+    torch_cuda.cuda.synchronize()
+    st = torch_cuda.cuda.Stream()
+    with torch_cuda.cuda.stream(st):
+        res = torch_cuda.empty(n * 16, dtype=torch_cuda.uint8, device="cuda")
+        ctx.classify(frames, STRIDE, FRAME_OFF, n, res, st)
+    ctx.sync()
+    assert_same(res.cpu().numpy().view(pa.RESULT_DTYPE), exp)
