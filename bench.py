@@ -77,7 +77,7 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s):
         passes = 0
         while True:
             orc.classify_batch(slots, STRIDE, FRAME_OFF, sample, entries, mask, max_conn, threads=fn_threads,
-                               release=release)
+                               release=release, ref_only=not release)
             passes += 1
             el = time.perf_counter() - t0
             if el >= secs:
@@ -91,8 +91,9 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s):
         "unit": "Gbit/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample} frames of the same workload (first shard slots), {p_mt} passes; "
-                  f"oracle/pn_oracle.c -O3 -march=x86-64-v3, contiguous index shards over {threads} threads",
+        "sample": f"'ref parse + checksum' (orc_refsum_batch: Core::checksum + pollNet + onPack header) over "
+                  f"{sample} frames of the same workload, {p_mt} passes; oracle/pn_oracle.c -O3 -march=x86-64-v3, "
+                  f"contiguous index shards over {threads} threads",
         "mframes_per_s": round(fr_mt / 1e6, 3),
         "single_thread": {"value": round(gb_1, 2), "unit": "Gbit/s", "mframes_per_s": round(fr_1 / 1e6, 3),
                           "cores": 1},

@@ -40,8 +40,14 @@ void orc_csum_add32(orc_csum* s, uint32_t a) {                /* Core.h:101-104 
   s->sum += a & 0xffff;
 }
 void orc_csum_add_bytes(orc_csum* s, const void* p, uint32_t len) { /* Core.h:106-117 */
+  /* The reference's loop `add(*(uint16_t*)(p + i))` keeps `sum` in a register
+   * (a uint16_t load cannot alias the uint32_t member); accumulate locally so this
+   * restatement compiles to the same vectorised loop. */
   const uint8_t* b = (const uint8_t*)p;
-  for (uint32_t i = 0; i < len; i += 2) orc_csum_add16(s, ld16(b + i)); /* odd len: reads b[len] too */
+  uint32_t sum = s->sum;
+  const uint32_t words = (uint32_t)(((uint64_t)len + 1) >> 1); /* odd len: the last word reads b[len] too */
+  for (uint32_t k = 0; k < words; k++) sum += ld16(b + 2 * (uint64_t)k);
+  s->sum = sum;
 }
 
 /* ---------------- connHashKey, Core.h:167-172 ---------------- */
@@ -146,8 +152,8 @@ int orc_table_del(orc_table* t, uint64_t key) { /* Core.h:578-605 */
 }
 
 /* ---------------- per-frame transform ---------------- */
-void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
-                        uint64_t mask, uint32_t max_conn, pn_result* out) {
+static void classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
+                           uint64_t mask, uint32_t max_conn, pn_result* out, int with_rfc) {
   const uint8_t* ip = eth + 14;  /* Core.h:506 */
   const uint8_t* tcp = ip + 20;  /* Core.h:507: IHL assumed 5 */
   uint32_t flags = 0;
@@ -193,7 +199,7 @@ void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry*
 
     /* RFC 791 / 793 verdicts (not part of the reference; C5's ihl_ne_5 companion) */
     uint32_t hl = ihl * 4;
-    if (ihl >= 5 && hl <= tot_len) {
+    if (with_rfc && ihl >= 5 && hl <= tot_len) {
       orc_csum r = {0};
       orc_csum_add_bytes(&r, ip, hl);
       if (orc_csum_fold(r) == 0) flags |= PN_F_RFC_IP_OK;
@@ -204,8 +210,7 @@ void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry*
       orc_csum_add16(&q, bswap16(6));
       orc_csum_add16(&q, bswap16((uint16_t)seg));
       const uint8_t* sp = ip + hl;
-      uint32_t i = 0;
-      for (; i + 1 < seg; i += 2) orc_csum_add16(&q, ld16(sp + i));
+      orc_csum_add_bytes(&q, sp, seg & ~1u);
       if (seg & 1) orc_csum_add16(&q, (uint16_t)sp[seg - 1]); /* zero-padded odd byte */
       if (orc_csum_fold(q) == 0) flags |= PN_F_RFC_TCP_OK;
     }
@@ -230,6 +235,11 @@ void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry*
   out->payload_len = (int16_t)(end - data_off);
   out->flags = (uint16_t)flags;
   out->tcp_fold = tcp_fold;
+}
+
+void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
+                        uint64_t mask, uint32_t max_conn, pn_result* out) {
+  classify_frame(eth, avail, tbl, n_entries, mask, max_conn, out, 1);
 }
 
 static void release_frame(const uint8_t* eth, const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask,
@@ -265,7 +275,7 @@ typedef struct job {
   uint64_t mask;
   uint32_t max_conn;
   pn_result* out;
-  int release;
+  int mode; /* 0 full (REF + RFC), 1 release path, 2 REF checksum path only */
 } job;
 
 static void* run_job(void* arg) {
@@ -273,24 +283,24 @@ static void* run_job(void* arg) {
   uint32_t avail = j->stride - j->off;
   for (uint32_t i = j->lo; i < j->hi; i++) {
     const uint8_t* eth = j->slots + (uint64_t)i * j->stride + j->off;
-    if (j->release)
+    if (j->mode == 1)
       release_frame(eth, j->tbl, j->n_entries, j->mask, j->max_conn, &j->out[i]);
     else
-      orc_classify_frame(eth, avail, j->tbl, j->n_entries, j->mask, j->max_conn, &j->out[i]);
+      classify_frame(eth, avail, j->tbl, j->n_entries, j->mask, j->max_conn, &j->out[i], j->mode == 0);
   }
   return NULL;
 }
 
 static void run_batch(const uint8_t* slots, uint32_t stride, uint32_t off, uint32_t n, const pn_conn_entry* tbl,
                       uint32_t n_entries, uint64_t mask, uint32_t max_conn, pn_result* out, int n_threads,
-                      int release) {
+                      int mode) {
   if (n_threads < 1) n_threads = 1;
   if (n_threads > 256) n_threads = 256;
   job jobs[256];
   pthread_t th[256];
   for (int k = 0; k < n_threads; k++) { /* contiguous index shards */
     jobs[k] = (job){slots, stride, off, (uint32_t)((uint64_t)n * k / n_threads),
-                    (uint32_t)((uint64_t)n * (k + 1) / n_threads), tbl, n_entries, mask, max_conn, out, release};
+                    (uint32_t)((uint64_t)n * (k + 1) / n_threads), tbl, n_entries, mask, max_conn, out, mode};
   }
   if (n_threads == 1) {
     run_job(&jobs[0]);
@@ -310,4 +320,10 @@ void orc_release_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t fram
                        const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
                        pn_result* out, int n_threads) {
   run_batch(slots, slot_stride, frame_off, n, tbl, n_entries, mask, max_conn, out, n_threads, 1);
+}
+
+void orc_refsum_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                      const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
+                      pn_result* out, int n_threads) {
+  run_batch(slots, slot_stride, frame_off, n, tbl, n_entries, mask, max_conn, out, n_threads, 2);
 }

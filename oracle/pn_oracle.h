@@ -66,6 +66,13 @@ void orc_release_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t fram
                        const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
                        pn_result* out, int n_threads);
 
+/* "ref parse + checksum": exactly the reference's work (Core::checksum + pollNet +
+ * onPack header) without this oracle's RFC extras; RFC bits left clear.  Timed as
+ * the primary CPU baseline. */
+void orc_refsum_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                      const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
+                      pn_result* out, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,7 @@ _tdel = _sig("orc_table_del", _i32, C.POINTER(_Table), _u64)
 _frame = _sig("orc_classify_frame", None, _vp, _u32, _vp, _u32, _u64, _u32, _vp)
 _batch = _sig("orc_classify_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 _release = _sig("orc_release_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
+_refsum = _sig("orc_refsum_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 
 
 class Csum:
@@ -129,11 +130,11 @@ def classify_frame(eth: bytes, avail: int, entries: np.ndarray, mask: int, max_c
 
 
 def classify_batch(slots: np.ndarray, stride: int, frame_off: int, n: int, entries: np.ndarray, mask: int,
-                   max_conn: int, threads: int = 1, release: bool = False) -> np.ndarray:
+                   max_conn: int, threads: int = 1, release: bool = False, ref_only: bool = False) -> np.ndarray:
     assert slots.dtype == np.uint8 and slots.flags.c_contiguous and slots.size >= n * stride
     ent = np.ascontiguousarray(entries, dtype=ENTRY_DTYPE)
     out = np.zeros(n, RESULT_DTYPE)
-    fn = _release if release else _batch
+    fn = _release if release else (_refsum if ref_only else _batch)
     fn(slots.ctypes.data, stride, frame_off, n, ent.ctypes.data, len(ent), mask, max_conn, out.ctypes.data, threads)
     return out
 

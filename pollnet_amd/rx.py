@@ -53,6 +53,14 @@ class PollnetError(RuntimeError):
 
 
 def _load():
+    # One HIP runtime per process: torch ships its own libamdhip64 with the same
+    # SONAME (libamdhip64.so.7) as /opt/rocm's.  Loading torch first makes our
+    # library bind to that already-loaded copy; the other order puts two HSA
+    # runtimes in the process and the second one finds no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # C++/ctypes users without torch get /opt/rocm's runtime
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} not built: run `make` (or __graft_entry__.build()); there is no CPU fallback for the RX path"

@@ -201,7 +201,7 @@ def test_probe_runs_to_array_end_and_tiny_tables(torch_cuda, ctx):
     tiny.add(keys[3], 0)
     e, m = tiny.snapshot()
     got = gpu_classify(torch_cuda, ctx, slots, STRIDE, FRAME_OFF, n, e, m, 1)
-    assert got[3]["conn_id"] == 0 and (got["flags"] & pa.F.HIT).sum() == 1
+    assert got[3]["conn_id"] == 0 and np.count_nonzero(got["flags"] & pa.F.HIT) == 1
 
 
 def test_boundary_errors(torch_cuda, ctx):
