@@ -7,11 +7,14 @@
 // Core.h:89-138 (CSum), TcpConn.h:469-473 (payload arithmetic).
 //
 // Execution model (one wavefront = 64 frames, no inter-wave communication):
-//  phase 1  lane f owns frame f: loads the 64-80 B header window straight to
-//           VGPRs, decodes fields at compile-time offsets (kernel specialised on
-//           (frame_off+14)%16), computes the 20-byte IP sum, connHashKey and the
-//           ordered probe of the (L2-resident) conn table.
-//  phase 2  the wave streams each frame's bytes [ip, ip+20+tcp_len(+pad)) with
+//  phase 1  lane f owns frame f: loads a 112-B header window straight to VGPRs
+//           (ending on the slot's first 128-B line for the default layout),
+//           decodes fields at compile-time offsets (kernel specialised on
+//           (frame_off+14)%16), computes the 20-byte IP sum, the sum of the
+//           frame's words inside the window, connHashKey and the ordered probe
+//           of the (L2-resident) conn table.
+//  phase 2  the wave streams the rest of each frame's summed region
+//           [ip, ip+20+tcp_len(+pad)) from the window end on, with
 //           1 KiB buffer_load_dwordx4 instructions (64 lanes x 16 B), summing
 //           u16 halves with v_dot2_u32_u16 (exact integer sums, no folding),
 //           8 frames per batch, reduced across lanes with permlane32/16 swaps
@@ -127,29 +130,39 @@ __device__ __forceinline__ uint32_t tail_sel(int end, int o) {
 
 template <int MIS>
 __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a) {
-  constexpr int NCH = (MIS + 64 + 15) / 16; // header window chunks: ip .. ip+64
+  // Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
+  // header.  112 B ends on the slot's first 128-B line boundary for the default
+  // layout (ip at slot+16), so the wave-wide stream below starts on a fresh line
+  // and no line is fetched twice.
+  constexpr int kWinChunks = 7;
+  constexpr int kWinBytes = 16 * kWinChunks;
+  static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wave_base = (blockIdx.x * kWavesPerWG + wave) * kFramesPerWave;
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
   const bool live = f < a.n;
+  const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
+  const uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
 
-  // ---------------- phase 1: header lane ----------------
-  Win<4 * NCH> h;
+  // ---------------- phase 1: header lane (lane f <-> frame f) ----------------
+  // One wave-uniform descriptor over the wave's slots; lanes past n read zeros.
+  Win<4 * kWinChunks> h;
   uint32_t ether_type;
   {
-    const uint8_t* ipa = a.frames + (uint64_t)(live ? f : wave_base) * a.stride + a.ipa_off;
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
+    const uint32_t lo = (uint32_t)lane * a.stride + a.ipa_off;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(ipa + 16 * c);
+    for (int c = 0; c < kWinChunks; ++c) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + 16 * c, 0, 0);
       h.d[4 * c + 0] = v.x;
       h.d[4 * c + 1] = v.y;
       h.d[4 * c + 2] = v.z;
       h.d[4 * c + 3] = v.w;
     }
     if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
-    else ether_type = *reinterpret_cast<const uint16_t*>(ipa - 2);
+    else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, 0) >> 16; // ipa_off >= 16 here
   }
   // IpHeader (Core.h:57-69), fields relative to ip = window + MIS
   const uint32_t ver_ihl = h.template b8<MIS + 0>();
@@ -181,8 +194,17 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
   const uint32_t seg_even = (tcp_len + 1) & ~1u;
   const bool trunc = 34 + seg_even > a.avail;
   if (trunc) flags |= PN_F_TRUNC;
-  // streamed region relative to the window: [MIS, MIS + 20 + seg_even)
+  // summed region relative to the window: [MIS, MIS + 20 + seg_even)
   const int end_rel = (live && !trunc) ? (int)(MIS + 20 + seg_even) : 0;
+
+  // the part of the region inside the window, summed by this lane from registers
+  uint32_t t_all = 0;
+#pragma unroll
+  for (int q = MIS / 4; q < 4 * kWinChunks; ++q) {
+    const uint32_t start_sel = ((4 * q >= MIS) ? 1u : 0u) | ((4 * q + 2 >= MIS) ? 0x10000u : 0u);
+    const uint32_t sel = tail_sel(end_rel, 4 * q) & start_sel;
+    t_all = dot2(h.d[q], sel, t_all);
+  }
 
   // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded
   uint32_t conn_id = PN_MISS;
@@ -207,10 +229,8 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
     }
   }
 
-  // ---------------- phase 2: streamed segment sums ----------------
-  uint32_t t_all = 0;
-  const uint8_t* wave_ipa = a.frames + (uint64_t)wave_base * a.stride + a.ipa_off;
-  const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
+  // ---------------- phase 2: the rest of each frame, streamed by the wave ----------------
+  const uint8_t* wave_ipa = wave_slot + a.ipa_off;
   for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
     uint32_t acc[kBatch];
     int ends[kBatch];
@@ -224,41 +244,35 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
       const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_ipa + (uint64_t)fi * a.stride, end16);
       // out-of-range chunks of a buffer load return 0 and fetch nothing
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
       const int end = ends[j];
       const u32x4 w0 = w0s[j], w1 = w1s[j];
+      const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
       uint32_t s = 0;
-      const int o0 = lane * 16, o1 = 1024 + lane * 16;
-      uint32_t m0 = tail_sel(end, o0), m1 = tail_sel(end, o0 + 4), m2 = tail_sel(end, o0 + 8), m3 = tail_sel(end, o0 + 12);
-      if constexpr (MIS != 0) {
-        // halves of chunk 0 below the IP header are not part of the sum
-        if (lane == 0) {
-          constexpr uint32_t sm[4] = {
-              (0 >= MIS ? 1u : 0u) | (2 >= MIS ? 0x10000u : 0u), (4 >= MIS ? 1u : 0u) | (6 >= MIS ? 0x10000u : 0u),
-              (8 >= MIS ? 1u : 0u) | (10 >= MIS ? 0x10000u : 0u), (12 >= MIS ? 1u : 0u) | (14 >= MIS ? 0x10000u : 0u)};
-          m0 &= sm[0];
-          m1 &= sm[1];
-          m2 &= sm[2];
-          m3 &= sm[3];
-        }
-      }
-      s = dot2(w0.x, m0, s);
-      s = dot2(w0.y, m1, s);
-      s = dot2(w0.z, m2, s);
-      s = dot2(w0.w, m3, s);
+      s = dot2(w0.x, tail_sel(end, o0), s);
+      s = dot2(w0.y, tail_sel(end, o0 + 4), s);
+      s = dot2(w0.z, tail_sel(end, o0 + 8), s);
+      s = dot2(w0.w, tail_sel(end, o0 + 12), s);
       s = dot2(w1.x, tail_sel(end, o1), s);
       s = dot2(w1.y, tail_sel(end, o1 + 4), s);
       s = dot2(w1.z, tail_sel(end, o1 + 8), s);
       s = dot2(w1.w, tail_sel(end, o1 + 12), s);
-      if (end > 2048) { // jumbo slots only (slot_stride > 2048): remaining KiBs, wave-uniform
+      acc[j] = s;
+    }
+    // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int end = ends[j];
+      if (end > kWinBytes + 2048) {
         const __amdgpu_buffer_rsrc_t rs =
             frame_rsrc(wave_ipa + (uint64_t)(b0 + j) * a.stride, (uint32_t)(end + 15) & ~15u);
-        for (int kb = 2048; kb < end; kb += 1024) {
+        uint32_t s = acc[j];
+        for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
           const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, 0);
           const int o = kb + lane * 16;
           s = dot2(w.x, tail_sel(end, o), s);
@@ -266,8 +280,8 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
           s = dot2(w.z, tail_sel(end, o + 8), s);
           s = dot2(w.w, tail_sel(end, o + 12), s);
         }
+        acc[j] = s;
       }
-      acc[j] = s;
     }
     // transpose-reduce 8 frames x 64 lanes -> lane l holds frame (l>>3)&7
 #pragma unroll
@@ -291,7 +305,7 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
     v += dpp<0x4E>(v);  // quad_perm [2,3,0,1]  -> lane ^ 2
     v += dpp<0x141>(v); // row_half_mirror      -> other quad of the 8
     const uint32_t tot = __shfl(v, (lane & 7) * 8);
-    if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all = tot;
+    if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
   }
 
   // ---------------- phase 3: finish on the frame's lane ----------------
