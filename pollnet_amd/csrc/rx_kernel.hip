@@ -128,8 +128,14 @@ __device__ __forceinline__ uint32_t tail_sel(int end, int o) {
   return (uint32_t)((t >> 1) + (t >> 2) * 0xffff);
 }
 
-template <int MIS>
-__global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a) {
+// WIN: 0 = each header lane loads its own 112-B window (7 x 16 B, one line per
+// lane per instruction); 1 = the same with the first chunk waited for before the
+// rest (diagnostic); 2 = the wave loads each slot's first 128-B line with 8 lanes
+// per line (one request per line) into an XOR-swizzled LDS tile the header lanes
+// read back (needs 128-B aligned slots and ip at line offset 16..31).
+template <int MIS, int BATCH = kBatch, int WPG = kWavesPerWG, int WIN = 0>
+__global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
+  static_assert(BATCH == 4 || BATCH == 8, "lane-transpose reduction is written for 4 or 8 frames");
   // Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
   // header.  112 B ends on the slot's first 128-B line boundary for the default
   // layout (ip at slot+16), so the wave-wide stream below starts on a fresh line
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
   static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave_base = (blockIdx.x * kWavesPerWG + wave) * kFramesPerWave;
+  const uint32_t wave_base = (blockIdx.x * WPG + wave) * kFramesPerWave;
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
   const bool live = f < a.n;
@@ -150,7 +156,31 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
   // One wave-uniform descriptor over the wave's slots; lanes past n read zeros.
   Win<4 * kWinChunks> h;
   uint32_t ether_type;
-  {
+  if constexpr (WIN == 2) {
+    static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
+    __shared__ u32x4 tile[WPG][kFramesPerWave * 8]; // 8 KiB per wave: 64 slots x 128 B
+    u32x4* t = tile[wave];
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
+    const uint32_t line0 = a.ipa_off & ~127u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + line0 + 16 * part, 0, 0);
+      t[r * 8 + (part ^ (r & 7))] = v;
+    }
+    const uint32_t p0 = (a.ipa_off & 127u) >> 4; // == 1 on this path
+#pragma unroll
+    for (int c = 0; c < kWinChunks; ++c) {
+      const u32x4 v = t[lane * 8 + ((p0 + c) ^ (lane & 7))];
+      h.d[4 * c + 0] = v.x;
+      h.d[4 * c + 1] = v.y;
+      h.d[4 * c + 2] = v.z;
+      h.d[4 * c + 3] = v.w;
+    }
+    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+    else ether_type = t[lane * 8 + ((p0 - 1) ^ (lane & 7))].w >> 16;
+  } else {
+    // One wave-uniform descriptor over the wave's slots; lanes past n read zeros.
     const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
     const uint32_t lo = (uint32_t)lane * a.stride + a.ipa_off;
 #pragma unroll
@@ -160,6 +190,9 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
       h.d[4 * c + 1] = v.y;
       h.d[4 * c + 2] = v.z;
       h.d[4 * c + 3] = v.w;
+      if constexpr (WIN == 1) {
+        if (c == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // first chunk lands before the rest issue
+      }
     }
     if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
     else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, 0) >> 16; // ipa_off >= 16 here
@@ -231,13 +264,13 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
 
   // ---------------- phase 2: the rest of each frame, streamed by the wave ----------------
   const uint8_t* wave_ipa = wave_slot + a.ipa_off;
-  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
-    uint32_t acc[kBatch];
-    int ends[kBatch];
-    u32x4 w0s[kBatch], w1s[kBatch];
-    // issue all 2*kBatch loads of the batch before consuming any of them
+  for (uint32_t b0 = 0; b0 < n_here; b0 += BATCH) {
+    uint32_t acc[BATCH];
+    int ends[BATCH];
+    u32x4 w0s[BATCH], w1s[BATCH];
+    // issue all 2*BATCH loads of the batch before consuming any of them
 #pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
+    for (int j = 0; j < BATCH; ++j) {
       const uint32_t fi = b0 + j; // wave-uniform
       const int end = __builtin_amdgcn_readlane(end_rel, fi & 63);
       ends[j] = end;
@@ -249,7 +282,7 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
 #pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
+    for (int j = 0; j < BATCH; ++j) {
       const int end = ends[j];
       const u32x4 w0 = w0s[j], w1 = w1s[j];
       const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
@@ -266,7 +299,7 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
     }
     // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
 #pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
+    for (int j = 0; j < BATCH; ++j) {
       const int end = ends[j];
       if (end > kWinBytes + 2048) {
         const __amdgpu_buffer_rsrc_t rs =
@@ -283,29 +316,43 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
         acc[j] = s;
       }
     }
-    // transpose-reduce 8 frames x 64 lanes -> lane l holds frame (l>>3)&7
+    // transpose-reduce BATCH frames x 64 lanes -> one total per lane group
+    uint32_t v;
+    if constexpr (BATCH == 8) { // lane l ends with frame (l>>3)&7
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { // xor 32
-      const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
-      acc[i] = r[0] + r[1];
-    }
+      for (int i = 0; i < 4; ++i) { // xor 32
+        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
+        acc[i] = r[0] + r[1];
+      }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) { // xor 16
-      const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
-      acc[i] = r[0] + r[1];
-    }
-    { // xor 8: keep one, send the other
-      const bool b3 = lane & 8;
+      for (int i = 0; i < 2; ++i) { // xor 16
+        const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
+        acc[i] = r[0] + r[1];
+      }
+      const bool b3 = lane & 8; // xor 8: keep one, send the other
       const uint32_t keep = b3 ? acc[1] : acc[0];
       const uint32_t send = b3 ? acc[0] : acc[1];
-      acc[0] = keep + dpp<0x128>(send); // row_ror:8 -> lane ^ 8
+      v = keep + dpp<0x128>(send); // row_ror:8 -> lane ^ 8
+      v += dpp<0xB1>(v);           // quad_perm [1,0,3,2]  -> lane ^ 1
+      v += dpp<0x4E>(v);           // quad_perm [2,3,0,1]  -> lane ^ 2
+      v += dpp<0x141>(v);          // row_half_mirror      -> other quad of the 8
+      const uint32_t tot = __shfl(v, (lane & 7) * 8);
+      if ((uint32_t)(lane >> 3) == b0 / 8) t_all += tot;
+    } else { // BATCH == 4: lane l ends with frame (l>>4)&3
+#pragma unroll
+      for (int i = 0; i < 2; ++i) { // xor 32
+        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 2], false, false);
+        acc[i] = r[0] + r[1];
+      }
+      const auto r = __builtin_amdgcn_permlane16_swap(acc[0], acc[1], false, false); // xor 16
+      v = r[0] + r[1];
+      v += dpp<0xB1>(v);  // lane ^ 1
+      v += dpp<0x4E>(v);  // lane ^ 2
+      v += dpp<0x141>(v); // other quad of the 8
+      v += dpp<0x128>(v); // row_ror:8 -> other 8 of the 16
+      const uint32_t tot = __shfl(v, (lane & 3) * 16);
+      if ((uint32_t)(lane >> 2) == b0 / 4) t_all += tot;
     }
-    uint32_t v = acc[0];
-    v += dpp<0xB1>(v);  // quad_perm [1,0,3,2]  -> lane ^ 1
-    v += dpp<0x4E>(v);  // quad_perm [2,3,0,1]  -> lane ^ 2
-    v += dpp<0x141>(v); // row_half_mirror      -> other quad of the 8
-    const uint32_t tot = __shfl(v, (lane & 7) * 8);
-    if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
   }
 
   // ---------------- phase 3: finish on the frame's lane ----------------
@@ -340,6 +387,7 @@ __global__ __launch_bounds__(kWave* kWavesPerWG) void rx_classify_kernel(KArgs a
 }
 
 __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src, uint64_t n16, uint32_t* sink) {
+  // the whole grid sweeps the buffer front to back, one 16-B coalesced load per lane per step
   uint32_t acc = 0;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
     const u32x4 v = src[i];
@@ -376,7 +424,16 @@ int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
 
 template <int MIS>
 void launch(const KArgs& a, uint32_t grid, hipStream_t s) {
-  hipLaunchKernelGGL(rx_classify_kernel<MIS>, dim3(grid), dim3(kWave * kWavesPerWG), 0, s, a);
+  hipLaunchKernelGGL((rx_classify_kernel<MIS>), dim3(grid), dim3(kWave * kWavesPerWG), 0, s, a);
+}
+
+// Tuning variants of the MIS=0 (default layout) kernel, A/B-timed in one process by
+// scripts/variants.py.  Not part of the public ABI.
+template <int BATCH, int WPG, int WIN = 0>
+void launch_variant(const KArgs& a, hipStream_t s) {
+  const uint32_t per_wg = kFramesPerWave * WPG;
+  hipLaunchKernelGGL((rx_classify_kernel<0, BATCH, WPG, WIN>), dim3((a.n + per_wg - 1) / per_wg), dim3(kWave * WPG), 0,
+                     s, a);
 }
 } // namespace
 
@@ -475,6 +532,41 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                        void* results_dev, void* stream, int variant) {
+  if (!ctx || !ctx->tbl_dev || (frame_off + 14) % 16 != 0 || n == 0) return set_err(ctx, PN_EINVAL, "variant: bad args");
+  if (variant >= 7 && (((frame_off + 14) & 127) >> 4) != 1) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
+  KArgs a;
+  a.frames = (const uint8_t*)frames_dev;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.avail = slot_stride - frame_off;
+  hipStream_t s = (hipStream_t)stream;
+  switch (variant) {
+    case 0: launch_variant<8, 4>(a, s); break;
+    case 1: launch_variant<4, 4>(a, s); break;
+    case 2: launch_variant<8, 1>(a, s); break;
+    case 3: launch_variant<4, 1>(a, s); break;
+    case 4: launch_variant<8, 2>(a, s); break;
+    case 5: launch_variant<4, 2>(a, s); break;
+    case 6: launch_variant<8, 4, 1>(a, s); break;
+    case 7: launch_variant<8, 4, 2>(a, s); break;
+    case 8: launch_variant<8, 1, 2>(a, s); break;
+    case 9: launch_variant<8, 2, 2>(a, s); break;
+    default: return set_err(ctx, PN_EINVAL, "variant: unknown");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "variant launch");
   ctx->last_stream = s;
   return PN_OK;
 }

@@ -103,6 +103,7 @@ _pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
 _pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
+_pn_variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
 _pn_gen_conn_table = _sig("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)
 _pn_wire_bytes = _sig("pn_wire_bytes", _u64, _vp, _u32, _u32, _u32)
@@ -237,6 +238,11 @@ class RxContext:
             self._h,
             "pn_classify",
         )
+
+    def classify_variant(self, frames_dev, slot_stride, frame_off, n, results_dev, stream, variant):
+        """Tuning-only kernel shapes (scripts/variants.py); not part of the C header."""
+        _check(_pn_variant(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(results_dev),
+                           _stream_handle(stream), variant), self._h, "pn_classify_variant")
 
     def sync(self):
         _check(_pn_sync(self._h), self._h, "pn_sync")

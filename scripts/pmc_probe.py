@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variant", type=int, default=-1, help="tuning variant instead of the production kernel")
     a = ap.parse_args()
     import torch
 
@@ -35,7 +36,10 @@ def main():
     st = torch.cuda.current_stream()
     for _ in range(a.reps):
         ctx.calib_stream_read(frames, frames.numel(), sink, st)
-        ctx.classify(frames, 2048, 2, a.frames, res, st)
+        if a.variant < 0:
+            ctx.classify(frames, 2048, 2, a.frames, res, st)
+        else:
+            ctx.classify_variant(frames, 2048, 2, a.frames, res, st, a.variant)
     torch.cuda.synchronize()
     print(f"calib_bytes={frames.numel()} wire_bytes={pa.wire_bytes(s, 2048, 2, a.frames)} frames={a.frames}")
 

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""A/B kernel shapes in ONE process, interleaved rounds (guide §5.4 rule 24).
+Every variant's records must equal the production kernel's bit for bit."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+NAMES = {0: "batch8_wpg4", 1: "batch4_wpg4", 2: "batch8_wpg1", 3: "batch4_wpg1", 4: "batch8_wpg2", 5: "batch4_wpg2",
+         6: "serialwin_b8_wpg4", 7: "coopwin_b8_wpg4", 8: "coopwin_b8_wpg1", 9: "coopwin_b8_wpg2"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=15)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="0,2,4,6,7,8,9")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+
+    import pollnet_amd as pa
+
+    p = pa.rx.GenParams.for_config(a.config)
+    s = pa.gen_frames(p, a.frames)
+    t = pa.gen_conn_table(p)
+    wire = pa.wire_bytes(s, 2048, 2, a.frames)
+    ctx = pa.RxContext(0)
+    ctx.set_conn_table(t)
+    frames = torch.from_numpy(s.reshape(-1)).cuda()
+    ref = torch.empty(a.frames * 16, dtype=torch.uint8, device="cuda")
+    res = torch.empty_like(ref)
+    sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    ctx.classify(frames, 2048, 2, a.frames, ref, st)
+    vs = [int(x) for x in a.variants.split(",")]
+    for v in vs:
+        res.zero_()
+        ctx.classify_variant(frames, 2048, 2, a.frames, res, st, v)
+        torch.cuda.synchronize()
+        assert torch.equal(res, ref), f"variant {v} differs from production"
+    times = {v: [] for v in vs}
+    times["calib"] = []
+    times["prod"] = []
+    times["prod_b2b50"] = []
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        ev[0].record(st)
+        for _ in range(a.reps):
+            fn()
+        ev[1].record(st)
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) / a.reps
+
+    for _ in range(a.rounds):
+        times["calib"].append(timed(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, st)))
+        times["prod"].append(timed(lambda: ctx.classify(frames, 2048, 2, a.frames, res, st)))
+        r0 = a.reps
+        a.reps = 50
+        times["prod_b2b50"].append(timed(lambda: ctx.classify(frames, 2048, 2, a.frames, res, st)))
+        a.reps = r0
+        for v in vs:
+            times[v].append(timed(lambda: ctx.classify_variant(frames, 2048, 2, a.frames, res, st, v)))
+    algo = wire + 16 * a.frames
+    out = {"config": a.config, "frames": a.frames,
+           "calib_stream_read_tbps": round(frames.numel() / (statistics.median(times["calib"]) * 1e-3) / 1e12, 3)}
+    for k, ts in times.items():
+        if k == "calib":
+            continue
+        med = statistics.median(ts)
+        out[NAMES.get(k, k)] = {"ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+                               "algo_tbps": round(algo / (med * 1e-3) / 1e12, 3)}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
