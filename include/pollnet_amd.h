@@ -145,6 +145,10 @@ int pn_sync(pn_ctx* ctx);
 /* HBM streaming-read calibration kernel (used by bench/profiling only): reads
  * `bytes` (multiple of 16) from src and writes one u32 per workgroup to sink. */
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream);
+/* Read-only ceiling for a slot layout: the first `bytes` (<= 2048) of each of n_slots
+ * slots, read with the RX kernel's own load pattern and no arithmetic. */
+int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
+                       int waves_per_wg, void* sink_dev, void* stream);
 
 /* ======================= synthetic frame generator =======================
  * Deterministic (seed, frame index) generator for the BASELINE configs; writes

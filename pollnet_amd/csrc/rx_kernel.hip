@@ -34,7 +34,7 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerWG = 4;
+constexpr int kWavesPerWG = 1; // 64-thread workgroups: +3% over 4 waves/WG (scripts/variants.py, profiles/)
 constexpr int kFramesPerWave = 64;
 constexpr int kBatch = 8;
 
@@ -396,6 +396,34 @@ __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src
   if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc; // keeps the loads live; practically never stores
 }
 
+// Read-only ceiling for the slot layout: each wave reads the first `bytes` of each of
+// its 64 slots with the same 1-KiB buffer loads and batching as phase 2 (no
+// header, no arithmetic).  Bounds what the RX kernel can reach on this layout.
+template <int WPG>
+__global__ __launch_bounds__(kWave* WPG) void calib_slot_read_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                                    uint32_t bytes, uint32_t* sink) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave_base = (blockIdx.x * WPG + wave) * kFramesPerWave;
+  if (wave_base >= n) return;
+  const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+  uint32_t acc = 0;
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    u32x4 w0s[kBatch], w1s[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const uint32_t nb = (b0 + j < n_here) ? bytes : 0u;
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(base + (uint64_t)(wave_base + b0 + j) * stride, nb);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+  }
+  if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+}
+
 } // namespace
 
 // ============================ C-ABI ============================
@@ -567,6 +595,24 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "variant launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
+                       int waves_per_wg, void* sink_dev, void* stream) {
+  if (!ctx || !src_dev || !sink_dev || (stride & 15) || bytes > stride || bytes > 2048 || n_slots == 0)
+    return set_err(ctx, PN_EINVAL, "pn_calib_slot_read: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t waves = (n_slots + kFramesPerWave - 1) / kFramesPerWave;
+  if (waves_per_wg == 1)
+    hipLaunchKernelGGL((calib_slot_read_kernel<1>), dim3(waves), dim3(64), 0, s, (const uint8_t*)src_dev, n_slots, stride,
+                       bytes, (uint32_t*)sink_dev);
+  else
+    hipLaunchKernelGGL((calib_slot_read_kernel<4>), dim3((waves + 3) / 4), dim3(256), 0, s, (const uint8_t*)src_dev,
+                       n_slots, stride, bytes, (uint32_t*)sink_dev);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "calib slot launch");
   ctx->last_stream = s;
   return PN_OK;
 }

@@ -103,6 +103,7 @@ _pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
 _pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
+_pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
 _pn_variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
 _pn_gen_conn_table = _sig("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)
@@ -238,6 +239,10 @@ class RxContext:
             self._h,
             "pn_classify",
         )
+
+    def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, waves_per_wg=1):
+        _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, waves_per_wg, _ptr(sink_dev),
+                              _stream_handle(stream)), self._h, "pn_calib_slot_read")
 
     def classify_variant(self, frames_dev, slot_stride, frame_off, n, results_dev, stream, variant):
         """Tuning-only kernel shapes (scripts/variants.py); not part of the C header."""

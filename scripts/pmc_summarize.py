@@ -34,6 +34,22 @@ def load(dirpath, counter):
     return calib, cls
 
 
+def load_ea(dirpath):
+    """Median per classify dispatch of every counter found under dirpath."""
+    rows = []
+    for f in glob.glob(os.path.join(dirpath, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            rows += list(csv.DictReader(fh))
+    per = {}
+    for r in rows:
+        if "rx_classify" not in r.get("Kernel_Name", ""):
+            continue
+        did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        per.setdefault(r["Counter_Name"], {}).setdefault(did, 0.0)
+        per[r["Counter_Name"]][did] += float(r["Counter_Value"])
+    return {k: statistics.median(v.values()) for k, v in per.items()}
+
+
 def main():
     fdir, wdir, calib_bytes, wire, frames, key = sys.argv[1:7]
     out = sys.argv[7] if len(sys.argv) > 7 else "profiles/pmc_traffic.json"
@@ -60,6 +76,19 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH scaled by a "
                   "same-run 16-B streaming-read calibration kernel over a known byte count",
     }
+    base = os.path.dirname(os.path.normpath(fdir))
+    ea = {}
+    for sub in ("ea", "eaw"):
+        if os.path.isdir(os.path.join(base, sub)):
+            ea.update(load_ea(os.path.join(base, sub)))
+    if ea:
+        rd = 32 * ea.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * ea.get("TCC_EA0_RDREQ_64B_sum", 0) + \
+            128 * ea.get("TCC_EA0_RDREQ_128B_sum", 0)
+        wr64 = ea.get("TCC_EA0_WRREQ_64B_sum", 0)
+        wr = 64 * wr64 + 32 * (ea.get("TCC_EA0_WRREQ_sum", wr64) - wr64)
+        entry["ea_request_counters"] = {k: ea[k] for k in sorted(ea)}
+        entry["ea_bytes_per_launch"] = int(rd + wr)
+        entry["ea_read_lines_per_frame"] = round(ea.get("TCC_EA0_RDREQ_128B_sum", 0) / frames, 4)
     d = {}
     if os.path.exists(out):
         with open(out) as f:

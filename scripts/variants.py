@@ -47,6 +47,9 @@ def main():
         assert torch.equal(res, ref), f"variant {v} differs from production"
     times = {v: [] for v in vs}
     times["calib"] = []
+    for b in (1536, 2048):
+        for wpg in (1, 4):
+            times[f"slotread_{b}_wpg{wpg}"] = []
     times["prod"] = []
     times["prod_b2b50"] = []
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -63,6 +66,10 @@ def main():
 
     for _ in range(a.rounds):
         times["calib"].append(timed(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, st)))
+        for b in (1536, 2048):
+            for wpg in (1, 4):
+                times[f"slotread_{b}_wpg{wpg}"].append(
+                    timed(lambda: ctx.calib_slot_read(frames, a.frames, 2048, b, sink, st, wpg)))
         times["prod"].append(timed(lambda: ctx.classify(frames, 2048, 2, a.frames, res, st)))
         r0 = a.reps
         a.reps = 50
@@ -77,6 +84,10 @@ def main():
         if k == "calib":
             continue
         med = statistics.median(ts)
+        if isinstance(k, str) and k.startswith("slotread_"):
+            b = int(k.split("_")[1])
+            out[k] = {"ms_median": round(med, 4), "read_tbps": round(b * a.frames / (med * 1e-3) / 1e12, 3)}
+            continue
         out[NAMES.get(k, k)] = {"ms_median": round(med, 4), "ms_min": round(min(ts), 4),
                                "algo_tbps": round(algo / (med * 1e-3) / 1e12, 3)}
     print(json.dumps(out, indent=1))
