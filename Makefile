@@ -12,7 +12,14 @@ HDRS = include/pollnet_amd.h
 ORACLE = oracle/liboracle.so
 REFDIR ?= /root/reference
 
-all: $(LIB) $(ORACLE) ref
+CPPTEST = tests/cpp/test_gpu_rx
+
+all: $(LIB) $(ORACLE) ref $(CPPTEST)
+
+# standalone C++ adapter test (no torch): links the product library and, as the checker, the oracle
+$(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O2 -std=c++17 -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 $(LIB): $(SRCS) $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lpthread
@@ -24,6 +31,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST)
 
 .PHONY: all ref clean

@@ -55,11 +55,6 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def shard_range(rank: int, world: int, n_per_rank: int):
-    """Contiguous index shard [lo, hi) of the global batch owned by `rank`."""
-    return rank * n_per_rank, (rank + 1) * n_per_rank
-
-
 def cpu_baseline(slots, n, entries, mask, max_conn, budget_s):
     """The oracle (a C port of the reference path, "port") on this host's cores:
     'ref parse + checksum' (Core::checksum + pollNet + onPack header, Core.h:448-526,
@@ -165,6 +160,7 @@ def main():
     import torch.distributed as dist
 
     import pollnet_amd as pa
+    from pollnet_amd.shard import shard_range
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

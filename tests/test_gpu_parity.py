@@ -236,3 +236,14 @@ def test_side_stream_and_sync(torch_cuda, ctx):
         ctx.classify(frames, STRIDE, FRAME_OFF, n, res, st)
     ctx.sync()
     assert_same(res.cpu().numpy().view(pa.RESULT_DTYPE), exp)
+
+
+def test_cpp_adapter_without_torch():
+    """include/pollnet_amd/gpu_rx.hpp driven from a plain C++ process (only /opt/rocm's
+    HIP runtime loaded): records and the pollNet-style TW/recv dispatch vs the oracle."""
+    import subprocess
+
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "test_gpu_rx")
+    assert os.path.exists(exe), "build with `make` first"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr

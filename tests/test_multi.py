@@ -1,0 +1,87 @@
+"""N>1 path on CPU: world_size-2 gloo ranks each own a contiguous index shard of one
+global batch (no data exchange), results aggregate to the single-process answer,
+and the bench's timing reduction (barrier + MAX over ranks) behaves.  The per-shard
+compute here is the oracle (no GPU in this container); on the GPU box the same
+sharding drives pn_classify (bench.py)."""
+import hashlib
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n_per_rank, cfg, out_dir):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch
+
+    import pollnet_amd as pa
+    from oracle import pyoracle as orc
+    from pollnet_amd.shard import shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    p = pa.rx.GenParams.for_config(cfg)
+    lo, hi = shard_range(rank, world, n_per_rank)
+    slots = pa.gen_frames(p, hi - lo, first_index=lo, threads=2)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    dist.barrier()
+    rec = orc.classify_batch(slots, 2048, 2, hi - lo, e, m, t.max_conn_cnt)
+    wall = torch.tensor([float(rank + 1)], dtype=torch.float64)  # stand-in per-rank time
+    dist.all_reduce(wall, op=dist.ReduceOp.MAX)
+    wire = torch.tensor([float(pa.wire_bytes(slots, 2048, 2, hi - lo))], dtype=torch.float64)
+    dist.all_reduce(wire, op=dist.ReduceOp.SUM)
+    np.save(os.path.join(out_dir, f"rank{rank}.npy"), rec)
+    if rank == 0:
+        with open(os.path.join(out_dir, "reduced.txt"), "w") as f:
+            f.write(f"{wall.item()} {wire.item()}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_two_rank_shards_match_single_process(tmp_path, cfg):
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import pollnet_amd as pa
+    from oracle import pyoracle as orc
+
+    world, n = 2, 3000
+    mp.spawn(_worker, args=(world, _free_port(), n, cfg, str(tmp_path)), nprocs=world, join=True)
+    parts = [np.load(tmp_path / f"rank{r}.npy") for r in range(world)]
+    p = pa.rx.GenParams.for_config(cfg)
+    full = pa.gen_frames(p, world * n, threads=4)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    exp = orc.classify_batch(full, 2048, 2, world * n, e, m, t.max_conn_cnt)
+    got = np.concatenate(parts)
+    assert np.array_equal(got, exp)
+    wall, wire = map(float, open(tmp_path / "reduced.txt").read().split())
+    assert wall == float(world)  # MAX over ranks
+    assert wire == float(pa.wire_bytes(full, 2048, 2, world * n))
+
+
+def test_shard_ranges():
+    from pollnet_amd.shard import shard_range, split_range
+
+    assert [shard_range(r, 4, 10) for r in range(4)] == [(0, 10), (10, 20), (20, 30), (30, 40)]
+    spans = [split_range(r, 3, 10) for r in range(3)]
+    assert spans[0][0] == 0 and spans[-1][1] == 10 and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    with pytest.raises(ValueError):
+        shard_range(4, 4, 10)
