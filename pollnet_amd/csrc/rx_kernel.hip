@@ -52,6 +52,7 @@ struct KArgs {
   uint32_t stride;
   uint32_t ipa_off; // (frame_off + 14) & ~15: 16-B aligned start of the header window
   uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
+  uint32_t gpw;     // groups of 64 frames per wave (kernel B)
 };
 
 __device__ __forceinline__ uint32_t dot2(uint32_t w, uint32_t sel, uint32_t acc) {
@@ -128,21 +129,244 @@ __device__ __forceinline__ uint32_t tail_sel(int end, int o) {
   return (uint32_t)((t >> 1) + (t >> 2) * 0xffff);
 }
 
-// WIN: 0 = each header lane loads its own 112-B window (7 x 16 B, one line per
-// lane per instruction); 1 = the same with the first chunk waited for before the
-// rest (diagnostic); 2 = the wave loads each slot's first 128-B line with 8 lanes
-// per line (one request per line) into an XOR-swizzled LDS tile the header lanes
-// read back (needs 128-B aligned slots and ip at line offset 16..31).
-template <int MIS, int BATCH = kBatch, int WPG = kWavesPerWG, int WIN = 0>
-__global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
-  static_assert(BATCH == 4 || BATCH == 8, "lane-transpose reduction is written for 4 or 8 frames");
-  // Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
-  // header.  112 B ends on the slot's first 128-B line boundary for the default
-  // layout (ip at slot+16), so the wave-wide stream below starts on a fresh line
-  // and no line is fetched twice.
-  constexpr int kWinChunks = 7;
-  constexpr int kWinBytes = 16 * kWinChunks;
+// Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
+// header.  112 B ends on the slot's first 128-B line for the default layout (ip at
+// slot+16), so the wave-wide stream starts on a fresh line.
+constexpr int kWinChunks = 7;
+constexpr int kWinBytes = 16 * kWinChunks;
+using Window = Win<4 * kWinChunks>;
+
+// Per-frame state the header lane keeps from phase 1 to phase 3.
+struct FrameState {
+  uint32_t flags, ihl, tot_len, src_ip, dst_ip, seq_raw, doff, tflags, s_ip20, s_opt, tcp_len, conn_id;
+  uint32_t t_all; // exact u16-word sum of [ip, ip+20+tcp_len(+pad)) accumulated so far
+  int end_rel;    // summed extent relative to the window start, 0 when nothing to stream
+  bool trunc;
+};
+
+// ---- phase 1: decode one frame from its header window (lane f <-> frame f) ----
+template <int MIS, int ABL = 0>
+__device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t ether_type, bool live, const KArgs& a) {
   static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
+  FrameState st;
+  // IpHeader (Core.h:57-69), fields relative to ip = window + MIS
+  const uint32_t ver_ihl = h.template b8<MIS + 0>();
+  st.ihl = ver_ihl & 0xf;
+  st.tot_len = bswap16(h.template u16<MIS + 2>());
+  const uint32_t proto = h.template b8<MIS + 9>();
+  st.src_ip = h.template u32<MIS + 12>();
+  st.dst_ip = h.template u32<MIS + 16>();
+  // TcpHeader at ip + 20 (IHL assumed 5: Core.h:507)
+  const uint32_t src_port = h.template u16<MIS + 20>();
+  st.seq_raw = h.template u32<MIS + 24>();
+  st.doff = h.template b8<MIS + 32>() >> 4;
+  st.tflags = h.template b8<MIS + 33>();
+
+  uint32_t flags = (st.tflags & 0x1f) << 4; // fin,syn,rst,psh,ack -> PN_F_FIN..PN_F_ACK
+  if (ether_type != 0x0008 || (ver_ihl >> 4) != 4 || proto != 6) flags |= PN_F_NOT_TCP;
+  if (st.ihl != 5) flags |= PN_F_IHL_NE_5;
+
+  // CSum.add<20>(ip).fold() (Core.h:451-453)
+  st.s_ip20 = h.template sum16<MIS, MIS + 20>();
+  if (csum_fold(st.s_ip20) == 0) flags |= PN_F_IP_OK;
+  // RFC option words [20, 4*IHL)
+  st.s_opt = 0;
+  if (st.ihl > 5) st.s_opt = h.template sum16_upto<MIS + 20, MIS + 60>(MIS + 4 * st.ihl);
+
+  // uint16_t tcp_len = ntohs(tot_len) - 20 ; CSum::add(tcp, tcp_len) reads ceil(tcp_len/2) words
+  st.tcp_len = (st.tot_len - 20) & 0xffff;
+  const uint32_t seg_even = (st.tcp_len + 1) & ~1u;
+  st.trunc = 34 + seg_even > a.avail;
+  if (st.trunc) flags |= PN_F_TRUNC;
+  // summed region relative to the window: [MIS, MIS + 20 + seg_even)
+  st.end_rel = (live && !st.trunc) ? (int)(MIS + 20 + seg_even) : 0;
+
+  // the part of the region inside the window, summed from registers
+  uint32_t t = 0;
+#pragma unroll
+  for (int q = MIS / 4; q < 4 * kWinChunks; ++q) {
+    const uint32_t start_sel = ((4 * q >= MIS) ? 1u : 0u) | ((4 * q + 2 >= MIS) ? 0x10000u : 0u);
+    t = dot2(h.d[q], tail_sel(st.end_rel, 4 * q) & start_sel, t);
+  }
+  st.t_all = t;
+
+  // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
+  st.conn_id = PN_MISS;
+  if (live && !(ABL & 1)) {
+    const uint32_t ip_h = __builtin_bswap32(st.src_ip);
+    const uint32_t port_h = bswap16(src_port);
+    const uint64_t key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
+    uint32_t e = (uint32_t)(key & a.mask);
+    uint64_t k = PN_EMPTY_KEY;
+    uint32_t cid = 0;
+    while (e < a.n_entries) {
+      const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
+      k = ((uint64_t)ent.y << 32) | ent.x;
+      cid = ent.z;
+      if (k >= key) break;
+      ++e;
+    }
+    if (e < a.n_entries && k == key) {
+      st.conn_id = cid;
+      flags |= PN_F_HIT;
+      if (cid >= a.max_conn) flags |= PN_F_TW;
+    }
+  }
+  st.flags = flags;
+  return st;
+}
+
+// ---- phase 2: the wave streams every frame's region past the window ----
+// group_ipa: window start of the group's first slot; frame fi's window is at
+// group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
+// frame with readlane); the total of frame fi lands on lane fi.
+template <int BATCH, int ABL = 0>
+__device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* group_ipa, uint32_t n_here, int lane,
+                                             int end_rel, uint32_t& t_all) {
+  static_assert(BATCH == 4 || BATCH == 8, "lane-transpose reduction is written for 4 or 8 frames");
+  for (uint32_t b0 = 0; b0 < n_here; b0 += BATCH) {
+    uint32_t acc[BATCH];
+    int ends[BATCH];
+    u32x4 w0s[BATCH], w1s[BATCH];
+    // issue all 2*BATCH loads of the batch before consuming any of them
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const uint32_t fi = b0 + j; // wave-uniform
+      const int end = __builtin_amdgcn_readlane(end_rel, fi & 63);
+      ends[j] = end;
+      const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(group_ipa + (uint64_t)fi * a.stride, end16);
+      // out-of-range chunks of a buffer load return 0 and fetch nothing
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
+    auto sel = [](int e, int o) -> uint32_t {
+      if constexpr (ABL & 4) return 0x10001u;
+      else return tail_sel(e, o);
+    };
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int end = ends[j];
+      const u32x4 w0 = w0s[j], w1 = w1s[j];
+      const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
+      uint32_t sum = 0;
+      sum = dot2(w0.x, sel(end, o0), sum);
+      sum = dot2(w0.y, sel(end, o0 + 4), sum);
+      sum = dot2(w0.z, sel(end, o0 + 8), sum);
+      sum = dot2(w0.w, sel(end, o0 + 12), sum);
+      sum = dot2(w1.x, sel(end, o1), sum);
+      sum = dot2(w1.y, sel(end, o1 + 4), sum);
+      sum = dot2(w1.z, sel(end, o1 + 8), sum);
+      sum = dot2(w1.w, sel(end, o1 + 12), sum);
+      acc[j] = sum;
+    }
+    // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
+#pragma unroll
+    for (int j = 0; j < BATCH; ++j) {
+      const int end = ends[j];
+      if (end > kWinBytes + 2048) {
+        const __amdgpu_buffer_rsrc_t rs =
+            frame_rsrc(group_ipa + (uint64_t)(b0 + j) * a.stride, (uint32_t)(end + 15) & ~15u);
+        uint32_t sum = acc[j];
+        for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
+          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, 0);
+          const int o = kb + lane * 16;
+          sum = dot2(w.x, tail_sel(end, o), sum);
+          sum = dot2(w.y, tail_sel(end, o + 4), sum);
+          sum = dot2(w.z, tail_sel(end, o + 8), sum);
+          sum = dot2(w.w, tail_sel(end, o + 12), sum);
+        }
+        acc[j] = sum;
+      }
+    }
+    // transpose-reduce BATCH frames x 64 lanes -> one total per lane group
+    if constexpr (ABL & 2) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < BATCH; ++j) x += acc[j];
+      if ((uint32_t)(lane >> 3) == b0 / BATCH) t_all += x;
+    } else if constexpr (BATCH == 8) { // lane l ends with frame (l>>3)&7
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { // xor 32
+        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
+        acc[i] = r[0] + r[1];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) { // xor 16
+        const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
+        acc[i] = r[0] + r[1];
+      }
+      const bool b3 = lane & 8; // xor 8: keep one, send the other
+      const uint32_t keep = b3 ? acc[1] : acc[0];
+      const uint32_t send = b3 ? acc[0] : acc[1];
+      uint32_t v = keep + dpp<0x128>(send); // row_ror:8 -> lane ^ 8
+      v += dpp<0xB1>(v);                    // quad_perm [1,0,3,2]  -> lane ^ 1
+      v += dpp<0x4E>(v);                    // quad_perm [2,3,0,1]  -> lane ^ 2
+      v += dpp<0x141>(v);                   // row_half_mirror      -> other quad of the 8
+      const uint32_t tot = __shfl(v, (lane & 7) * 8);
+      if ((uint32_t)(lane >> 3) == b0 / 8) t_all += tot;
+    } else { // BATCH == 4: lane l ends with frame (l>>4)&3
+#pragma unroll
+      for (int i = 0; i < 2; ++i) { // xor 32
+        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 2], false, false);
+        acc[i] = r[0] + r[1];
+      }
+      const auto r = __builtin_amdgcn_permlane16_swap(acc[0], acc[1], false, false); // xor 16
+      uint32_t v = r[0] + r[1];
+      v += dpp<0xB1>(v);  // lane ^ 1
+      v += dpp<0x4E>(v);  // lane ^ 2
+      v += dpp<0x141>(v); // other quad of the 8
+      v += dpp<0x128>(v); // row_ror:8 -> other 8 of the 16
+      const uint32_t tot = __shfl(v, (lane & 3) * 16);
+      if ((uint32_t)(lane >> 2) == b0 / 4) t_all += tot;
+    }
+  }
+}
+
+// ---- phase 3: fold and write the record on the frame's lane ----
+template <int MIS>
+__device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f) {
+  uint32_t flags = st.flags;
+  uint32_t tcp_fold = 0xffff;
+  if (!st.trunc) {
+    const uint32_t s_seg = st.t_all - st.s_ip20; // exact: both are exact word sums
+    const uint32_t s_addr = (st.src_ip >> 16) + (st.src_ip & 0xffff) + (st.dst_ip >> 16) + (st.dst_ip & 0xffff);
+    // sum.add(ntohs(0x6)) ; sum.add(htons(tcp_len))  (Core.h:462-464)
+    tcp_fold = csum_fold(s_addr + 0x0600 + bswap16(st.tcp_len) + s_seg);
+    if (tcp_fold == 0) flags |= PN_F_TCP_OK;
+    const uint32_t hl = 4 * st.ihl;
+    if (st.ihl >= 5 && hl <= st.tot_len) {
+      if (csum_fold(st.s_ip20 + st.s_opt) == 0) flags |= PN_F_RFC_IP_OK;
+      uint32_t pad = 0;
+      if (st.tot_len & 1) {
+        const uint8_t* ip = a.frames + (uint64_t)f * a.stride + a.ipa_off + MIS;
+        pad = (uint32_t)ip[st.tot_len] << 8; // the byte the reference sums past the segment
+      }
+      const uint32_t rfc = s_addr + 0x0600 + bswap16(st.tot_len - hl) + (s_seg - st.s_opt - pad);
+      if (csum_fold(rfc) == 0) flags |= PN_F_RFC_TCP_OK;
+    }
+  }
+  // TcpConn::onPack (TcpConn.h:469-473)
+  const int data_off = 34 + 4 * (int)st.doff;
+  const int data_end = 14 + (int)min(st.tot_len, 1500u);
+  u32x4 rec;
+  rec.x = st.conn_id;
+  rec.y = __builtin_bswap32(st.seq_raw) + ((st.tflags >> 1) & 1);
+  rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
+  rec.w = flags | (tcp_fold << 16);
+  *reinterpret_cast<u32x4*>(a.out + f) = rec;
+}
+
+// ---- kernel A: one 64-frame group per wave ----
+// WIN: 0 = each header lane loads its own 112-B window (7 x 16 B buffer loads, one
+// line per lane per instruction); 2 = the wave loads each slot's first 128-B line
+// with 8 lanes per line (exactly one request per line) into an XOR-swizzled LDS
+// tile the header lanes read back (needs 128-B aligned slots and ip at line+16).
+// ABL: timing-only ablations for scripts/variants.py (results are wrong when set):
+// bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail masks.
+template <int MIS, int BATCH = kBatch, int WPG = kWavesPerWG, int WIN = 0, int ABL = 0>
+__global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wave_base = (blockIdx.x * WPG + wave) * kFramesPerWave;
@@ -152,9 +376,7 @@ __global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
   const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
   const uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
 
-  // ---------------- phase 1: header lane (lane f <-> frame f) ----------------
-  // One wave-uniform descriptor over the wave's slots; lanes past n read zeros.
-  Win<4 * kWinChunks> h;
+  Window h;
   uint32_t ether_type;
   if constexpr (WIN == 2) {
     static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
@@ -165,8 +387,7 @@ __global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + line0 + 16 * part, 0, 0);
-      t[r * 8 + (part ^ (r & 7))] = v;
+      t[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + line0 + 16 * part, 0, 0);
     }
     const uint32_t p0 = (a.ipa_off & 127u) >> 4; // == 1 on this path
 #pragma unroll
@@ -190,200 +411,72 @@ __global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
       h.d[4 * c + 1] = v.y;
       h.d[4 * c + 2] = v.z;
       h.d[4 * c + 3] = v.w;
-      if constexpr (WIN == 1) {
-        if (c == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // first chunk lands before the rest issue
-      }
     }
     if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
     else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, 0) >> 16; // ipa_off >= 16 here
   }
-  // IpHeader (Core.h:57-69), fields relative to ip = window + MIS
-  const uint32_t ver_ihl = h.template b8<MIS + 0>();
-  const uint32_t ihl = ver_ihl & 0xf;
-  const uint32_t tot_len = bswap16(h.template u16<MIS + 2>());
-  const uint32_t proto = h.template b8<MIS + 9>();
-  const uint32_t src_ip = h.template u32<MIS + 12>();
-  const uint32_t dst_ip = h.template u32<MIS + 16>();
-  // TcpHeader at ip + 20 (IHL assumed 5: Core.h:507)
-  const uint32_t src_port = h.template u16<MIS + 20>();
-  const uint32_t seq_raw = h.template u32<MIS + 24>();
-  const uint32_t doff = h.template b8<MIS + 32>() >> 4;
-  const uint32_t tflags = h.template b8<MIS + 33>();
+  FrameState st = header_phase<MIS, ABL>(h, ether_type, live, a);
+  stream_phase<BATCH, ABL>(a, wave_slot + a.ipa_off, n_here, lane, st.end_rel, st.t_all);
+  if (live) finish<MIS>(a, st, f);
+}
 
-  uint32_t flags = (tflags & 0x1f) << 4; // fin,syn,rst,psh,ack -> PN_F_FIN..PN_F_ACK
-  if (ether_type != 0x0008 || (ver_ihl >> 4) != 4 || proto != 6) flags |= PN_F_NOT_TCP;
-  if (ihl != 5) flags |= PN_F_IHL_NE_5;
+// ---- kernel B: a wave walks `gpw` consecutive 64-frame groups and prefetches the
+// next group's header window straight into LDS (buffer_load ... lds, no VGPRs)
+// while it streams the current group, so the header round trip leaves the critical
+// path.  LDS image per wave: [chunk][lane] x 16 B (conflict-free ds_read_b128).
+template <int MIS, int BATCH = kBatch>
+__global__ __launch_bounds__(kWave) void rx_classify_groups_kernel(KArgs a) {
+  constexpr int kPre = kWinChunks + (MIS < 2 ? 1 : 0); // + the chunk holding the ether type
+  __shared__ u32x4 pre[kPre][kWave];
+  const int lane = threadIdx.x;
+  const uint32_t n_groups = (a.n + kFramesPerWave - 1) / kFramesPerWave;
+  const uint32_t g0 = blockIdx.x * a.gpw;
+  if (g0 >= n_groups) return;
+  const uint32_t g_end = min(g0 + a.gpw, n_groups);
 
-  // CSum.add<20>(ip).fold() (Core.h:451-453)
-  const uint32_t s_ip20 = h.template sum16<MIS, MIS + 20>();
-  if (csum_fold(s_ip20) == 0) flags |= PN_F_IP_OK;
-  // RFC option words [20, 4*IHL)
-  const uint32_t hl = 4 * ihl;
-  uint32_t s_opt = 0;
-  if (ihl > 5) s_opt = h.template sum16_upto<MIS + 20, MIS + 60>(MIS + hl);
-
-  // uint16_t tcp_len = ntohs(tot_len) - 20 ; CSum::add(tcp, tcp_len) reads ceil(tcp_len/2) words
-  const uint32_t tcp_len = (tot_len - 20) & 0xffff;
-  const uint32_t seg_even = (tcp_len + 1) & ~1u;
-  const bool trunc = 34 + seg_even > a.avail;
-  if (trunc) flags |= PN_F_TRUNC;
-  // summed region relative to the window: [MIS, MIS + 20 + seg_even)
-  const int end_rel = (live && !trunc) ? (int)(MIS + 20 + seg_even) : 0;
-
-  // the part of the region inside the window, summed by this lane from registers
-  uint32_t t_all = 0;
+  auto prefetch = [&](uint32_t g) {
+    const uint32_t base = g * kFramesPerWave;
+    const uint32_t nh = min((uint32_t)kFramesPerWave, a.n - base);
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.frames + (uint64_t)base * a.stride, nh * a.stride);
+    const uint32_t lo = (uint32_t)lane * a.stride + a.ipa_off;
 #pragma unroll
-  for (int q = MIS / 4; q < 4 * kWinChunks; ++q) {
-    const uint32_t start_sel = ((4 * q >= MIS) ? 1u : 0u) | ((4 * q + 2 >= MIS) ? 0x10000u : 0u);
-    const uint32_t sel = tail_sel(end_rel, 4 * q) & start_sel;
-    t_all = dot2(h.d[q], sel, t_all);
+    for (int c = 0; c < kWinChunks; ++c)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&pre[c][0], 16, lo + 16 * c,
+                                               0, 0, 0);
+    if constexpr (MIS < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&pre[kWinChunks][0], 16,
+                                               lo - 16, 0, 0, 0);
+  };
+
+  prefetch(g0);
+  for (uint32_t g = g0; g < g_end; ++g) {
+    const uint32_t wave_base = g * kFramesPerWave;
+    const uint32_t f = wave_base + lane;
+    const bool live = f < a.n;
+    const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
+    // the window for g has landed (nothing else is outstanding here)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    Window h;
+#pragma unroll
+    for (int c = 0; c < kWinChunks; ++c) {
+      const u32x4 v = pre[c][lane];
+      h.d[4 * c + 0] = v.x;
+      h.d[4 * c + 1] = v.y;
+      h.d[4 * c + 2] = v.z;
+      h.d[4 * c + 3] = v.w;
+    }
+    uint32_t ether_type;
+    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+    else ether_type = pre[kWinChunks][lane].w >> 16;
+    FrameState st = header_phase<MIS>(h, ether_type, live, a);
+    // The LDS image is consumed (its values are in registers); refill it for the next
+    // group now, after the probe (whose load would otherwise wait for the DMA, vmcnt
+    // being in-order) and ahead of the stream it hides behind.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (g + 1 < g_end) prefetch(g + 1);
+    stream_phase<BATCH>(a, a.frames + (uint64_t)wave_base * a.stride + a.ipa_off, n_here, lane, st.end_rel, st.t_all);
+    if (live) finish<MIS>(a, st, f);
   }
-
-  // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded
-  uint32_t conn_id = PN_MISS;
-  if (live) {
-    const uint32_t ip_h = __builtin_bswap32(src_ip);
-    const uint32_t port_h = bswap16(src_port);
-    const uint64_t key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
-    uint32_t e = (uint32_t)(key & a.mask);
-    uint64_t k = PN_EMPTY_KEY;
-    uint32_t cid = 0;
-    while (e < a.n_entries) {
-      const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
-      k = ((uint64_t)ent.y << 32) | ent.x;
-      cid = ent.z;
-      if (k >= key) break;
-      ++e;
-    }
-    if (e < a.n_entries && k == key) {
-      conn_id = cid;
-      flags |= PN_F_HIT;
-      if (cid >= a.max_conn) flags |= PN_F_TW;
-    }
-  }
-
-  // ---------------- phase 2: the rest of each frame, streamed by the wave ----------------
-  const uint8_t* wave_ipa = wave_slot + a.ipa_off;
-  for (uint32_t b0 = 0; b0 < n_here; b0 += BATCH) {
-    uint32_t acc[BATCH];
-    int ends[BATCH];
-    u32x4 w0s[BATCH], w1s[BATCH];
-    // issue all 2*BATCH loads of the batch before consuming any of them
-#pragma unroll
-    for (int j = 0; j < BATCH; ++j) {
-      const uint32_t fi = b0 + j; // wave-uniform
-      const int end = __builtin_amdgcn_readlane(end_rel, fi & 63);
-      ends[j] = end;
-      const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
-      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_ipa + (uint64_t)fi * a.stride, end16);
-      // out-of-range chunks of a buffer load return 0 and fetch nothing
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, 0);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
-#pragma unroll
-    for (int j = 0; j < BATCH; ++j) {
-      const int end = ends[j];
-      const u32x4 w0 = w0s[j], w1 = w1s[j];
-      const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
-      uint32_t s = 0;
-      s = dot2(w0.x, tail_sel(end, o0), s);
-      s = dot2(w0.y, tail_sel(end, o0 + 4), s);
-      s = dot2(w0.z, tail_sel(end, o0 + 8), s);
-      s = dot2(w0.w, tail_sel(end, o0 + 12), s);
-      s = dot2(w1.x, tail_sel(end, o1), s);
-      s = dot2(w1.y, tail_sel(end, o1 + 4), s);
-      s = dot2(w1.z, tail_sel(end, o1 + 8), s);
-      s = dot2(w1.w, tail_sel(end, o1 + 12), s);
-      acc[j] = s;
-    }
-    // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
-#pragma unroll
-    for (int j = 0; j < BATCH; ++j) {
-      const int end = ends[j];
-      if (end > kWinBytes + 2048) {
-        const __amdgpu_buffer_rsrc_t rs =
-            frame_rsrc(wave_ipa + (uint64_t)(b0 + j) * a.stride, (uint32_t)(end + 15) & ~15u);
-        uint32_t s = acc[j];
-        for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
-          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, 0);
-          const int o = kb + lane * 16;
-          s = dot2(w.x, tail_sel(end, o), s);
-          s = dot2(w.y, tail_sel(end, o + 4), s);
-          s = dot2(w.z, tail_sel(end, o + 8), s);
-          s = dot2(w.w, tail_sel(end, o + 12), s);
-        }
-        acc[j] = s;
-      }
-    }
-    // transpose-reduce BATCH frames x 64 lanes -> one total per lane group
-    uint32_t v;
-    if constexpr (BATCH == 8) { // lane l ends with frame (l>>3)&7
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { // xor 32
-        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
-        acc[i] = r[0] + r[1];
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) { // xor 16
-        const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
-        acc[i] = r[0] + r[1];
-      }
-      const bool b3 = lane & 8; // xor 8: keep one, send the other
-      const uint32_t keep = b3 ? acc[1] : acc[0];
-      const uint32_t send = b3 ? acc[0] : acc[1];
-      v = keep + dpp<0x128>(send); // row_ror:8 -> lane ^ 8
-      v += dpp<0xB1>(v);           // quad_perm [1,0,3,2]  -> lane ^ 1
-      v += dpp<0x4E>(v);           // quad_perm [2,3,0,1]  -> lane ^ 2
-      v += dpp<0x141>(v);          // row_half_mirror      -> other quad of the 8
-      const uint32_t tot = __shfl(v, (lane & 7) * 8);
-      if ((uint32_t)(lane >> 3) == b0 / 8) t_all += tot;
-    } else { // BATCH == 4: lane l ends with frame (l>>4)&3
-#pragma unroll
-      for (int i = 0; i < 2; ++i) { // xor 32
-        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 2], false, false);
-        acc[i] = r[0] + r[1];
-      }
-      const auto r = __builtin_amdgcn_permlane16_swap(acc[0], acc[1], false, false); // xor 16
-      v = r[0] + r[1];
-      v += dpp<0xB1>(v);  // lane ^ 1
-      v += dpp<0x4E>(v);  // lane ^ 2
-      v += dpp<0x141>(v); // other quad of the 8
-      v += dpp<0x128>(v); // row_ror:8 -> other 8 of the 16
-      const uint32_t tot = __shfl(v, (lane & 3) * 16);
-      if ((uint32_t)(lane >> 2) == b0 / 4) t_all += tot;
-    }
-  }
-
-  // ---------------- phase 3: finish on the frame's lane ----------------
-  if (!live) return;
-  uint32_t tcp_fold = 0xffff;
-  if (!trunc) {
-    const uint32_t s_seg = t_all - s_ip20; // exact: both are exact word sums
-    const uint32_t s_addr = (src_ip >> 16) + (src_ip & 0xffff) + (dst_ip >> 16) + (dst_ip & 0xffff);
-    // sum.add(ntohs(0x6)) ; sum.add(htons(tcp_len))  (Core.h:462-464)
-    tcp_fold = csum_fold(s_addr + 0x0600 + bswap16(tcp_len) + s_seg);
-    if (tcp_fold == 0) flags |= PN_F_TCP_OK;
-    if (ihl >= 5 && hl <= tot_len) {
-      if (csum_fold(s_ip20 + s_opt) == 0) flags |= PN_F_RFC_IP_OK;
-      uint32_t pad = 0;
-      if (tot_len & 1) {
-        const uint8_t* ip = a.frames + (uint64_t)f * a.stride + a.ipa_off + MIS;
-        pad = (uint32_t)ip[tot_len] << 8; // the byte the reference sums past the segment
-      }
-      const uint32_t rfc = s_addr + 0x0600 + bswap16(tot_len - hl) + (s_seg - s_opt - pad);
-      if (csum_fold(rfc) == 0) flags |= PN_F_RFC_TCP_OK;
-    }
-  }
-  // TcpConn::onPack (TcpConn.h:469-473)
-  const int data_off = 34 + 4 * (int)doff;
-  const int data_end = 14 + (int)min(tot_len, 1500u);
-  u32x4 rec;
-  rec.x = conn_id;
-  rec.y = __builtin_bswap32(seq_raw) + ((tflags >> 1) & 1);
-  rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
-  rec.w = flags | (tcp_fold << 16);
-  *reinterpret_cast<u32x4*>(a.out + f) = rec;
 }
 
 __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src, uint64_t n16, uint32_t* sink) {
@@ -396,10 +489,14 @@ __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src
   if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc; // keeps the loads live; practically never stores
 }
 
-// Read-only ceiling for the slot layout: each wave reads the first `bytes` of each of
-// its 64 slots with the same 1-KiB buffer loads and batching as phase 2 (no
-// header, no arithmetic).  Bounds what the RX kernel can reach on this layout.
-template <int WPG>
+// Read-only ceilings for the slot layout (no header work, no arithmetic):
+// MODE 0: each wave streams the first `bytes` of each of its 64 slots with the RX
+//         kernel's 1-KiB buffer loads, 8 slots per batch;
+// MODE 1: "split" — line 0 of all 64 slots first (one lane per slot), then lines
+//         1.. of each slot in batches (the one-group kernel's access order);
+// MODE 2: "pipelined" — per batch, line 0 of the NEXT 8 slots (8 lanes per line)
+//         is fetched together with lines 1.. of the current 8 slots.
+template <int WPG, int MODE>
 __global__ __launch_bounds__(kWave* WPG) void calib_slot_read_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
                                                                     uint32_t bytes, uint32_t* sink) {
   const int lane = threadIdx.x & 63;
@@ -407,19 +504,43 @@ __global__ __launch_bounds__(kWave* WPG) void calib_slot_read_kernel(const uint8
   const uint32_t wave_base = (blockIdx.x * WPG + wave) * kFramesPerWave;
   if (wave_base >= n) return;
   const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+  const uint8_t* wb = base + (uint64_t)wave_base * stride;
   uint32_t acc = 0;
+  const uint32_t first = MODE == 0 ? 0u : 128u;
+  if constexpr (MODE == 1) {
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb, n_here * stride);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * stride + 16 * c, 0, 0);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  }
+  u32x4 line0 = {0, 0, 0, 0};
+  if constexpr (MODE == 2) {
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb, n_here * stride);
+    line0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (lane >> 3) * stride + 16 * (lane & 7), 0, 0);
+  }
   for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
     u32x4 w0s[kBatch], w1s[kBatch];
+    u32x4 nxt = {0, 0, 0, 0};
+    if constexpr (MODE == 2) {
+      if (b0 + kBatch < n_here) {
+        const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb, n_here * stride);
+        nxt = __builtin_amdgcn_raw_buffer_load_b128(rs, (b0 + kBatch + (lane >> 3)) * stride + 16 * (lane & 7), 0, 0);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
       const uint32_t nb = (b0 + j < n_here) ? bytes : 0u;
-      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(base + (uint64_t)(wave_base + b0 + j) * stride, nb);
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, first + lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, first + 1024 + lane * 16, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
+    acc ^= line0.x ^ line0.y ^ line0.z ^ line0.w;
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+    line0 = nxt;
   }
   if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
 }
@@ -457,11 +578,18 @@ void launch(const KArgs& a, uint32_t grid, hipStream_t s) {
 
 // Tuning variants of the MIS=0 (default layout) kernel, A/B-timed in one process by
 // scripts/variants.py.  Not part of the public ABI.
-template <int BATCH, int WPG, int WIN = 0>
+template <int BATCH, int WPG, int WIN = 0, int ABL = 0>
 void launch_variant(const KArgs& a, hipStream_t s) {
   const uint32_t per_wg = kFramesPerWave * WPG;
-  hipLaunchKernelGGL((rx_classify_kernel<0, BATCH, WPG, WIN>), dim3((a.n + per_wg - 1) / per_wg), dim3(kWave * WPG), 0,
-                     s, a);
+  hipLaunchKernelGGL((rx_classify_kernel<0, BATCH, WPG, WIN, ABL>), dim3((a.n + per_wg - 1) / per_wg), dim3(kWave * WPG),
+                     0, s, a);
+}
+
+template <int BATCH>
+void launch_groups_variant(KArgs a, uint32_t gpw, hipStream_t s) {
+  const uint32_t n_groups = (a.n + kFramesPerWave - 1) / kFramesPerWave;
+  a.gpw = gpw;
+  hipLaunchKernelGGL((rx_classify_groups_kernel<0, BATCH>), dim3((n_groups + gpw - 1) / gpw), dim3(kWave), 0, s, a);
 }
 } // namespace
 
@@ -543,6 +671,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
+  a.gpw = 1;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
@@ -567,7 +696,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                         void* results_dev, void* stream, int variant) {
   if (!ctx || !ctx->tbl_dev || (frame_off + 14) % 16 != 0 || n == 0) return set_err(ctx, PN_EINVAL, "variant: bad args");
-  if (variant >= 7 && (((frame_off + 14) & 127) >> 4) != 1) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
+  if (variant == 1 && (((frame_off + 14) & 127) >> 4) != 1) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
   KArgs a;
   a.frames = (const uint8_t*)frames_dev;
   a.out = (pn_result*)results_dev;
@@ -579,18 +708,20 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
+  a.gpw = 1;
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
-    case 0: launch_variant<8, 4>(a, s); break;
-    case 1: launch_variant<4, 4>(a, s); break;
-    case 2: launch_variant<8, 1>(a, s); break;
-    case 3: launch_variant<4, 1>(a, s); break;
-    case 4: launch_variant<8, 2>(a, s); break;
-    case 5: launch_variant<4, 2>(a, s); break;
-    case 6: launch_variant<8, 4, 1>(a, s); break;
-    case 7: launch_variant<8, 4, 2>(a, s); break;
-    case 8: launch_variant<8, 1, 2>(a, s); break;
-    case 9: launch_variant<8, 2, 2>(a, s); break;
+    case 0: launch_variant<8, 1>(a, s); break;            // one group per wave, per-lane window
+    case 1: launch_variant<8, 1, 2>(a, s); break;         // one group per wave, cooperative window
+    case 2: launch_groups_variant<8>(a, 2, s); break;     // groups per wave + LDS prefetch
+    case 3: launch_groups_variant<8>(a, 4, s); break;
+    case 4: launch_groups_variant<8>(a, 8, s); break;
+    case 5: launch_groups_variant<4>(a, 4, s); break;
+    case 6: launch_variant<8, 4>(a, s); break;            // 256-thread workgroups
+    case 11: launch_variant<8, 1, 0, 1>(a, s); break;     // timing-only ablations from here
+    case 12: launch_variant<8, 1, 0, 2>(a, s); break;
+    case 14: launch_variant<8, 1, 0, 4>(a, s); break;
+    case 17: launch_variant<8, 1, 0, 7>(a, s); break;
     default: return set_err(ctx, PN_EINVAL, "variant: unknown");
   }
   hipError_t e = hipGetLastError();
@@ -605,12 +736,15 @@ int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint3
     return set_err(ctx, PN_EINVAL, "pn_calib_slot_read: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t waves = (n_slots + kFramesPerWave - 1) / kFramesPerWave;
-  if (waves_per_wg == 1)
-    hipLaunchKernelGGL((calib_slot_read_kernel<1>), dim3(waves), dim3(64), 0, s, (const uint8_t*)src_dev, n_slots, stride,
-                       bytes, (uint32_t*)sink_dev);
-  else
-    hipLaunchKernelGGL((calib_slot_read_kernel<4>), dim3((waves + 3) / 4), dim3(256), 0, s, (const uint8_t*)src_dev,
-                       n_slots, stride, bytes, (uint32_t*)sink_dev);
+  const uint8_t* src = (const uint8_t*)src_dev;
+  uint32_t* sink = (uint32_t*)sink_dev;
+  switch (waves_per_wg) { // >= 10: access-order experiments (mode = waves_per_wg / 10), 64-thread WGs
+    case 1: hipLaunchKernelGGL((calib_slot_read_kernel<1, 0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 11: hipLaunchKernelGGL((calib_slot_read_kernel<1, 1>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 21: hipLaunchKernelGGL((calib_slot_read_kernel<1, 2>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    default:
+      hipLaunchKernelGGL((calib_slot_read_kernel<4, 0>), dim3((waves + 3) / 4), dim3(256), 0, s, src, n_slots, stride, bytes, sink);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "calib slot launch");
   ctx->last_stream = s;
