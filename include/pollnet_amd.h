@@ -145,10 +145,12 @@ int pn_sync(pn_ctx* ctx);
 /* HBM streaming-read calibration kernel (used by bench/profiling only): reads
  * `bytes` (multiple of 16) from src and writes one u32 per workgroup to sink. */
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream);
-/* Read-only ceiling for a slot layout: the first `bytes` (<= 2048) of each of n_slots
- * slots, read with the RX kernel's own load pattern and no arithmetic. */
+/* Ceiling for a slot layout: the first `bytes` (<= 2048) of each of n_slots slots,
+ * read with the RX kernel's own load pattern and no arithmetic; store_bytes = 16 / 8
+ * also writes that many bytes per slot to sink_dev (n_slots x 16 B) like the RX
+ * kernel's records, 0 writes nothing. */
 int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
-                       int waves_per_wg, void* sink_dev, void* stream);
+                       int store_bytes, void* sink_dev, void* stream);
 
 /* ======================= synthetic frame generator =======================
  * Deterministic (seed, frame index) generator for the BASELINE configs; writes

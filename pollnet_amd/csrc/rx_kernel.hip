@@ -6,9 +6,11 @@
 // findConnEntry, TIME_WAIT test), Core.h:448-472 (checksum, debug build),
 // Core.h:89-138 (CSum), TcpConn.h:469-473 (payload arithmetic).
 //
-// Execution model (one wavefront = 64 frames, no inter-wave communication):
-//  phase 1  lane f owns frame f: loads a 112-B header window straight to VGPRs
-//           (ending on the slot's first 128-B line for the default layout),
+// Execution model (one wavefront = 64 frames, 64-thread workgroups, no
+// inter-wave communication):
+//  phase 1  lane f owns frame f: gets a 112-B header window (either 8 lanes per
+//           slot load its first 128-B line coalesced into a swizzled LDS tile, or
+//           each lane loads its own window when the layout is not line-aligned),
 //           decodes fields at compile-time offsets (kernel specialised on
 //           (frame_off+14)%16), computes the 20-byte IP sum, the sum of the
 //           frame's words inside the window, connHashKey and the ordered probe
@@ -22,7 +24,10 @@
 //  phase 3  lane f subtracts the IP-header words, adds the pseudo-header and
 //           folds exactly like CSum::fold; one coalesced 16-B record per lane.
 // HBM bytes per frame = the frame itself (+16 B result): the kernel is bound by
-// HBM read bandwidth (no MFMA: there is no contraction).
+// HBM bandwidth (no MFMA: there is no contraction).  It runs within ~1 % of a
+// no-arithmetic kernel with the same reads and record writes;
+// the remaining gap to pure streaming is the DRAM cost of interleaving the
+// record writes with the frame reads.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -34,9 +39,13 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerWG = 1; // 64-thread workgroups: +3% over 4 waves/WG (scripts/variants.py, profiles/)
-constexpr int kFramesPerWave = 64;
-constexpr int kBatch = 8;
+constexpr int kFramesPerWave = 64; // one wave per 64-thread workgroup: +3 % over 4 waves/WG (profiles/r01_experiments)
+constexpr int kBatch = 8;        // frames per stream batch: 16 x 1-KiB loads in flight per wave
+// Cache policy (buffer-instruction aux bits on gfx950: 1 sc0, 2 nt, 16 sc1).  Frame
+// bytes are read once: non-temporal loads.  Records are written once: write-through
+// (sc1) stores.  Together -1.1..1.3 % kernel time (profiles/r01_experiments).
+constexpr int kLoadAux = 2;
+constexpr int kStoreAux = 16;
 
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
 using u16x2 = __attribute__((ext_vector_type(2))) unsigned short;
@@ -52,7 +61,6 @@ struct KArgs {
   uint32_t stride;
   uint32_t ipa_off; // (frame_off + 14) & ~15: 16-B aligned start of the header window
   uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
-  uint32_t gpw;     // groups of 64 frames per wave (kernel B)
 };
 
 __device__ __forceinline__ uint32_t dot2(uint32_t w, uint32_t sel, uint32_t acc) {
@@ -144,8 +152,13 @@ struct FrameState {
   bool trunc;
 };
 
+// Timing-only ablations (scripts/variants.py; records are wrong when set):
+// bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
+// masks, bit3 no record store.
+enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8 };
+
 // ---- phase 1: decode one frame from its header window (lane f <-> frame f) ----
-template <int MIS, int ABL = 0>
+template <int MIS, int ABL>
 __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t ether_type, bool live, const KArgs& a) {
   static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
   FrameState st;
@@ -192,7 +205,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 
   // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
   st.conn_id = PN_MISS;
-  if (live && !(ABL & 1)) {
+  if (live && !(ABL & kAblNoProbe)) {
     const uint32_t ip_h = __builtin_bswap32(st.src_ip);
     const uint32_t port_h = bswap16(src_port);
     const uint64_t key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
@@ -220,33 +233,32 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 // group_ipa: window start of the group's first slot; frame fi's window is at
 // group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
 // frame with readlane); the total of frame fi lands on lane fi.
-template <int BATCH, int ABL = 0>
+template <int ABL, int LAUX>
 __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* group_ipa, uint32_t n_here, int lane,
                                              int end_rel, uint32_t& t_all) {
-  static_assert(BATCH == 4 || BATCH == 8, "lane-transpose reduction is written for 4 or 8 frames");
-  for (uint32_t b0 = 0; b0 < n_here; b0 += BATCH) {
-    uint32_t acc[BATCH];
-    int ends[BATCH];
-    u32x4 w0s[BATCH], w1s[BATCH];
-    // issue all 2*BATCH loads of the batch before consuming any of them
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    uint32_t acc[kBatch];
+    int ends[kBatch];
+    u32x4 w0s[kBatch], w1s[kBatch];
+    // issue all 2*kBatch loads of the batch before consuming any of them
 #pragma unroll
-    for (int j = 0; j < BATCH; ++j) {
+    for (int j = 0; j < kBatch; ++j) {
       const uint32_t fi = b0 + j; // wave-uniform
       const int end = __builtin_amdgcn_readlane(end_rel, fi & 63);
       ends[j] = end;
       const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(group_ipa + (uint64_t)fi * a.stride, end16);
       // out-of-range chunks of a buffer load return 0 and fetch nothing
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, 0);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, 0);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, LAUX);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, LAUX);
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
     auto sel = [](int e, int o) -> uint32_t {
-      if constexpr (ABL & 4) return 0x10001u;
+      if constexpr (ABL & kAblNoMask) return 0x10001u;
       else return tail_sel(e, o);
     };
 #pragma unroll
-    for (int j = 0; j < BATCH; ++j) {
+    for (int j = 0; j < kBatch; ++j) {
       const int end = ends[j];
       const u32x4 w0 = w0s[j], w1 = w1s[j];
       const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
@@ -263,14 +275,14 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
     }
     // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
 #pragma unroll
-    for (int j = 0; j < BATCH; ++j) {
+    for (int j = 0; j < kBatch; ++j) {
       const int end = ends[j];
       if (end > kWinBytes + 2048) {
         const __amdgpu_buffer_rsrc_t rs =
             frame_rsrc(group_ipa + (uint64_t)(b0 + j) * a.stride, (uint32_t)(end + 15) & ~15u);
         uint32_t sum = acc[j];
         for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
-          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, 0);
+          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
           const int o = kb + lane * 16;
           sum = dot2(w.x, tail_sel(end, o), sum);
           sum = dot2(w.y, tail_sel(end, o + 4), sum);
@@ -280,52 +292,38 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
         acc[j] = sum;
       }
     }
-    // transpose-reduce BATCH frames x 64 lanes -> one total per lane group
-    if constexpr (ABL & 2) {
+    // transpose-reduce 8 frames x 64 lanes: lane l ends with the total of frame (l>>3)&7
+    if constexpr (ABL & kAblNoReduce) {
       uint32_t x = 0;
 #pragma unroll
-      for (int j = 0; j < BATCH; ++j) x += acc[j];
-      if ((uint32_t)(lane >> 3) == b0 / BATCH) t_all += x;
-    } else if constexpr (BATCH == 8) { // lane l ends with frame (l>>3)&7
+      for (int j = 0; j < kBatch; ++j) x += acc[j];
+      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += x;
+    } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { // xor 32
+      for (int i = 0; i < 4; ++i) { // xor 32: v_permlane32_swap
         const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
         acc[i] = r[0] + r[1];
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i) { // xor 16
+      for (int i = 0; i < 2; ++i) { // xor 16: v_permlane16_swap
         const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
         acc[i] = r[0] + r[1];
       }
       const bool b3 = lane & 8; // xor 8: keep one, send the other
       const uint32_t keep = b3 ? acc[1] : acc[0];
       const uint32_t send = b3 ? acc[0] : acc[1];
-      uint32_t v = keep + dpp<0x128>(send); // row_ror:8 -> lane ^ 8
+      uint32_t v = keep + dpp<0x128>(send); // row_ror:8           -> lane ^ 8
       v += dpp<0xB1>(v);                    // quad_perm [1,0,3,2]  -> lane ^ 1
       v += dpp<0x4E>(v);                    // quad_perm [2,3,0,1]  -> lane ^ 2
       v += dpp<0x141>(v);                   // row_half_mirror      -> other quad of the 8
       const uint32_t tot = __shfl(v, (lane & 7) * 8);
-      if ((uint32_t)(lane >> 3) == b0 / 8) t_all += tot;
-    } else { // BATCH == 4: lane l ends with frame (l>>4)&3
-#pragma unroll
-      for (int i = 0; i < 2; ++i) { // xor 32
-        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 2], false, false);
-        acc[i] = r[0] + r[1];
-      }
-      const auto r = __builtin_amdgcn_permlane16_swap(acc[0], acc[1], false, false); // xor 16
-      uint32_t v = r[0] + r[1];
-      v += dpp<0xB1>(v);  // lane ^ 1
-      v += dpp<0x4E>(v);  // lane ^ 2
-      v += dpp<0x141>(v); // other quad of the 8
-      v += dpp<0x128>(v); // row_ror:8 -> other 8 of the 16
-      const uint32_t tot = __shfl(v, (lane & 3) * 16);
-      if ((uint32_t)(lane >> 2) == b0 / 4) t_all += tot;
+      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
     }
   }
 }
 
 // ---- phase 3: fold and write the record on the frame's lane ----
-template <int MIS>
+template <int MIS, int ABL, int SAUX>
 __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f) {
   uint32_t flags = st.flags;
   uint32_t tcp_fold = 0xffff;
@@ -355,128 +353,72 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   rec.y = __builtin_bswap32(st.seq_raw) + ((st.tflags >> 1) & 1);
   rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
   rec.w = flags | (tcp_fold << 16);
-  *reinterpret_cast<u32x4*>(a.out + f) = rec;
+  if constexpr (ABL & kAblNoStore) {
+    if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
+  } else {
+    // one coalesced 1-KiB store per wave; the descriptor covers this wave's 64 records
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc((const uint8_t*)(a.out + (f & ~63u)), 64 * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(rec, rs, (f & 63u) * 16, 0, SAUX);
+  }
 }
 
-// ---- kernel A: one 64-frame group per wave ----
-// WIN: 0 = each header lane loads its own 112-B window (7 x 16 B buffer loads, one
-// line per lane per instruction); 2 = the wave loads each slot's first 128-B line
-// with 8 lanes per line (exactly one request per line) into an XOR-swizzled LDS
-// tile the header lanes read back (needs 128-B aligned slots and ip at line+16).
-// ABL: timing-only ablations for scripts/variants.py (results are wrong when set):
-// bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail masks.
-template <int MIS, int BATCH = kBatch, int WPG = kWavesPerWG, int WIN = 0, int ABL = 0>
-__global__ __launch_bounds__(kWave* WPG) void rx_classify_kernel(KArgs a) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave_base = (blockIdx.x * WPG + wave) * kFramesPerWave;
+// ---- the kernel: one 64-frame group per 64-thread workgroup ----
+// COOP = 1: 8 lanes per slot load its first 128-B line (exactly one request per
+// line, the line the header window lives in) into an XOR-swizzled LDS tile that
+// the header lanes read back; needs 128-B aligned lines with ip at line + 16..31.
+// COOP = 0: each lane loads its own 112-B window (any layout).
+template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux>
+// 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
+// default and ef_vi layouts); the 2-mod-4 alignments need two more VGPRs and keep 4.
+__global__ __launch_bounds__(kWave, (MIS % 4 == 0) ? 5 : 4) void rx_classify_kernel(KArgs a) {
+  const int lane = threadIdx.x;
+  const uint32_t wave_base = blockIdx.x * kFramesPerWave;
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
   const bool live = f < a.n;
   const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
   const uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
+  // one wave-uniform descriptor over the wave's slots; lanes past n read zeros
+  const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
 
   Window h;
   uint32_t ether_type;
-  if constexpr (WIN == 2) {
+  if constexpr (COOP) {
     static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
-    __shared__ u32x4 tile[WPG][kFramesPerWave * 8]; // 8 KiB per wave: 64 slots x 128 B
-    u32x4* t = tile[wave];
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
+    __shared__ u32x4 tile[kFramesPerWave * 8]; // 8 KiB: 64 slots x 128 B, chunk p of slot r at r*8 + (p ^ (r&7))
     const uint32_t line0 = a.ipa_off & ~127u;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-      t[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + line0 + 16 * part, 0, 0);
+      tile[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + line0 + 16 * part, 0, LAUX);
     }
     const uint32_t p0 = (a.ipa_off & 127u) >> 4; // == 1 on this path
 #pragma unroll
     for (int c = 0; c < kWinChunks; ++c) {
-      const u32x4 v = t[lane * 8 + ((p0 + c) ^ (lane & 7))];
+      const u32x4 v = tile[lane * 8 + ((p0 + c) ^ (lane & 7))];
       h.d[4 * c + 0] = v.x;
       h.d[4 * c + 1] = v.y;
       h.d[4 * c + 2] = v.z;
       h.d[4 * c + 3] = v.w;
     }
     if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
-    else ether_type = t[lane * 8 + ((p0 - 1) ^ (lane & 7))].w >> 16;
+    else ether_type = tile[lane * 8 + ((p0 - 1) ^ (lane & 7))].w >> 16;
   } else {
-    // One wave-uniform descriptor over the wave's slots; lanes past n read zeros.
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
     const uint32_t lo = (uint32_t)lane * a.stride + a.ipa_off;
 #pragma unroll
     for (int c = 0; c < kWinChunks; ++c) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + 16 * c, 0, 0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + 16 * c, 0, LAUX);
       h.d[4 * c + 0] = v.x;
       h.d[4 * c + 1] = v.y;
       h.d[4 * c + 2] = v.z;
       h.d[4 * c + 3] = v.w;
     }
     if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
-    else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, 0) >> 16; // ipa_off >= 16 here
+    else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, LAUX) >> 16; // ipa_off >= 16 here
   }
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live, a);
-  stream_phase<BATCH, ABL>(a, wave_slot + a.ipa_off, n_here, lane, st.end_rel, st.t_all);
-  if (live) finish<MIS>(a, st, f);
-}
-
-// ---- kernel B: a wave walks `gpw` consecutive 64-frame groups and prefetches the
-// next group's header window straight into LDS (buffer_load ... lds, no VGPRs)
-// while it streams the current group, so the header round trip leaves the critical
-// path.  LDS image per wave: [chunk][lane] x 16 B (conflict-free ds_read_b128).
-template <int MIS, int BATCH = kBatch>
-__global__ __launch_bounds__(kWave) void rx_classify_groups_kernel(KArgs a) {
-  constexpr int kPre = kWinChunks + (MIS < 2 ? 1 : 0); // + the chunk holding the ether type
-  __shared__ u32x4 pre[kPre][kWave];
-  const int lane = threadIdx.x;
-  const uint32_t n_groups = (a.n + kFramesPerWave - 1) / kFramesPerWave;
-  const uint32_t g0 = blockIdx.x * a.gpw;
-  if (g0 >= n_groups) return;
-  const uint32_t g_end = min(g0 + a.gpw, n_groups);
-
-  auto prefetch = [&](uint32_t g) {
-    const uint32_t base = g * kFramesPerWave;
-    const uint32_t nh = min((uint32_t)kFramesPerWave, a.n - base);
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.frames + (uint64_t)base * a.stride, nh * a.stride);
-    const uint32_t lo = (uint32_t)lane * a.stride + a.ipa_off;
-#pragma unroll
-    for (int c = 0; c < kWinChunks; ++c)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&pre[c][0], 16, lo + 16 * c,
-                                               0, 0, 0);
-    if constexpr (MIS < 2)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)&pre[kWinChunks][0], 16,
-                                               lo - 16, 0, 0, 0);
-  };
-
-  prefetch(g0);
-  for (uint32_t g = g0; g < g_end; ++g) {
-    const uint32_t wave_base = g * kFramesPerWave;
-    const uint32_t f = wave_base + lane;
-    const bool live = f < a.n;
-    const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
-    // the window for g has landed (nothing else is outstanding here)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    Window h;
-#pragma unroll
-    for (int c = 0; c < kWinChunks; ++c) {
-      const u32x4 v = pre[c][lane];
-      h.d[4 * c + 0] = v.x;
-      h.d[4 * c + 1] = v.y;
-      h.d[4 * c + 2] = v.z;
-      h.d[4 * c + 3] = v.w;
-    }
-    uint32_t ether_type;
-    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
-    else ether_type = pre[kWinChunks][lane].w >> 16;
-    FrameState st = header_phase<MIS>(h, ether_type, live, a);
-    // The LDS image is consumed (its values are in registers); refill it for the next
-    // group now, after the probe (whose load would otherwise wait for the DMA, vmcnt
-    // being in-order) and ahead of the stream it hides behind.
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (g + 1 < g_end) prefetch(g + 1);
-    stream_phase<BATCH>(a, a.frames + (uint64_t)wave_base * a.stride + a.ipa_off, n_here, lane, st.end_rel, st.t_all);
-    if (live) finish<MIS>(a, st, f);
-  }
+  stream_phase<ABL, LAUX>(a, wave_slot + a.ipa_off, n_here, lane, st.end_rel, st.t_all);
+  if (live) finish<MIS, ABL, SAUX>(a, st, f);
 }
 
 __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src, uint64_t n16, uint32_t* sink) {
@@ -489,60 +431,43 @@ __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src
   if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc; // keeps the loads live; practically never stores
 }
 
-// Read-only ceilings for the slot layout (no header work, no arithmetic):
-// MODE 0: each wave streams the first `bytes` of each of its 64 slots with the RX
-//         kernel's 1-KiB buffer loads, 8 slots per batch;
-// MODE 1: "split" — line 0 of all 64 slots first (one lane per slot), then lines
-//         1.. of each slot in batches (the one-group kernel's access order);
-// MODE 2: "pipelined" — per batch, line 0 of the NEXT 8 slots (8 lanes per line)
-//         is fetched together with lines 1.. of the current 8 slots.
-template <int WPG, int MODE>
-__global__ __launch_bounds__(kWave* WPG) void calib_slot_read_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
-                                                                    uint32_t bytes, uint32_t* sink) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave_base = (blockIdx.x * WPG + wave) * kFramesPerWave;
+// Read-only ceilings for the slot layout (no header work, no arithmetic): each wave
+// streams the first `bytes` of each of its 64 slots with the RX kernel's 1-KiB
+// buffer loads, 8 slots per batch.  STORE = 16 / 8: plus a per-slot record store
+// of that many bytes at the wave's end (sink holds n x 16 B), the RX kernel's
+// write pattern.
+template <int STORE>
+__global__ __launch_bounds__(kWave) void calib_slot_read_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                               uint32_t bytes, uint32_t* sink) {
+  const int lane = threadIdx.x;
+  const uint32_t wave_base = blockIdx.x * kFramesPerWave;
   if (wave_base >= n) return;
   const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
   const uint8_t* wb = base + (uint64_t)wave_base * stride;
   uint32_t acc = 0;
-  const uint32_t first = MODE == 0 ? 0u : 128u;
-  if constexpr (MODE == 1) {
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb, n_here * stride);
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * stride + 16 * c, 0, 0);
-      acc ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-  }
-  u32x4 line0 = {0, 0, 0, 0};
-  if constexpr (MODE == 2) {
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb, n_here * stride);
-    line0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (lane >> 3) * stride + 16 * (lane & 7), 0, 0);
-  }
   for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
     u32x4 w0s[kBatch], w1s[kBatch];
-    u32x4 nxt = {0, 0, 0, 0};
-    if constexpr (MODE == 2) {
-      if (b0 + kBatch < n_here) {
-        const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb, n_here * stride);
-        nxt = __builtin_amdgcn_raw_buffer_load_b128(rs, (b0 + kBatch + (lane >> 3)) * stride + 16 * (lane & 7), 0, 0);
-      }
-    }
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
       const uint32_t nb = (b0 + j < n_here) ? bytes : 0u;
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, first + lane * 16, 0, 0);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, first + 1024 + lane * 16, 0, 0);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    acc ^= line0.x ^ line0.y ^ line0.z ^ line0.w;
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
-    line0 = nxt;
   }
-  if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+  if constexpr (STORE == 16) {
+    if (lane < (int)n_here) {
+      u32x4 r = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+      *reinterpret_cast<u32x4*>(sink + 4 * (uint64_t)(wave_base + lane)) = r;
+    }
+  } else if constexpr (STORE == 8) {
+    if (lane < (int)n_here) *reinterpret_cast<uint64_t*>(sink + 2 * (uint64_t)(wave_base + lane)) = ((uint64_t)acc << 32) | acc;
+  } else {
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+  }
 }
 
 } // namespace
@@ -571,25 +496,25 @@ int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
   return set_err(ctx, PN_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Whether the cooperative header-window load applies: 128-B aligned slot lines
+// with the IP header's 16-B chunk at line offset 16 (the default frame_off = 2
+// layout, and ef_vi's 10 + prefix for prefix <= 5).
+bool coop_layout(const KArgs& a) {
+  return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
+}
+
+template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux>
+void launch_one(const KArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX>), dim3((a.n + kFramesPerWave - 1) / kFramesPerWave),
+                     dim3(kWave), 0, s, a);
+}
+
 template <int MIS>
-void launch(const KArgs& a, uint32_t grid, hipStream_t s) {
-  hipLaunchKernelGGL((rx_classify_kernel<MIS>), dim3(grid), dim3(kWave * kWavesPerWG), 0, s, a);
-}
-
-// Tuning variants of the MIS=0 (default layout) kernel, A/B-timed in one process by
-// scripts/variants.py.  Not part of the public ABI.
-template <int BATCH, int WPG, int WIN = 0, int ABL = 0>
-void launch_variant(const KArgs& a, hipStream_t s) {
-  const uint32_t per_wg = kFramesPerWave * WPG;
-  hipLaunchKernelGGL((rx_classify_kernel<0, BATCH, WPG, WIN, ABL>), dim3((a.n + per_wg - 1) / per_wg), dim3(kWave * WPG),
-                     0, s, a);
-}
-
-template <int BATCH>
-void launch_groups_variant(KArgs a, uint32_t gpw, hipStream_t s) {
-  const uint32_t n_groups = (a.n + kFramesPerWave - 1) / kFramesPerWave;
-  a.gpw = gpw;
-  hipLaunchKernelGGL((rx_classify_groups_kernel<0, BATCH>), dim3((n_groups + gpw - 1) / gpw), dim3(kWave), 0, s, a);
+void launch(const KArgs& a, hipStream_t s) {
+  if constexpr (MIS + 16 + kWinBytes <= 128 + 16) {
+    if (coop_layout(a)) return launch_one<MIS, 1>(a, s);
+  }
+  launch_one<MIS, 0>(a, s);
 }
 } // namespace
 
@@ -671,21 +596,18 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
-  a.gpw = 1;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  const uint32_t frames_per_wg = kFramesPerWave * kWavesPerWG;
-  const uint32_t grid = (n + frames_per_wg - 1) / frames_per_wg;
   switch ((frame_off + 14) & 15) {
-    case 0: launch<0>(a, grid, s); break;
-    case 2: launch<2>(a, grid, s); break;
-    case 4: launch<4>(a, grid, s); break;
-    case 6: launch<6>(a, grid, s); break;
-    case 8: launch<8>(a, grid, s); break;
-    case 10: launch<10>(a, grid, s); break;
-    case 12: launch<12>(a, grid, s); break;
-    default: launch<14>(a, grid, s); break;
+    case 0: launch<0>(a, s); break;
+    case 2: launch<2>(a, s); break;
+    case 4: launch<4>(a, s); break;
+    case 6: launch<6>(a, s); break;
+    case 8: launch<8>(a, s); break;
+    case 10: launch<10>(a, s); break;
+    case 12: launch<12>(a, s); break;
+    default: launch<14>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify launch");
@@ -696,7 +618,6 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                         void* results_dev, void* stream, int variant) {
   if (!ctx || !ctx->tbl_dev || (frame_off + 14) % 16 != 0 || n == 0) return set_err(ctx, PN_EINVAL, "variant: bad args");
-  if (variant == 1 && (((frame_off + 14) & 127) >> 4) != 1) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
   KArgs a;
   a.frames = (const uint8_t*)frames_dev;
   a.out = (pn_result*)results_dev;
@@ -708,20 +629,19 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
-  a.gpw = 1;
   hipStream_t s = (hipStream_t)stream;
+  if ((variant & 1) && !coop_layout(a)) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
+  // Tuning variants of the MIS = 0 (ip at slot+16) kernel, A/B-timed in one process by
+  // scripts/variants.py; not part of the public header.  History: profiles/r01_experiments.
   switch (variant) {
-    case 0: launch_variant<8, 1>(a, s); break;            // one group per wave, per-lane window
-    case 1: launch_variant<8, 1, 2>(a, s); break;         // one group per wave, cooperative window
-    case 2: launch_groups_variant<8>(a, 2, s); break;     // groups per wave + LDS prefetch
-    case 3: launch_groups_variant<8>(a, 4, s); break;
-    case 4: launch_groups_variant<8>(a, 8, s); break;
-    case 5: launch_groups_variant<4>(a, 4, s); break;
-    case 6: launch_variant<8, 4>(a, s); break;            // 256-thread workgroups
-    case 11: launch_variant<8, 1, 0, 1>(a, s); break;     // timing-only ablations from here
-    case 12: launch_variant<8, 1, 0, 2>(a, s); break;
-    case 14: launch_variant<8, 1, 0, 4>(a, s); break;
-    case 17: launch_variant<8, 1, 0, 7>(a, s); break;
+    case 0: launch_one<0, 0>(a, s); break;                         // per-lane window
+    case 1: launch_one<0, 1>(a, s); break;                         // cooperative window (production here)
+    case 2: launch_one<0, 0, 0, 0, 0>(a, s); break;                // per-lane, default cache policy
+    case 3: launch_one<0, 1, 0, 0, 0>(a, s); break;                // cooperative, default cache policy
+    case 11: launch_one<0, 1, kAblNoProbe>(a, s); break;           // timing-only ablations from here
+    case 12: launch_one<0, 1, kAblNoReduce>(a, s); break;
+    case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
+    case 18: launch_one<0, 1, kAblNoStore>(a, s); break;
     default: return set_err(ctx, PN_EINVAL, "variant: unknown");
   }
   hipError_t e = hipGetLastError();
@@ -731,19 +651,17 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
 }
 
 int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
-                       int waves_per_wg, void* sink_dev, void* stream) {
+                       int store_bytes, void* sink_dev, void* stream) {
   if (!ctx || !src_dev || !sink_dev || (stride & 15) || bytes > stride || bytes > 2048 || n_slots == 0)
     return set_err(ctx, PN_EINVAL, "pn_calib_slot_read: bad arguments");
   hipStream_t s = (hipStream_t)stream;
   const uint32_t waves = (n_slots + kFramesPerWave - 1) / kFramesPerWave;
   const uint8_t* src = (const uint8_t*)src_dev;
   uint32_t* sink = (uint32_t*)sink_dev;
-  switch (waves_per_wg) { // >= 10: access-order experiments (mode = waves_per_wg / 10), 64-thread WGs
-    case 1: hipLaunchKernelGGL((calib_slot_read_kernel<1, 0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
-    case 11: hipLaunchKernelGGL((calib_slot_read_kernel<1, 1>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
-    case 21: hipLaunchKernelGGL((calib_slot_read_kernel<1, 2>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
-    default:
-      hipLaunchKernelGGL((calib_slot_read_kernel<4, 0>), dim3((waves + 3) / 4), dim3(256), 0, s, src, n_slots, stride, bytes, sink);
+  switch (store_bytes) {
+    case 16: hipLaunchKernelGGL((calib_slot_read_kernel<16>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 8: hipLaunchKernelGGL((calib_slot_read_kernel<8>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    default: hipLaunchKernelGGL((calib_slot_read_kernel<0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "calib slot launch");

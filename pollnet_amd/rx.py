@@ -240,8 +240,8 @@ class RxContext:
             "pn_classify",
         )
 
-    def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, waves_per_wg=1):
-        _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, waves_per_wg, _ptr(sink_dev),
+    def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, store_bytes=0):
+        _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, store_bytes, _ptr(sink_dev),
                               _stream_handle(stream)), self._h, "pn_calib_slot_read")
 
     def classify_variant(self, frames_dev, slot_stride, frame_off, n, results_dev, stream, variant):

@@ -10,10 +10,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-NAMES = {0: "onegroup_b8_wpg1", 1: "onegroup_coopwin", 2: "groups2_ldsprefetch", 3: "groups4_ldsprefetch",
-         4: "groups8_ldsprefetch", 5: "groups4_b4_ldsprefetch", 6: "onegroup_b8_wpg4",
-         11: "ABL_noprobe", 12: "ABL_noreduce", 14: "ABL_nomask", 17: "ABL_all3"}
-TIMING_ONLY = {11, 12, 14, 17}
+NAMES = {0: "perlane_window", 1: "coop_window", 2: "perlane_defaultpolicy", 3: "coop_defaultpolicy",
+         11: "ABL_noprobe", 12: "ABL_noreduce", 14: "ABL_nomask", 18: "ABL_nostore"}
+TIMING_ONLY = {11, 12, 14, 18}
 
 
 def main():
@@ -22,7 +21,8 @@ def main():
     ap.add_argument("--frames", type=int, default=1 << 20)
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="0,1,2,3,4,5")
+    ap.add_argument("--variants", default="0,1,2,3,18")
+    ap.add_argument("--uncached", action="store_true", help="frame ring from hipExtMallocWithFlags(Uncached)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -36,6 +36,24 @@ def main():
     ctx = pa.RxContext(0)
     ctx.set_conn_table(t)
     frames = torch.from_numpy(s.reshape(-1)).cuda()
+    if a.uncached:
+        import ctypes as C
+        hip = C.CDLL("libamdhip64.so.7")
+        ptr = C.c_void_p()
+        assert hip.hipExtMallocWithFlags(C.byref(ptr), C.c_size_t(frames.numel()), C.c_uint(0x3)) == 0  # Uncached
+        assert hip.hipMemcpy(ptr, C.c_void_p(frames.data_ptr()), C.c_size_t(frames.numel()), 3) == 0  # D2D
+
+        class Raw:  # minimal stand-in exposing data_ptr/numel for the bindings
+            def __init__(self, p, n):
+                self.p, self.n = p, n
+
+            def data_ptr(self):
+                return self.p
+
+            def numel(self):
+                return self.n
+
+        frames = Raw(ptr.value, frames.numel())
     ref = torch.empty(a.frames * 16, dtype=torch.uint8, device="cuda")
     res = torch.empty_like(ref)
     sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
@@ -50,9 +68,9 @@ def main():
             assert torch.equal(res, ref), f"variant {v} differs from production"
     times = {v: [] for v in vs}
     times["calib"] = []
-    SLOT_MODES = [(1536, 1), (1536, 4), (1536, 11), (1536, 21), (2048, 1)]
+    SLOT_MODES = [(1536, 0), (1536, 16), (1536, 8)]  # (bytes per slot, record store bytes)
     for b, wpg in SLOT_MODES:
-        times[f"slotread_{b}_m{wpg}"] = []
+        times[f"slotread_{b}_store{wpg}"] = []
     times["prod"] = []
     times["prod_b2b50"] = []
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -70,7 +88,8 @@ def main():
     for _ in range(a.rounds):
         times["calib"].append(timed(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, st)))
         for b, wpg in SLOT_MODES:
-            times[f"slotread_{b}_m{wpg}"].append(timed(lambda: ctx.calib_slot_read(frames, a.frames, 2048, b, sink, st, wpg)))
+            tgt = res if wpg else sink
+            times[f"slotread_{b}_store{wpg}"].append(timed(lambda: ctx.calib_slot_read(frames, a.frames, 2048, b, tgt, st, wpg)))
         times["prod"].append(timed(lambda: ctx.classify(frames, 2048, 2, a.frames, res, st)))
         r0 = a.reps
         a.reps = 50
