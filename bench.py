@@ -142,6 +142,31 @@ def e2e_rate(torch, ctx, slots, n, chunk=1 << 16, passes=3):
             "note": "pinned hipMemcpyAsync H2D of whole 2048-B slots + kernel + D2H records, 2 streams"}, host_res
 
 
+def ceilings(torch, ctx, frames, n, res, stream, reps=10):
+    """Same-run bandwidth ceilings (no arithmetic): a front-to-back stream read of the
+    whole ring, and the RX kernel's own load pattern over the first 1536 B of each slot
+    with and without its 16-B/frame record writes."""
+    sink = torch.zeros(4096, dtype=torch.int32, device=frames.device)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def t(fn):
+        fn()
+        ev[0].record(stream)
+        for _ in range(reps):
+            fn()
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) / reps * 1e-3
+
+    ts = t(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, stream))
+    t0 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, sink, stream, 0))
+    t16 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, res, stream, 16))
+    return {"stream_read_gbs": round(frames.numel() / ts / 1e9, 1),
+            "slot_pattern_read_gbs": round(n * 1536 / t0 / 1e9, 1),
+            "slot_pattern_read_plus_16B_records_ms": round(t16 * 1e3, 5),
+            "note": "calib kernels in pollnet_amd/csrc/rx_kernel.hip; no header work, no arithmetic"}
+
+
 def load_pmc_traffic(workload_key):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -268,6 +293,10 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
+    if rank == 0 and world == 1:
+        c = ceilings(torch, ctx, frames, n, res, stream)
+        c["kernel_vs_read_plus_records_ceiling"] = round(c["slot_pattern_read_plus_16B_records_ms"] / kern_ms, 4)
+        out["roofline"]["same_run_ceilings"] = c
     if rank == 0 and world == 1 and not args.no_e2e:
         try:
             out["e2e_pinned_host"], _ = e2e_rate(torch, ctx, slots, n)

@@ -247,3 +247,29 @@ def test_cpp_adapter_without_torch():
     assert os.path.exists(exe), "build with `make` first"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_cooperative_and_per_lane_windows_agree(torch_cuda, ctx, cfg):
+    """The kernel loads the header window cooperatively (one request per 128-B line) when
+    slot lines are 128-B aligned with ip at line+16, else per lane.  Shift the same ring
+    by 16 bytes to force the other path: records must be identical (and match the oracle)."""
+    p = pa.rx.GenParams.for_config(cfg)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = 3000
+    s = pa.gen_frames(p, n)
+    exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, threads=8)
+    ctx.set_conn_entries(e, m, t.max_conn_cnt)
+    outs = []
+    for shift in (0, 16, 32, 48):
+        buf = torch_cuda.zeros(n * STRIDE + 256, dtype=torch_cuda.uint8, device="cuda")
+        base = buf.data_ptr()
+        pad = (-base) % 128 + shift  # slots start `shift` bytes past a 128-B boundary
+        buf[pad:pad + n * STRIDE].copy_(torch_cuda.from_numpy(s.reshape(-1)))
+        res = torch_cuda.empty(n * 16, dtype=torch_cuda.uint8, device="cuda")
+        ctx.classify(base + pad, STRIDE, FRAME_OFF, n, res, torch_cuda.cuda.current_stream())
+        torch_cuda.cuda.synchronize()
+        outs.append(res.cpu().numpy().view(pa.RESULT_DTYPE).copy())
+    for o in outs:
+        assert_same(o, exp)
