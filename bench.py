@@ -293,7 +293,7 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and cfg in (2, 4):  # ceilings are for 1514-B frames (1536 B of lines per slot)
         c = ceilings(torch, ctx, frames, n, res, stream)
         c["kernel_vs_read_plus_records_ceiling"] = round(c["slot_pattern_read_plus_16B_records_ms"] / kern_ms, 4)
         out["roofline"]["same_run_ceilings"] = c
