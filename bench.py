@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg")
+    ap.add_argument("--batches", type=int, default=4,
+                    help="distinct resident batches the steps rotate over (defeats reuse of a fixed slice of "
+                         "the 256 MiB memory-side cache across launches)")
     return ap.parse_args()
 
 
@@ -142,7 +145,7 @@ def e2e_rate(torch, ctx, slots, n, chunk=1 << 16, passes=3):
             "note": "pinned hipMemcpyAsync H2D of whole 2048-B slots + kernel + D2H records, 2 streams"}, host_res
 
 
-def ceilings(torch, ctx, frames, n, res, stream, reps=10):
+def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, reps=10):
     """Same-run bandwidth ceilings (no arithmetic): a front-to-back stream read of the
     whole ring, and the RX kernel's own load pattern over the first 1536 B of each slot
     with and without its 16-B/frame record writes."""
@@ -159,12 +162,14 @@ def ceilings(torch, ctx, frames, n, res, stream, reps=10):
         return ev[0].elapsed_time(ev[1]) / reps * 1e-3
 
     ts = t(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, stream))
-    t0 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, sink, stream, 0))
-    t16 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, res, stream, 16))
-    return {"stream_read_gbs": round(frames.numel() / ts / 1e9, 1),
-            "slot_pattern_read_gbs": round(n * 1536 / t0 / 1e9, 1),
-            "slot_pattern_read_plus_16B_records_ms": round(t16 * 1e3, 5),
-            "note": "calib kernels in pollnet_amd/csrc/rx_kernel.hip; no header work, no arithmetic"}
+    out = {"stream_read_gbs": round(frames.numel() / ts / 1e9, 1),
+           "note": "calib kernels in pollnet_amd/csrc/rx_kernel.hip; no header work, no arithmetic"}
+    if slot_pattern:
+        t0 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, sink, stream, 0))
+        t16 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, res, stream, 16))
+        out["slot_pattern_read_gbs"] = round(n * 1536 / t0 / 1e9, 1)
+        out["slot_pattern_read_plus_16B_records_ms"] = round(t16 * 1e3, 5)
+    return out
 
 
 def load_pmc_traffic(workload_key):
@@ -203,15 +208,27 @@ def main():
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     gen_threads = max(1, min(16, (os.cpu_count() or 16) // max(1, local_world)))
     t0 = time.perf_counter()
-    slots = pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=lo, threads=gen_threads)
+    R = max(1, args.batches)
     table = pa.gen_conn_table(params)
     entries, mask = table.snapshot()
-    wire = pa.wire_bytes(slots, STRIDE, FRAME_OFF, n)
-    log(f"[rank {rank}] generated {n} frames ({wire / 1e9:.2f} GB wire) in {time.perf_counter() - t0:.1f}s")
-
     ctx = pa.RxContext(local_rank)
     ctx.set_conn_table(table)
-    frames = torch.from_numpy(slots.reshape(-1)).to(f"cuda:{local_rank}")
+    # R distinct batches per rank; batch b of rank r holds global frames [(b*world + r)*n, +n)
+    frames_b, wires = [], []
+    host = np.empty((n, STRIDE), dtype=np.uint8)
+    slots = None
+    for b in range(R):
+        first = (b * world + rank) * n if R > 1 else lo
+        pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=first, threads=gen_threads, out=host)
+        wires.append(pa.wire_bytes(host, STRIDE, FRAME_OFF, n))
+        frames_b.append(torch.from_numpy(host.reshape(-1)).to(f"cuda:{local_rank}"))
+        if b == 0:
+            slots = host.copy()  # batch 0 stays on the host: oracle check, CPU baseline, e2e leg
+    del host
+    wire = wires[0]
+    frames = frames_b[0]
+    log(f"[rank {rank}] generated {R} x {n} frames ({sum(wires) / 1e9:.2f} GB wire) in {time.perf_counter() - t0:.1f}s")
+
     res = torch.empty(n * 16, dtype=torch.uint8, device=f"cuda:{local_rank}")
     stream = torch.cuda.current_stream()
 
@@ -229,16 +246,16 @@ def main():
         if not verified:
             log("ERROR: GPU records differ from the oracle on the bench batch")
 
-    for _ in range(args.warmup):
-        ctx.classify(frames, STRIDE, FRAME_OFF, n, res, stream)
+    for w in range(args.warmup):
+        ctx.classify(frames_b[w % R], STRIDE, FRAME_OFF, n, res, stream)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        ctx.classify(frames, STRIDE, FRAME_OFF, n, res, stream)
+    for k in range(args.steps):
+        ctx.classify(frames_b[k % R], STRIDE, FRAME_OFF, n, res, stream)
     ev1.record(stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -254,17 +271,19 @@ def main():
         kern_ms_max = kern_ms
 
     total_frames = n * world * args.steps
-    total_wire = wire * world * args.steps  # each rank's shard has (statistically) equal bytes; exact for C2/C4
+    step_wire = float(sum(wires[k % R] for k in range(args.steps)))  # this rank's wire bytes over the K steps
+    total_wire = step_wire
     if world > 1:
-        wt = torch.tensor([float(wire)], dtype=torch.float64, device=f"cuda:{local_rank}")
+        wt = torch.tensor([step_wire], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(wt, op=dist.ReduceOp.SUM)
-        total_wire = float(wt[0]) * args.steps
+        total_wire = float(wt[0])
     gbit = total_wire * 8 / wall / 1e9
     mfps = total_frames / wall / 1e6
 
     out = None
     if rank == 0:
-        algo_bytes = wire + 16 * n  # every frame byte read once + the 16-B record written
+        # every frame byte read once + the 16-B record written, averaged over the launches timed
+        algo_bytes = int(step_wire / args.steps) + 16 * n
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         wl_key = f"c{cfg}_n{n}"
         traffic = load_pmc_traffic(wl_key)
@@ -283,7 +302,8 @@ def main():
             "dtype": "u16/u32 integer (one's-complement sums)",
             "data": "synthetic (deterministic seeded generator, pollnet_amd/csrc/framegen.cpp)",
             "config": {"workload": WORKLOADS[cfg], "frames_per_gpu": n, "slot_stride": STRIDE, "frame_off": FRAME_OFF,
-                       "parallelism": f"index-sharded x{world}, no collective", "global_frames": n * world},
+                       "parallelism": f"index-sharded x{world}, no collective", "global_frames": n * world,
+                       "resident_batches_per_gpu": R},
             "verified_vs_oracle": verified,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -293,9 +313,10 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
-    if rank == 0 and world == 1 and cfg in (2, 4):  # ceilings are for 1514-B frames (1536 B of lines per slot)
-        c = ceilings(torch, ctx, frames, n, res, stream)
-        c["kernel_vs_read_plus_records_ceiling"] = round(c["slot_pattern_read_plus_16B_records_ms"] / kern_ms, 4)
+    if rank == 0 and world == 1:  # the slot-pattern ceilings are for 1514-B frames (1536 B of lines per slot)
+        c = ceilings(torch, ctx, frames, n, res, stream, slot_pattern=cfg in (2, 4))
+        if cfg in (2, 4):
+            c["kernel_vs_read_plus_records_ceiling"] = round(c["slot_pattern_read_plus_16B_records_ms"] / kern_ms, 4)
         out["roofline"]["same_run_ceilings"] = c
     if rank == 0 and world == 1 and not args.no_e2e:
         try:

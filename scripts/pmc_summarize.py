@@ -51,18 +51,24 @@ def load_ea(dirpath):
 
 
 def main():
-    fdir, wdir, calib_bytes, wire, frames, key = sys.argv[1:7]
-    out = sys.argv[7] if len(sys.argv) > 7 else "profiles/pmc_traffic.json"
-    calib_bytes, wire, frames = int(calib_bytes), int(wire), int(frames)
-    fc, fk = load(fdir, "FETCH_SIZE")
-    wc, wk = load(wdir, "WRITE_SIZE")
+    """Usage: pmc_summarize.py <pass_root_dir> [out.json]  (pass dirs fetch/, write/, ea/, eaw/ + fetch.json bench line)"""
+    root = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+    with open(os.path.join(root, "fetch.json")) as f:
+        bench = json.loads(f.read().strip().splitlines()[-1])
+    n = bench["config"]["frames_per_gpu"]
+    cfg_key = "c" + bench["config"]["workload"].split(":")[0][1:] + f"_n{n}"
+    algo = bench["roofline"]["algorithmic_bytes_per_launch"]
+    calib_bytes = n * bench["config"]["slot_stride"]
+    fc, fk = load(os.path.join(root, "fetch"), "FETCH_SIZE")
+    wc, wk = load(os.path.join(root, "write"), "WRITE_SIZE")
     assert fc and fk and wk, (len(fc), len(fk), len(wk))
-    fetch_calib = statistics.median(fc) * 1024
-    factor = calib_bytes / fetch_calib
+    factor = calib_bytes / (statistics.median(fc) * 1024)
     read = statistics.median(fk) * 1024 * factor
     write = statistics.median(wk) * 1024
-    algo = wire + 16 * frames
     entry = {
+        "workload": bench["config"]["workload"],
+        "frames_per_launch": n,
         "fetch_size_kib_classify": statistics.median(fk),
         "write_size_kib_classify": statistics.median(wk),
         "fetch_size_kib_calib": statistics.median(fc),
@@ -73,14 +79,13 @@ def main():
         "hbm_bytes_per_launch": int(read + write),
         "algorithmic_bytes_per_launch": algo,
         "traffic_over_algorithmic": round((read + write) / algo, 4),
-        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH scaled by a "
-                  "same-run 16-B streaming-read calibration kernel over a known byte count",
+        "method": "bench.py under rocprofv3: --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH "
+                  "scaled by the same run's 16-B streaming-read calibration kernel over a known byte count",
     }
-    base = os.path.dirname(os.path.normpath(fdir))
     ea = {}
     for sub in ("ea", "eaw"):
-        if os.path.isdir(os.path.join(base, sub)):
-            ea.update(load_ea(os.path.join(base, sub)))
+        if os.path.isdir(os.path.join(root, sub)):
+            ea.update(load_ea(os.path.join(root, sub)))
     if ea:
         rd = 32 * ea.get("TCC_EA0_RDREQ_32B_sum", 0) + 64 * ea.get("TCC_EA0_RDREQ_64B_sum", 0) + \
             128 * ea.get("TCC_EA0_RDREQ_128B_sum", 0)
@@ -88,15 +93,18 @@ def main():
         wr = 64 * wr64 + 32 * (ea.get("TCC_EA0_WRREQ_sum", wr64) - wr64)
         entry["ea_request_counters"] = {k: ea[k] for k in sorted(ea)}
         entry["ea_bytes_per_launch"] = int(rd + wr)
-        entry["ea_read_lines_per_frame"] = round(ea.get("TCC_EA0_RDREQ_128B_sum", 0) / frames, 4)
+        entry["ea_read_lines_per_frame"] = round(ea.get("TCC_EA0_RDREQ_128B_sum", 0) / n, 4)
+        if "TCC_EA0_RDREQ_DRAM_sum" in ea:
+            entry["dram_read_requests_over_all_read_requests"] = round(
+                ea["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, ea.get("TCC_EA0_RDREQ_sum", 1.0)), 4)
     d = {}
     if os.path.exists(out):
         with open(out) as f:
             d = json.load(f)
-    d[key] = entry
+    d[cfg_key] = entry
     with open(out, "w") as f:
         json.dump(d, f, indent=1)
-    print(json.dumps({key: entry}, indent=1))
+    print(json.dumps({cfg_key: entry}, indent=1))
 
 
 if __name__ == "__main__":
