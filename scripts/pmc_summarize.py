@@ -94,9 +94,6 @@ def main():
         entry["ea_request_counters"] = {k: ea[k] for k in sorted(ea)}
         entry["ea_bytes_per_launch"] = int(rd + wr)
         entry["ea_read_lines_per_frame"] = round(ea.get("TCC_EA0_RDREQ_128B_sum", 0) / n, 4)
-        if "TCC_EA0_RDREQ_DRAM_sum" in ea:
-            entry["dram_read_requests_over_all_read_requests"] = round(
-                ea["TCC_EA0_RDREQ_DRAM_sum"] / max(1.0, ea.get("TCC_EA0_RDREQ_sum", 1.0)), 4)
     d = {}
     if os.path.exists(out):
         with open(out) as f:
