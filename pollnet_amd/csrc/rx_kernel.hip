@@ -148,9 +148,11 @@ using Window = Win<4 * kWinChunks>;
 struct FrameState {
   uint32_t flags, ihl, tot_len, src_ip, dst_ip, seq_raw, doff, tflags, s_ip20, s_opt, tcp_len, conn_id;
   uint32_t t_all; // exact u16-word sum of [ip, ip+20+tcp_len(+pad)) accumulated so far
-  int end_rel;    // summed extent relative to the window start, 0 when nothing to stream
+  int end_rel;    // summed extent relative to the window start (even), | 1 when tcp_len is odd; 0 = nothing to stream
+  uint32_t pad;   // odd tcp_len: the byte after the segment (kPadUnknown until phase 2 captured it)
   bool trunc;
 };
+constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
 
 // Timing-only ablations (scripts/variants.py; records are wrong when set):
 // bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
@@ -191,15 +193,17 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   const uint32_t seg_even = (st.tcp_len + 1) & ~1u;
   st.trunc = 34 + seg_even > a.avail;
   if (st.trunc) flags |= PN_F_TRUNC;
-  // summed region relative to the window: [MIS, MIS + 20 + seg_even)
-  st.end_rel = (live && !st.trunc) ? (int)(MIS + 20 + seg_even) : 0;
+  // summed region relative to the window: [MIS, MIS + 20 + seg_even); bit 0 flags an odd
+  // tcp_len, whose last summed byte (end - 1) is the byte after the segment
+  st.end_rel = (live && !st.trunc) ? (int)((MIS + 20 + seg_even) | (st.tcp_len & 1)) : 0;
+  st.pad = kPadUnknown;
 
   // the part of the region inside the window, summed from registers
   uint32_t t = 0;
 #pragma unroll
   for (int q = MIS / 4; q < 4 * kWinChunks; ++q) {
     const uint32_t start_sel = ((4 * q >= MIS) ? 1u : 0u) | ((4 * q + 2 >= MIS) ? 0x10000u : 0u);
-    t = dot2(h.d[q], tail_sel(st.end_rel, 4 * q) & start_sel, t);
+    t = dot2(h.d[q], tail_sel(st.end_rel & ~1, 4 * q) & start_sel, t);
   }
   st.t_all = t;
 
@@ -235,7 +239,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 // frame with readlane); the total of frame fi lands on lane fi.
 template <int ABL, int LAUX>
 __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* group_ipa, uint32_t n_here, int lane,
-                                             int end_rel, uint32_t& t_all) {
+                                             int end_rel, uint32_t& t_all, uint32_t& pad) {
   for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
     uint32_t acc[kBatch];
     int ends[kBatch];
@@ -244,7 +248,7 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
       const uint32_t fi = b0 + j; // wave-uniform
-      const int end = __builtin_amdgcn_readlane(end_rel, fi & 63);
+      const int end = __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1; // bit 0 = odd tcp_len, read below
       ends[j] = end;
       const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(group_ipa + (uint64_t)fi * a.stride, end16);
@@ -272,6 +276,17 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
       sum = dot2(w1.z, sel(end, o1 + 8), sum);
       sum = dot2(w1.w, sel(end, o1 + 12), sum);
       acc[j] = sum;
+      // odd tcp_len: the RFC verdict needs the byte the reference sums past the segment (window
+      // offset end - 1); take it from the lane that streamed it instead of re-reading the line later
+      const int p = end - 1;
+      if ((__builtin_amdgcn_readlane(end_rel, (b0 + j) & 63) & 1) && p >= kWinBytes && p < kWinBytes + 2048) {
+        const int q = p - kWinBytes;                 // wave-uniform
+        const u32x4 w = (q < 1024) ? w0 : w1;
+        const int dw = (q >> 2) & 3;
+        const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
+        const uint32_t b = __builtin_amdgcn_readlane((d >> (8 * (q & 3))) & 0xff, (q & 1023) >> 4);
+        if ((uint32_t)lane == b0 + j) pad = b;
+      }
     }
     // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
 #pragma unroll
@@ -337,9 +352,10 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
     if (st.ihl >= 5 && hl <= st.tot_len) {
       if (csum_fold(st.s_ip20 + st.s_opt) == 0) flags |= PN_F_RFC_IP_OK;
       uint32_t pad = 0;
-      if (st.tot_len & 1) {
-        const uint8_t* ip = a.frames + (uint64_t)f * a.stride + a.ipa_off + MIS;
-        pad = (uint32_t)ip[st.tot_len] << 8; // the byte the reference sums past the segment
+      if (st.tot_len & 1) { // the byte the reference sums past the segment (high half of the last word)
+        uint32_t b = st.pad;
+        if (b == kPadUnknown) b = (a.frames + (uint64_t)f * a.stride + a.ipa_off + MIS)[st.tot_len]; // in-window / jumbo
+        pad = b << 8;
       }
       const uint32_t rfc = s_addr + 0x0600 + bswap16(st.tot_len - hl) + (s_seg - st.s_opt - pad);
       if (csum_fold(rfc) == 0) flags |= PN_F_RFC_TCP_OK;
@@ -417,7 +433,7 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0) ? 5 : 4) void rx_classify_ker
     else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, LAUX) >> 16; // ipa_off >= 16 here
   }
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live, a);
-  stream_phase<ABL, LAUX>(a, wave_slot + a.ipa_off, n_here, lane, st.end_rel, st.t_all);
+  stream_phase<ABL, LAUX>(a, wave_slot + a.ipa_off, n_here, lane, st.end_rel, st.t_all, st.pad);
   if (live) finish<MIS, ABL, SAUX>(a, st, f);
 }
 
