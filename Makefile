@@ -13,8 +13,20 @@ ORACLE = oracle/liboracle.so
 REFDIR ?= /root/reference
 
 CPPTEST = tests/cpp/test_gpu_rx
+RXCONNTEST = tests/cpp/test_rx_conn
+TCPRXTEST = tests/cpp/test_gpu_tcp_rx
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST)
+all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST)
+
+# receive-side server loop on the GPU vs a sequential twin with reference semantics
+$(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
+  include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# receive-side state machine (host only): scenarios + differential vs the reference TcpStream
+$(RXCONNTEST): tests/cpp/test_rx_conn.cpp tests/cpp/segframes.hpp include/pollnet_amd/rx_conn.hpp $(HDRS) $(ORACLE)
+	g++ -O2 -std=c++17 -Wall -o $@ $< -Loracle -loracle -ldl -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # standalone C++ adapter test (no torch): links the product library and, as the checker, the oracle
 $(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
@@ -31,6 +43,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST)
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST)
 
 .PHONY: all ref clean

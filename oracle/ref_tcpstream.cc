@@ -47,3 +47,33 @@ int ref_handle_packet(const uint8_t* eth, uint32_t size, uint32_t* payload_off, 
   return 1;
 }
 }
+
+// ---- stateful stream (test-only): the reference's reassembly driven packet by packet ----
+// The handler consumes whole msg_len-byte messages (msg_len 0: everything) and logs
+// each call's size and the consumed bytes, so a test can compare the exact sequence
+// of deliveries with another implementation.
+extern "C" {
+struct ref_stream_log {
+  uint8_t* bytes;      // consumed bytes, appended
+  uint64_t n_bytes;
+  uint64_t cap_bytes;
+  uint32_t* call_sizes; // size presented by each handler call
+  uint32_t n_calls;
+  uint32_t cap_calls;
+};
+
+void* ref_stream_new(void) { return new Stream(); }
+void ref_stream_free(void* s) { delete static_cast<Stream*>(s); }
+
+int ref_stream_handle(void* s, const uint8_t* eth, uint32_t size, uint32_t msg_len, ref_stream_log* log) {
+  return static_cast<Stream*>(s)->handlePacket(eth, size, [&](const uint8_t* data, uint32_t n) -> uint32_t {
+    const uint32_t keep = msg_len ? n % msg_len : 0;
+    if (log->n_calls < log->cap_calls) log->call_sizes[log->n_calls] = n;
+    log->n_calls++;
+    const uint32_t take = n - keep;
+    if (log->n_bytes + take <= log->cap_bytes) std::memcpy(log->bytes + log->n_bytes, data, take);
+    log->n_bytes += take;
+    return keep;
+  }) ? 1 : 0;
+}
+}
