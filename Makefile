@@ -15,8 +15,15 @@ REFDIR ?= /root/reference
 CPPTEST = tests/cpp/test_gpu_rx
 RXCONNTEST = tests/cpp/test_rx_conn
 TCPRXTEST = tests/cpp/test_gpu_tcp_rx
+TCPRXBENCH = bench/bench_tcp_rx
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST)
+all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH)
+
+# poll() throughput (GPU-classified) vs the same host loop over the CPU release path
+$(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
+  include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
 # receive-side server loop on the GPU vs a sequential twin with reference semantics
 $(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
@@ -43,6 +50,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST)
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH)
 
 .PHONY: all ref clean

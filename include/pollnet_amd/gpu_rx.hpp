@@ -1,9 +1,9 @@
 // gpu_rx.hpp — header-only C++ host adapter over the pn_* C-ABI.
 //
 // Mirrors the RX branch of efvitcp's Core<Conf>::pollNet (efvitcp/Core.h:494-552)
-// for a batch of ring slots: one GPU launch classifies the whole batch, then the
-// records are dispatched on the host in ring order exactly where the reference
-// would have branched:
+// for a run of ring slots: GPU launches classify it chunk by chunk (chunk k+1 on the
+// GPU while chunk k is dispatched), and the records are dispatched on the host in
+// ring order exactly where the reference would have branched:
 //   - TIME_WAIT hit (entry->key == key && conn_id >= MaxConnCnt, Core.h:510)
 //       -> tw_handler(key, tw_id, eth, rec)            (reference: :511-523)
 //   - otherwise -> recv_handler(key, entry_index, eth, rec)   (reference: :526)
@@ -20,6 +20,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 
@@ -60,6 +61,13 @@ class ConnTable {
 
 class GpuRx {
  public:
+  // Copy: pollBatch copies the slots H2D, classifies in device memory and copies the
+  //   records back (any host memory; pinned copies fastest).
+  // ZeroCopy: the kernel reads the slots straight from pinned host memory over PCIe
+  //   (hipHostMalloc / hipHostRegister'd) and writes the records to pinned memory —
+  //   only the frames' own cache lines cross the bus, no slot padding, no copy stage.
+  enum class Mode { Copy, ZeroCopy };
+
   GpuRx() = default;
   GpuRx(const GpuRx&) = delete;
   GpuRx& operator=(const GpuRx&) = delete;
@@ -67,19 +75,27 @@ class GpuRx {
 
   // device: GPU ordinal; slot_stride/frame_off: the ring layout (RecvBufSize = 2048,
   // frame_off = sizeof(RecvBuf) + receive_prefix_len in the reference); max_batch:
-  // the largest n passed to pollBatch().
-  const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch) {
+  // the chunk pollBatch() classifies per launch (two chunks are in flight at once).
+  const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, Mode mode = Mode::Copy) {
     destruct();
+    if (max_batch == 0) return "max_batch must be > 0";
     if (pn_open(device, &ctx_)) return pn_last_error(nullptr);
     stride_ = slot_stride;
     off_ = frame_off;
     cap_ = max_batch;
+    mode_ = mode;
     if (hipSetDevice(device) != hipSuccess) return "hipSetDevice failed";
     if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return "hipStreamCreate failed";
-    if (hipMalloc(&d_frames_, (size_t)slot_stride * max_batch) != hipSuccess) return "hipMalloc(frames) failed";
-    if (hipMalloc(&d_res_, sizeof(pn_result) * (size_t)max_batch) != hipSuccess) return "hipMalloc(results) failed";
-    if (hipHostMalloc(&h_res_, sizeof(pn_result) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
-      return "hipHostMalloc(results) failed";
+    for (int b = 0; b < 2; b++) {
+      if (mode == Mode::Copy) {
+        if (hipMalloc(&d_frames_[b], (size_t)slot_stride * max_batch) != hipSuccess) return "hipMalloc(frames) failed";
+        if (hipMalloc(&d_res_[b], sizeof(pn_result) * (size_t)max_batch) != hipSuccess)
+          return "hipMalloc(results) failed";
+      }
+      if (hipHostMalloc(&h_res_[b], sizeof(pn_result) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
+        return "hipHostMalloc(results) failed";
+      if (hipEventCreateWithFlags(&done_[b], hipEventDisableTiming) != hipSuccess) return "hipEventCreate failed";
+    }
     return nullptr;
   }
 
@@ -92,34 +108,43 @@ class GpuRx {
     return pn_set_conn_table(ctx_, e, n, mask, max_conn_) ? pn_last_error(ctx_) : nullptr;
   }
 
-  // Classify n slots of the host ring (pinned memory copies fastest) and dispatch.
+  // Classify n slots of the host ring and dispatch every record in ring order.  The
+  // slots go in chunks of max_batch; chunk k+1 is on the GPU while chunk k is
+  // dispatched on the host.
   // recv_handler(uint64_t key, const pn_result& rec, const uint8_t* eth, uint32_t miss_entry_idx)
   // tw_handler(uint64_t key, uint32_t tw_id, const uint8_t* eth, const pn_result& rec)
   template <class RecvHandler, class TwHandler>
   const char* pollBatch(const uint8_t* host_slots, uint32_t n, const ConnTable& table, RecvHandler&& recv_handler,
                         TwHandler&& tw_handler) {
-    if (n > cap_) return "batch larger than max_batch";
     if (n == 0) return nullptr;
-    if (hipMemcpyAsync(d_frames_, host_slots, (size_t)stride_ * n, hipMemcpyHostToDevice, stream_) != hipSuccess)
-      return "hipMemcpyAsync H2D failed";
-    if (pn_classify(ctx_, d_frames_, stride_, off_, n, d_res_, stream_)) return pn_last_error(ctx_);
-    if (hipMemcpyAsync(h_res_, d_res_, sizeof(pn_result) * n, hipMemcpyDeviceToHost, stream_) != hipSuccess)
-      return "hipMemcpyAsync D2H failed";
-    if (hipStreamSynchronize(stream_) != hipSuccess) return "hipStreamSynchronize failed";
-    for (uint32_t i = 0; i < n; i++) {
-      const uint8_t* eth = host_slots + (size_t)i * stride_ + off_;
-      const pn_result& r = h_res_[i];
-      uint32_t ip_be;
-      uint16_t port_be;
-      std::memcpy(&ip_be, eth + 14 + 12, 4);  // ip_hdr->src_ip
-      std::memcpy(&port_be, eth + 14 + 20, 2); // tcp_hdr->src_port (tcp = ip + 20)
-      const uint64_t key = pn_conn_hash_key(ip_be, port_be);
-      if (r.flags & PN_F_TW) {
-        tw_handler(key, r.conn_id - max_conn_, eth, r);
-      } else {
-        uint32_t idx = PN_MISS;
-        if (!(r.flags & PN_F_HIT)) table.find(key, &idx, nullptr);
-        recv_handler(key, r, eth, idx);
+    if (mode_ == Mode::ZeroCopy) {
+      hipPointerAttribute_t attr;
+      if (hipPointerGetAttributes(&attr, host_slots) != hipSuccess || attr.type != hipMemoryTypeHost)
+        return "zero-copy ring must be pinned host memory (hipHostMalloc / hipHostRegister)";
+    }
+    const uint32_t chunks = (n + cap_ - 1) / cap_;
+    if (const char* e = launch(host_slots, n, 0)) return e;
+    for (uint32_t k = 0; k < chunks; k++) {
+      if (k + 1 < chunks)
+        if (const char* e = launch(host_slots, n, k + 1)) return e;
+      if (hipEventSynchronize(done_[k & 1]) != hipSuccess) return "hipEventSynchronize failed";
+      const uint32_t base = k * cap_, m = std::min(cap_, n - base);
+      const pn_result* res = h_res_[k & 1];
+      for (uint32_t i = 0; i < m; i++) {
+        const uint8_t* eth = host_slots + (size_t)(base + i) * stride_ + off_;
+        const pn_result& r = res[i];
+        uint32_t ip_be;
+        uint16_t port_be;
+        std::memcpy(&ip_be, eth + 14 + 12, 4);  // ip_hdr->src_ip
+        std::memcpy(&port_be, eth + 14 + 20, 2); // tcp_hdr->src_port (tcp = ip + 20)
+        const uint64_t key = pn_conn_hash_key(ip_be, port_be);
+        if (r.flags & PN_F_TW) {
+          tw_handler(key, r.conn_id - max_conn_, eth, r);
+        } else {
+          uint32_t idx = PN_MISS;
+          if (!(r.flags & PN_F_HIT)) table.find(key, &idx, nullptr);
+          recv_handler(key, r, eth, idx);
+        }
       }
     }
     return nullptr;
@@ -127,26 +152,51 @@ class GpuRx {
 
   pn_ctx* ctx() { return ctx_; }
   hipStream_t stream() { return stream_; }
+  Mode mode() const { return mode_; }
 
  private:
+  // Issue chunk k (H2D + classify + D2H, or one zero-copy classify) into buffer k&1.
+  const char* launch(const uint8_t* host_slots, uint32_t n, uint32_t k) {
+    const uint32_t base = k * cap_, m = std::min(cap_, n - base), b = k & 1;
+    const uint8_t* src = host_slots + (size_t)base * stride_;
+    if (mode_ == Mode::ZeroCopy) {
+      if (pn_classify(ctx_, src, stride_, off_, m, h_res_[b], stream_)) return pn_last_error(ctx_);
+    } else {
+      if (hipMemcpyAsync(d_frames_[b], src, (size_t)stride_ * m, hipMemcpyHostToDevice, stream_) != hipSuccess)
+        return "hipMemcpyAsync H2D failed";
+      if (pn_classify(ctx_, d_frames_[b], stride_, off_, m, d_res_[b], stream_)) return pn_last_error(ctx_);
+      if (hipMemcpyAsync(h_res_[b], d_res_[b], sizeof(pn_result) * m, hipMemcpyDeviceToHost, stream_) != hipSuccess)
+        return "hipMemcpyAsync D2H failed";
+    }
+    if (hipEventRecord(done_[b], stream_) != hipSuccess) return "hipEventRecord failed";
+    return nullptr;
+  }
+
   void destruct() {
-    if (h_res_) (void)hipHostFree(h_res_);
-    if (d_res_) (void)hipFree(d_res_);
-    if (d_frames_) (void)hipFree(d_frames_);
+    if (stream_) (void)hipStreamSynchronize(stream_);
+    for (int b = 0; b < 2; b++) {
+      if (done_[b]) (void)hipEventDestroy(done_[b]);
+      if (h_res_[b]) (void)hipHostFree(h_res_[b]);
+      if (d_res_[b]) (void)hipFree(d_res_[b]);
+      if (d_frames_[b]) (void)hipFree(d_frames_[b]);
+      done_[b] = nullptr;
+      h_res_[b] = nullptr;
+      d_res_[b] = nullptr;
+      d_frames_[b] = nullptr;
+    }
     if (stream_) (void)hipStreamDestroy(stream_);
     pn_close(ctx_);
-    h_res_ = nullptr;
-    d_res_ = nullptr;
-    d_frames_ = nullptr;
     stream_ = nullptr;
     ctx_ = nullptr;
   }
 
   pn_ctx* ctx_ = nullptr;
   hipStream_t stream_ = nullptr;
-  void* d_frames_ = nullptr;
-  pn_result* d_res_ = nullptr;
-  pn_result* h_res_ = nullptr;
+  Mode mode_ = Mode::Copy;
+  void* d_frames_[2] = {nullptr, nullptr};
+  pn_result* d_res_[2] = {nullptr, nullptr};
+  pn_result* h_res_[2] = {nullptr, nullptr};
+  hipEvent_t done_[2] = {nullptr, nullptr};
   uint32_t stride_ = 0, off_ = 0, cap_ = 0, max_conn_ = 0;
 };
 

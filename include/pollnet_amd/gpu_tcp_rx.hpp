@@ -55,12 +55,13 @@ class GpuTcpRx {
 
   GpuTcpRx() : conns_(Conf::MaxConnCnt) {}
 
-  // device / ring layout as GpuRx::init; the table holds MaxConnCnt connections and
-  // MaxTimeWaitConnCnt TIME_WAIT entries (Core.h:780-781).
-  const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch) {
+  // device / ring layout / chunk / mode as GpuRx::init; the table holds MaxConnCnt
+  // connections and MaxTimeWaitConnCnt TIME_WAIT entries (Core.h:780-781).
+  const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch,
+                   GpuRx::Mode mode = GpuRx::Mode::Copy) {
     const char* e = table_.init(Conf::MaxConnCnt, Conf::MaxTimeWaitConnCnt);
     if (e) return e;
-    if ((e = rx_.init(device, slot_stride, frame_off, max_batch))) return e;
+    if ((e = rx_.init(device, slot_stride, frame_off, max_batch, mode))) return e;
     free_.clear();
     for (uint32_t i = Conf::MaxConnCnt; i-- > 0;) free_.push_back(i);
     dirty_ = true;
@@ -116,6 +117,8 @@ class GpuTcpRx {
   GpuRx& rx() { return rx_; }
 
   // Classify n ring slots (host memory) on the GPU and dispatch them in ring order.
+  // The table snapshot is refreshed here, never while a chunk is in flight; chunks
+  // classified before a change made during this poll are re-resolved on the host.
   template <class Handler>
   const char* poll(Handler& h, const uint8_t* slots, uint32_t n) {
     if (dirty_) {

@@ -576,6 +576,12 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
     return set_err(ctx, PN_EINVAL, "pn_set_conn_table: tbl_mask must be 2^k-1 < n_entries");
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  // a classify launched on this ctx may still be reading the table: let it finish
+  // before the snapshot is replaced (the copy below is not ordered against that stream)
+  if (ctx->tbl_dev) {
+    e = hipStreamSynchronize(ctx->last_stream);
+    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(last classify)");
+  }
   if (n_entries > ctx->n_entries) {
     if (ctx->tbl_dev) (void)hipFree(ctx->tbl_dev);
     ctx->tbl_dev = nullptr;

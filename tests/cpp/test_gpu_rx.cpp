@@ -11,7 +11,7 @@
 #include "../../include/pollnet_amd/gpu_rx.hpp"
 #include "../../oracle/pn_oracle.h"
 
-static int run(uint32_t cfg, uint32_t n) {
+static int run(uint32_t cfg, uint32_t n, pollnet_amd::GpuRx::Mode mode, uint32_t chunk) {
   pn_gen_params p{};
   p.cfg = cfg;
   p.n_flows = cfg == 2 ? 1 : 1024;
@@ -35,7 +35,7 @@ static int run(uint32_t cfg, uint32_t n) {
     if (ents[i].key != PN_EMPTY_KEY) table.add(ents[i].key, ents[i].conn_id);
   pn_table_destroy(raw);
   pollnet_amd::GpuRx rx;
-  if (const char* err = rx.init(0, stride, off, n)) {
+  if (const char* err = rx.init(0, stride, off, chunk, mode)) {
     std::printf("init: %s\n", err);
     return 6;
   }
@@ -77,17 +77,24 @@ static int run(uint32_t cfg, uint32_t n) {
     if (std::memcmp(&got[k], &exp[k], sizeof(pn_result))) diff++;
     if (exp[k].flags & PN_F_TW) exp_tw++;
   }
-  std::printf("cfg %u: n=%u recv=%u tw=%u (expected tw %u) misses=%u diff=%u bad_idx=%u\n", cfg, n, recv_calls,
-              tw_calls, exp_tw, misses, diff, bad_idx);
+  std::printf("cfg %u (%s, chunk %u): n=%u recv=%u tw=%u (expected tw %u) misses=%u diff=%u bad_idx=%u\n", cfg,
+              mode == pollnet_amd::GpuRx::Mode::ZeroCopy ? "zero-copy" : "copy", chunk, n, recv_calls, tw_calls, exp_tw,
+              misses, diff, bad_idx);
   (void)hipHostFree(ring);
   return (diff || bad_idx || tw_calls != exp_tw || i != n) ? 1 : 0;
 }
 
 int main() {
   int rc = 0;
-  rc |= run(2, 100000);
-  rc |= run(3, 100000);
-  rc |= run(5, 50000);
+  using M = pollnet_amd::GpuRx::Mode;
+  rc |= run(2, 100000, M::Copy, 100000);
+  rc |= run(3, 100000, M::Copy, 100000);
+  rc |= run(5, 50000, M::Copy, 50000);
+  // chunked pipeline (ragged last chunk) and the zero-copy mode
+  rc |= run(3, 100000, M::Copy, 7777);
+  rc |= run(3, 100000, M::ZeroCopy, 100000);
+  rc |= run(5, 50000, M::ZeroCopy, 4096);
+  rc |= run(2, 100000, M::ZeroCopy, 333);
   std::printf(rc ? "FAIL\n" : "PASS\n");
   return rc;
 }

@@ -179,7 +179,11 @@ struct Twin {
 };
 
 int main(int argc, char** argv) {
+  // argv: batch [twin | copy | zc] [span]: `span` polls the whole ring in one call
+  // (chunks of `batch` pipelined inside GpuRx) instead of one poll per batch
   const uint32_t n_flows = 200, n_tw = 8, batch = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 1000;
+  const bool zero_copy = argc > 2 && std::strcmp(argv[2], "zc") == 0;
+  const bool span = argc > 3 && std::strcmp(argv[3], "span") == 0;
   const uint32_t stride = 2048, off = 2;
   std::mt19937_64 rng(0x7C9E5EEDull);
   auto U = [&](uint32_t lo, uint32_t hi) { return lo + (uint32_t)(rng() % (hi - lo + 1)); };
@@ -288,8 +292,9 @@ int main(int argc, char** argv) {
       auto* c = srv.accept(pn_conn_hash_key(htonl(F.ip), htons(F.port)), F.isn);
       if (!c || srv.enterTW(*c, t) != PN_OK) return false;
     }
-    for (uint32_t b = 0; b < n; b += batch) {
-      if (!poll_fn(h, ring + (size_t)b * stride, std::min(batch, n - b))) return false;
+    const uint32_t step = span ? n : batch;
+    for (uint32_t b = 0; b < n; b += step) {
+      if (!poll_fn(h, ring + (size_t)b * stride, std::min(step, n - b))) return false;
     }
     log_out = std::move(h.log);
     got.clear();
@@ -314,7 +319,7 @@ int main(int argc, char** argv) {
   }
 
   auto gpu = std::make_unique<GpuTcpRx<Conf>>();
-  if (const char* e = gpu->init(0, stride, off, batch)) {
+  if (const char* e = gpu->init(0, stride, off, batch, zero_copy ? GpuRx::Mode::ZeroCopy : GpuRx::Mode::Copy)) {
     std::printf("init: %s\n", e);
     return 4;
   }
@@ -346,6 +351,7 @@ int main(int argc, char** argv) {
   }
   size_t cnt[6] = {};
   for (auto& e : glog) cnt[e.type]++;
+  std::printf("%s%s: ", zero_copy ? "zero-copy" : "copy", span ? ", one poll over the ring" : "");
   std::printf("frames %u in batches of %u: %zu events (data %zu, disconnect %zu, ack %zu, new %zu, tw %zu); "
               "%u/%u streams (%u B) intact; conns left %u\n",
               n, batch, glog.size(), cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], streams_ok, n_flows, bytes,

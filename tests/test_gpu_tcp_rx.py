@@ -15,9 +15,12 @@ BIN = os.path.join(ROOT, "tests", "cpp", "test_gpu_tcp_rx")
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch", [1000, 64, 1, 8192])
-def test_gpu_tcp_rx_matches_sequential_twin(batch):
+@pytest.mark.parametrize("batch,mode,span", [(1000, "copy", ""), (64, "copy", ""), (1, "copy", ""),
+                                             (8192, "zc", ""), (1000, "zc", ""), (64, "zc", "span"),
+                                             (700, "copy", "span")])
+def test_gpu_tcp_rx_matches_sequential_twin(batch, mode, span):
     assert os.path.exists(BIN), "tests/cpp/test_gpu_tcp_rx not built (make)"
-    p = subprocess.run([BIN, str(batch)], capture_output=True, text=True, timeout=300)
+    p = subprocess.run([BIN, str(batch), mode] + ([span] if span else []), capture_output=True, text=True,
+                       timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout and "200/200 streams" in p.stdout, p.stdout
