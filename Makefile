@@ -16,8 +16,14 @@ CPPTEST = tests/cpp/test_gpu_rx
 RXCONNTEST = tests/cpp/test_rx_conn
 TCPRXTEST = tests/cpp/test_gpu_tcp_rx
 TCPRXBENCH = bench/bench_tcp_rx
+RINGTEST = tests/cpp/test_rx_ring
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH)
+all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST)
+
+# RX-ring ingestion: socket batcher (+ loopback capture when permitted), ef_vi event rings on the GPU
+$(RINGTEST): tests/cpp/test_rx_ring.cpp include/pollnet_amd/rx_ring.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # poll() throughput (GPU-classified) vs the same host loop over the CPU release path
 $(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
@@ -50,6 +56,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH)
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST)
 
 .PHONY: all ref clean

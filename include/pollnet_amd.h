@@ -78,6 +78,8 @@ typedef struct pn_result {
                                    (TcpStream.h:45-46; efvitcp itself trusts the NIC filter, Core.h:375-383) */
 #define PN_F_TRUNC 0x2000u      /* ip+20+tcp_len(+pad) exceeds the slot: the reference would read past
                                    the frame (undefined); TCP_OK/RFC_TCP_OK cleared, tcp_fold=0xFFFF */
+#define PN_F_BADOFF 0x4000u     /* pn_classify_indexed: offset outside the call's eth_mod16 class; the
+                                   frame was not read and the record is {PN_MISS, 0, 0, 0, BADOFF, 0} */
 
 /* ---- 16-byte conn-table entry, identical layout to ConnHashEntry (Core.h:178-182) ---- */
 typedef struct pn_conn_entry {
@@ -140,6 +142,21 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
  * Frame length is taken from ip->tot_len only, as the reference does (Core.h:463, TcpConn.h:472). */
 int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                 void* results_dev, void* stream);
+
+/* Classify n frames at arbitrary places — a ring whose slots are named by RX events
+ * (ef_vi: slot id * RecvBufSize + sizeof(RecvBuf) + receive_prefix_len, Core.h:503-505,
+ * wrapping and skipping discarded slots), a packet-mmap block, a packed capture:
+ * frame i's Ethernet header is at base + offsets[i].
+ *   base      : 16-byte aligned; device memory or pinned host memory (zero-copy).
+ *   offsets   : n u64, readable by the device (device or pinned host memory).
+ *   eth_mod16 : offsets[i] % 16, the same for every frame (even): the kernel is
+ *               specialised on it; a frame outside the class gets a PN_F_BADOFF record.
+ *   avail     : readable bytes from each Ethernet header, in [96, 65536] (ef_vi:
+ *               RecvBufSize - sizeof(RecvBuf) - receive_prefix_len); bounds every read.
+ * Records are written in offsets order, identical to pn_classify's for the same frame
+ * bytes and avail.  Asynchronous on `stream`. */
+int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
+                        uint32_t avail, void* results, void* stream);
 
 /* Wait for the last stream used by this ctx. */
 int pn_sync(pn_ctx* ctx);

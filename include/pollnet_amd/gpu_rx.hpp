@@ -94,6 +94,9 @@ class GpuRx {
       }
       if (hipHostMalloc(&h_res_[b], sizeof(pn_result) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
         return "hipHostMalloc(results) failed";
+      if (mode == Mode::ZeroCopy &&
+          hipHostMalloc(&h_offs_[b], sizeof(uint64_t) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
+        return "hipHostMalloc(offsets) failed";
       if (hipEventCreateWithFlags(&done_[b], hipEventDisableTiming) != hipSuccess) return "hipEventCreate failed";
     }
     return nullptr;
@@ -116,22 +119,64 @@ class GpuRx {
   template <class RecvHandler, class TwHandler>
   const char* pollBatch(const uint8_t* host_slots, uint32_t n, const ConnTable& table, RecvHandler&& recv_handler,
                         TwHandler&& tw_handler) {
+    if (mode_ == Mode::ZeroCopy)
+      if (const char* e = check_pinned(host_slots)) return e;
+    return run(
+        n, table, [&](uint32_t k) { return launch(host_slots, n, k); },
+        [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; }, recv_handler, tw_handler);
+  }
+
+  // RX events instead of a contiguous run: frame i's Ethernet
+  // header is at ring + offsets[i] — for ef_vi, id * RecvBufSize + sizeof(RecvBuf) +
+  // receive_prefix_len of each RX event in event order (Core.h:503-505), wrapping
+  // round the ring and skipping discarded slots.  ZeroCopy mode only (the ring stays
+  // where the NIC wrote it; it must be pinned or hipHostRegister'd).  eth_mod16 =
+  // offsets[i] % 16 for every i; avail = readable bytes from each Ethernet header.
+  // Records are dispatched in offsets order.
+  template <class RecvHandler, class TwHandler>
+  const char* pollIndexed(const uint8_t* ring, const uint64_t* offsets, uint32_t n, uint32_t eth_mod16, uint32_t avail,
+                          const ConnTable& table, RecvHandler&& recv_handler, TwHandler&& tw_handler) {
+    if (mode_ != Mode::ZeroCopy) return "pollIndexed needs Mode::ZeroCopy";
+    if (const char* e = check_pinned(ring)) return e;
+    auto launch_k = [&](uint32_t k) -> const char* {
+      const uint32_t base = k * cap_, m = std::min(cap_, n - base), b = k & 1;
+      std::memcpy(h_offs_[b], offsets + base, sizeof(uint64_t) * m); // buffer b is free: chunk k-2 was dispatched
+      if (pn_classify_indexed(ctx_, ring, h_offs_[b], eth_mod16, m, avail, h_res_[b], stream_)) return pn_last_error(ctx_);
+      if (hipEventRecord(done_[b], stream_) != hipSuccess) return "hipEventRecord failed";
+      return nullptr;
+    };
+    return run(
+        n, table, launch_k, [&](uint32_t i) { return ring + offsets[i]; }, recv_handler, tw_handler);
+  }
+
+  pn_ctx* ctx() { return ctx_; }
+  hipStream_t stream() { return stream_; }
+  Mode mode() const { return mode_; }
+
+ private:
+  static const char* check_pinned(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess || attr.type != hipMemoryTypeHost)
+      return "zero-copy ring must be pinned host memory (hipHostMalloc / hipHostRegister)";
+    return nullptr;
+  }
+
+  // Chunked pipeline shared by pollBatch / pollIndexed: chunk k+1 is launched before
+  // chunk k is dispatched; eth_of(i) = frame i's Ethernet header in host memory.
+  template <class Launch, class EthOf, class RecvHandler, class TwHandler>
+  const char* run(uint32_t n, const ConnTable& table, Launch&& launch_k, EthOf&& eth_of, RecvHandler& recv_handler,
+                  TwHandler& tw_handler) {
     if (n == 0) return nullptr;
-    if (mode_ == Mode::ZeroCopy) {
-      hipPointerAttribute_t attr;
-      if (hipPointerGetAttributes(&attr, host_slots) != hipSuccess || attr.type != hipMemoryTypeHost)
-        return "zero-copy ring must be pinned host memory (hipHostMalloc / hipHostRegister)";
-    }
     const uint32_t chunks = (n + cap_ - 1) / cap_;
-    if (const char* e = launch(host_slots, n, 0)) return e;
+    if (const char* e = launch_k(0)) return e;
     for (uint32_t k = 0; k < chunks; k++) {
       if (k + 1 < chunks)
-        if (const char* e = launch(host_slots, n, k + 1)) return e;
+        if (const char* e = launch_k(k + 1)) return e;
       if (hipEventSynchronize(done_[k & 1]) != hipSuccess) return "hipEventSynchronize failed";
       const uint32_t base = k * cap_, m = std::min(cap_, n - base);
       const pn_result* res = h_res_[k & 1];
       for (uint32_t i = 0; i < m; i++) {
-        const uint8_t* eth = host_slots + (size_t)(base + i) * stride_ + off_;
+        const uint8_t* eth = eth_of(base + i);
         const pn_result& r = res[i];
         uint32_t ip_be;
         uint16_t port_be;
@@ -150,11 +195,6 @@ class GpuRx {
     return nullptr;
   }
 
-  pn_ctx* ctx() { return ctx_; }
-  hipStream_t stream() { return stream_; }
-  Mode mode() const { return mode_; }
-
- private:
   // Issue chunk k (H2D + classify + D2H, or one zero-copy classify) into buffer k&1.
   const char* launch(const uint8_t* host_slots, uint32_t n, uint32_t k) {
     const uint32_t base = k * cap_, m = std::min(cap_, n - base), b = k & 1;
@@ -177,6 +217,8 @@ class GpuRx {
     for (int b = 0; b < 2; b++) {
       if (done_[b]) (void)hipEventDestroy(done_[b]);
       if (h_res_[b]) (void)hipHostFree(h_res_[b]);
+      if (h_offs_[b]) (void)hipHostFree(h_offs_[b]);
+      h_offs_[b] = nullptr;
       if (d_res_[b]) (void)hipFree(d_res_[b]);
       if (d_frames_[b]) (void)hipFree(d_frames_[b]);
       done_[b] = nullptr;
@@ -196,6 +238,7 @@ class GpuRx {
   void* d_frames_[2] = {nullptr, nullptr};
   pn_result* d_res_[2] = {nullptr, nullptr};
   pn_result* h_res_[2] = {nullptr, nullptr};
+  uint64_t* h_offs_[2] = {nullptr, nullptr}; // ZeroCopy: pinned offsets the indexed kernel reads
   hipEvent_t done_[2] = {nullptr, nullptr};
   uint32_t stride_ = 0, off_ = 0, cap_ = 0, max_conn_ = 0;
 };

@@ -121,16 +121,43 @@ class GpuTcpRx {
   // classified before a change made during this poll are re-resolved on the host.
   template <class Handler>
   const char* poll(Handler& h, const uint8_t* slots, uint32_t n) {
+    if (const char* e = refresh()) return e;
+    Dispatch<Handler> d{this, h};
+    return rx_.pollBatch(
+        slots, n, table_, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { d(key, r, eth); },
+        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { d(key, r, eth); });
+  }
+  // The same over RX events (GpuRx::pollIndexed: ZeroCopy mode, frame i at ring + offsets[i]).
+  template <class Handler>
+  const char* pollIndexed(Handler& h, const uint8_t* ring, const uint64_t* offsets, uint32_t n, uint32_t eth_mod16,
+                          uint32_t avail) {
+    if (const char* e = refresh()) return e;
+    Dispatch<Handler> d{this, h};
+    return rx_.pollIndexed(
+        ring, offsets, n, eth_mod16, avail, table_,
+        [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { d(key, r, eth); },
+        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { d(key, r, eth); });
+  }
+
+ private:
+  const char* refresh() {
     if (dirty_) {
       if (const char* e = rx_.syncTable(table_)) return e;
       dirty_ = false;
     }
-    auto dispatch = [&](uint64_t key, const pn_result& rec, const uint8_t* eth) {
-      if (drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
+    return nullptr;
+  }
+
+  template <class Handler>
+  struct Dispatch {
+    GpuTcpRx* self;
+    Handler& h;
+    void operator()(uint64_t key, const pn_result& rec, const uint8_t* eth) {
+      if (self->drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
       pn_result r = rec;
-      if (dirty_) { // the table changed earlier in this batch: resolve on the host, fix the record
+      if (self->dirty_) { // the table changed earlier in this poll: resolve on the host, fix the record
         uint32_t conn_id = PN_MISS;
-        const bool hit = table_.find(key, nullptr, &conn_id);
+        const bool hit = self->table_.find(key, nullptr, &conn_id);
         r.conn_id = conn_id;
         r.flags = (uint16_t)((r.flags & ~(PN_F_HIT | PN_F_TW)) | (hit ? PN_F_HIT : 0) |
                              (hit && conn_id >= Conf::MaxConnCnt ? PN_F_TW : 0));
@@ -140,14 +167,9 @@ class GpuTcpRx {
       else if (!(r.flags & PN_F_HIT))
         h.onNewSegment(key, eth, r);
       else
-        deliver(h, conns_[r.conn_id], eth, r);
-    };
-    return rx_.pollBatch(
-        slots, n, table_, [&](uint64_t key, const pn_result& rec, const uint8_t* eth, uint32_t) { dispatch(key, rec, eth); },
-        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& rec) { dispatch(key, rec, eth); });
-  }
-
- private:
+        self->deliver(h, self->conns_[r.conn_id], eth, r);
+    }
+  };
   // One segment of a live connection.  A connection that closes (remote FIN, RST,
   // buffer overrun) leaves the table at once, as TcpConn::onClose does
   // (TcpConn.h:451-465 -> Core::delConnEntry).

@@ -61,6 +61,7 @@ struct KArgs {
   uint32_t stride;
   uint32_t ipa_off; // (frame_off + 14) & ~15: 16-B aligned start of the header window
   uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
+  const uint64_t* offs; // indexed layout: frame i's Ethernet header at frames + offs[i] (nullptr: strided)
 };
 
 __device__ __forceinline__ uint32_t dot2(uint32_t w, uint32_t sel, uint32_t acc) {
@@ -237,9 +238,20 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 // group_ipa: window start of the group's first slot; frame fi's window is at
 // group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
 // frame with readlane); the total of frame fi lands on lane fi.
-template <int ABL, int LAUX>
-__device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* group_ipa, uint32_t n_here, int lane,
-                                             int end_rel, uint32_t& t_all, uint32_t& pad) {
+template <int ABL, int LAUX, int IDX>
+__device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
+                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
+  // window start of frame fi: strided from the group's first slot, or (indexed) the
+  // address its own lane computed, broadcast with two readlanes
+  auto frame_win = [&](uint32_t fi) -> const uint8_t* {
+    if constexpr (IDX) {
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_win, fi & 63);
+      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_win >> 32), fi & 63);
+      return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+    } else {
+      return group_ipa + (uint64_t)fi * a.stride;
+    }
+  };
   for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
     uint32_t acc[kBatch];
     int ends[kBatch];
@@ -251,7 +263,7 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
       const int end = __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1; // bit 0 = odd tcp_len, read below
       ends[j] = end;
       const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
-      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(group_ipa + (uint64_t)fi * a.stride, end16);
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi), end16);
       // out-of-range chunks of a buffer load return 0 and fetch nothing
       w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, LAUX);
       w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, LAUX);
@@ -293,8 +305,7 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
     for (int j = 0; j < kBatch; ++j) {
       const int end = ends[j];
       if (end > kWinBytes + 2048) {
-        const __amdgpu_buffer_rsrc_t rs =
-            frame_rsrc(group_ipa + (uint64_t)(b0 + j) * a.stride, (uint32_t)(end + 15) & ~15u);
+        const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(b0 + j), (uint32_t)(end + 15) & ~15u);
         uint32_t sum = acc[j];
         for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
           const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
@@ -339,7 +350,7 @@ __device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* grou
 
 // ---- phase 3: fold and write the record on the frame's lane ----
 template <int MIS, int ABL, int SAUX>
-__device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f) {
+__device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f, const uint8_t* win, bool bad_off) {
   uint32_t flags = st.flags;
   uint32_t tcp_fold = 0xffff;
   if (!st.trunc) {
@@ -354,7 +365,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
       uint32_t pad = 0;
       if (st.tot_len & 1) { // the byte the reference sums past the segment (high half of the last word)
         uint32_t b = st.pad;
-        if (b == kPadUnknown) b = (a.frames + (uint64_t)f * a.stride + a.ipa_off + MIS)[st.tot_len]; // in-window / jumbo
+        if (b == kPadUnknown) b = (win + MIS)[st.tot_len]; // in-window / jumbo
         pad = b << 8;
       }
       const uint32_t rfc = s_addr + 0x0600 + bswap16(st.tot_len - hl) + (s_seg - st.s_opt - pad);
@@ -369,6 +380,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   rec.y = __builtin_bswap32(st.seq_raw) + ((st.tflags >> 1) & 1);
   rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
   rec.w = flags | (tcp_fold << 16);
+  if (bad_off) rec = u32x4{PN_MISS, 0, 0, PN_F_BADOFF}; // outside the launch's alignment class: not parsed
   if constexpr (ABL & kAblNoStore) {
     if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
   } else {
@@ -383,10 +395,12 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // line, the line the header window lives in) into an XOR-swizzled LDS tile that
 // the header lanes read back; needs 128-B aligned lines with ip at line + 16..31.
 // COOP = 0: each lane loads its own 112-B window (any layout).
-template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux>
+// IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
+// class); per-lane bounds-checked window loads, per-frame stream descriptors.
+template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0>
 // 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
-// default and ef_vi layouts); the 2-mod-4 alignments need two more VGPRs and keep 4.
-__global__ __launch_bounds__(kWave, (MIS % 4 == 0) ? 5 : 4) void rx_classify_kernel(KArgs a) {
+// default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
+__global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
   const int lane = threadIdx.x;
   const uint32_t wave_base = blockIdx.x * kFramesPerWave;
   if (wave_base >= a.n) return;
@@ -399,7 +413,34 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0) ? 5 : 4) void rx_classify_ker
 
   Window h;
   uint32_t ether_type;
-  if constexpr (COOP) {
+  const uint8_t* win = nullptr; // this lane's window start (ip - MIS)
+  bool bad_off = false;
+  if constexpr (IDX) {
+    static_assert(!COOP, "indexed frames use per-lane windows");
+    ether_type = 0;
+#pragma unroll
+    for (int q = 0; q < 4 * kWinChunks; ++q) h.d[q] = 0;
+    if (live) {
+      const uint64_t o = a.offs[f];
+      bad_off = ((o + 14) & 15) != (uint64_t)MIS;
+      win = a.frames + o + 14 - MIS;
+      if (!bad_off) {
+        // window chunk c spans eth + (14 - MIS) + 16c .. +16: load it only inside avail
+#pragma unroll
+        for (int c = 0; c < kWinChunks; ++c) {
+          if ((uint32_t)(14 - MIS + 16 * c + 16) <= a.avail) {
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(win) + c);
+            h.d[4 * c + 0] = v.x;
+            h.d[4 * c + 1] = v.y;
+            h.d[4 * c + 2] = v.z;
+            h.d[4 * c + 3] = v.w;
+          }
+        }
+        if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+        else ether_type = *reinterpret_cast<const uint32_t*>(win - 4) >> 16; // eth + 10 - MIS >= eth
+      }
+    }
+  } else if constexpr (COOP) {
     static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
     __shared__ u32x4 tile[kFramesPerWave * 8]; // 8 KiB: 64 slots x 128 B, chunk p of slot r at r*8 + (p ^ (r&7))
     const uint32_t line0 = a.ipa_off & ~127u;
@@ -432,9 +473,10 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0) ? 5 : 4) void rx_classify_ker
     if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
     else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, LAUX) >> 16; // ipa_off >= 16 here
   }
-  FrameState st = header_phase<MIS, ABL>(h, ether_type, live, a);
-  stream_phase<ABL, LAUX>(a, wave_slot + a.ipa_off, n_here, lane, st.end_rel, st.t_all, st.pad);
-  if (live) finish<MIS, ABL, SAUX>(a, st, f);
+  if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
+  FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, a);
+  stream_phase<ABL, LAUX, IDX>(a, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
+  if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off);
 }
 
 __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src, uint64_t n16, uint32_t* sink) {
@@ -519,10 +561,10 @@ bool coop_layout(const KArgs& a) {
   return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
 }
 
-template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux>
+template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0>
 void launch_one(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX>), dim3((a.n + kFramesPerWave - 1) / kFramesPerWave),
-                     dim3(kWave), 0, s, a);
+  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX>),
+                     dim3((a.n + kFramesPerWave - 1) / kFramesPerWave), dim3(kWave), 0, s, a);
 }
 
 template <int MIS>
@@ -618,6 +660,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
+  a.offs = nullptr;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
@@ -637,6 +680,47 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   return PN_OK;
 }
 
+int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
+                        uint32_t avail, void* results_dev, void* stream) {
+  if (!ctx) return set_err(nullptr, PN_EINVAL, "pn_classify_indexed: ctx is NULL");
+  if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, "pn_classify_indexed: no conn table (call pn_set_conn_table)");
+  if (n == 0) return PN_OK;
+  if (!base || !offsets || !results_dev) return set_err(ctx, PN_EINVAL, "pn_classify_indexed: NULL buffer");
+  if (((uintptr_t)base & 15) || ((uintptr_t)results_dev & 15) || ((uintptr_t)offsets & 7))
+    return set_err(ctx, PN_EINVAL, "pn_classify_indexed: base/results must be 16-byte, offsets 8-byte aligned");
+  if (eth_mod16 > 15 || (eth_mod16 & 1) || avail < 96 || avail > 65536)
+    return set_err(ctx, PN_EINVAL, "pn_classify_indexed: eth_mod16 must be even < 16, avail in [96, 65536]");
+  KArgs a;
+  a.frames = (const uint8_t*)base;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.n = n;
+  a.stride = 0;
+  a.ipa_off = 0;
+  a.avail = avail;
+  a.offs = offsets;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  switch ((eth_mod16 + 14) & 15) {
+    case 0: launch_one<0, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 2: launch_one<2, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 4: launch_one<4, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 6: launch_one<6, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 8: launch_one<8, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 10: launch_one<10, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 12: launch_one<12, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    default: launch_one<14, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                         void* results_dev, void* stream, int variant) {
   if (!ctx || !ctx->tbl_dev || (frame_off + 14) % 16 != 0 || n == 0) return set_err(ctx, PN_EINVAL, "variant: bad args");
@@ -647,10 +731,12 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   a.mask = ctx->mask;
   a.n_entries = ctx->n_entries;
   a.max_conn = ctx->max_conn;
+  a.offs = nullptr;
   a.n = n;
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
+  a.offs = nullptr;
   hipStream_t s = (hipStream_t)stream;
   if ((variant & 1) && !coop_layout(a)) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
   // Tuning variants of the MIS = 0 (ip at slot+16) kernel, A/B-timed in one process by

@@ -39,6 +39,7 @@ class F:
     RFC_TCP_OK = 0x0800
     NOT_TCP = 0x1000
     TRUNC = 0x2000
+    BADOFF = 0x4000
 
 
 RESULT_DTYPE = np.dtype(
@@ -101,6 +102,7 @@ _pn_last_error = _sig("pn_last_error", _c.c_char_p, _vp)
 _pn_device_count = _sig("pn_device_count", _i32, _c.POINTER(_i32))
 _pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
 _pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
+_pn_classify_indexed = _sig("pn_classify_indexed", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
@@ -238,6 +240,16 @@ class RxContext:
             _pn_classify(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(results_dev), _stream_handle(stream)),
             self._h,
             "pn_classify",
+        )
+
+    def classify_indexed(self, base, offsets, eth_mod16: int, n: int, avail: int, results, stream=None):
+        """Frames at base + offsets[i] (u64; device or pinned host memory), all with
+        offsets[i] % 16 == eth_mod16; asynchronous on `stream`."""
+        _check(
+            _pn_classify_indexed(self._h, _ptr(base), _ptr(offsets), eth_mod16, n, avail, _ptr(results),
+                                 _stream_handle(stream)),
+            self._h,
+            "pn_classify_indexed",
         )
 
     def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, store_bytes=0):

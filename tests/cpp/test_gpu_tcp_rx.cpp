@@ -182,7 +182,8 @@ int main(int argc, char** argv) {
   // argv: batch [twin | copy | zc] [span]: `span` polls the whole ring in one call
   // (chunks of `batch` pipelined inside GpuRx) instead of one poll per batch
   const uint32_t n_flows = 200, n_tw = 8, batch = argc > 1 ? (uint32_t)std::atoi(argv[1]) : 1000;
-  const bool zero_copy = argc > 2 && std::strcmp(argv[2], "zc") == 0;
+  const bool indexed = argc > 2 && std::strcmp(argv[2], "idx") == 0; // pollIndexed over event offsets
+  const bool zero_copy = indexed || (argc > 2 && std::strcmp(argv[2], "zc") == 0);
   const bool span = argc > 3 && std::strcmp(argv[3], "span") == 0;
   const uint32_t stride = 2048, off = 2;
   std::mt19937_64 rng(0x7C9E5EEDull);
@@ -324,9 +325,12 @@ int main(int argc, char** argv) {
     return 4;
   }
   gpu->setDropBadChecksum(true);
+  std::vector<uint64_t> offs(n);
+  for (uint32_t i = 0; i < n; i++) offs[i] = (uint64_t)i * stride + off;
   if (!run(*gpu,
            [&](auto& h, const uint8_t* s, uint32_t m) {
-             const char* e = gpu->poll(h, s, m);
+             const char* e = indexed ? gpu->pollIndexed(h, ring, offs.data() + (s - ring) / stride, m, off % 16, stride - off)
+                                     : gpu->poll(h, s, m);
              if (e) std::printf("poll: %s\n", e);
              return e == nullptr;
            },
@@ -351,7 +355,8 @@ int main(int argc, char** argv) {
   }
   size_t cnt[6] = {};
   for (auto& e : glog) cnt[e.type]++;
-  std::printf("%s%s: ", zero_copy ? "zero-copy" : "copy", span ? ", one poll over the ring" : "");
+  std::printf("%s%s: ", indexed ? "indexed zero-copy" : zero_copy ? "zero-copy" : "copy",
+              span ? ", one poll over the ring" : "");
   std::printf("frames %u in batches of %u: %zu events (data %zu, disconnect %zu, ack %zu, new %zu, tw %zu); "
               "%u/%u streams (%u B) intact; conns left %u\n",
               n, batch, glog.size(), cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], streams_ok, n_flows, bytes,

@@ -17,7 +17,7 @@ BIN = os.path.join(ROOT, "tests", "cpp", "test_gpu_tcp_rx")
 @pytest.mark.gpu
 @pytest.mark.parametrize("batch,mode,span", [(1000, "copy", ""), (64, "copy", ""), (1, "copy", ""),
                                              (8192, "zc", ""), (1000, "zc", ""), (64, "zc", "span"),
-                                             (700, "copy", "span")])
+                                             (700, "copy", "span"), (500, "idx", ""), (128, "idx", "span")])
 def test_gpu_tcp_rx_matches_sequential_twin(batch, mode, span):
     assert os.path.exists(BIN), "tests/cpp/test_gpu_tcp_rx not built (make)"
     p = subprocess.run([BIN, str(batch), mode] + ([span] if span else []), capture_output=True, text=True,
