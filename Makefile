@@ -6,8 +6,9 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CFLAGS_ORACLE = -O3 -march=x86-64-v3 -fPIC -Wall -std=c11
 
 LIB = pollnet_amd/libpollnet_amd.so
-SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
+SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
 HDRS = include/pollnet_amd.h
+KHDRS = pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp
 
 ORACLE = oracle/liboracle.so
 REFDIR ?= /root/reference
@@ -17,8 +18,21 @@ RXCONNTEST = tests/cpp/test_rx_conn
 TCPRXTEST = tests/cpp/test_gpu_tcp_rx
 TCPRXBENCH = bench/bench_tcp_rx
 RINGTEST = tests/cpp/test_rx_ring
+STREAMTEST = tests/cpp/test_tcp_stream
+GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST)
+all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST)
+
+# TcpStream reassembly restated vs the reference's own TcpStream (4 instantiations)
+$(STREAMTEST): tests/cpp/test_tcp_stream.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_stream.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle -ldl \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# pn_match_streams + GpuTcpStreams vs the reference filterPacket / TcpStream (GPU)
+$(GPUSTREAMTEST): tests/cpp/test_gpu_tcp_stream.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_stream.hpp \
+  include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle -ldl \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # RX-ring ingestion: socket batcher (+ loopback capture when permitted), ef_vi event rings on the GPU
 $(RINGTEST): tests/cpp/test_rx_ring.cpp include/pollnet_amd/rx_ring.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
@@ -46,7 +60,7 @@ $(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(L
 	$(HIPCC) -O2 -std=c++17 -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
-$(LIB): $(SRCS) $(HDRS)
+$(LIB): $(SRCS) $(HDRS) $(KHDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lpthread
 
 $(ORACLE): oracle/pn_oracle.c oracle/pn_oracle.h $(HDRS)
@@ -56,6 +70,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST)
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST)
 
 .PHONY: all ref clean

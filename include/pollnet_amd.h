@@ -158,6 +158,27 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
 int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
                         uint32_t avail, void* results, void* stream);
 
+/* ---- TcpStream's packet filter over a batch (TcpStream.h:32-52), many streams ---- */
+#define PN_MAX_STREAM_FILTERS 64
+#define PN_NO_STREAM 0xFFFFFFFFu
+typedef struct pn_stream_filter { /* TcpStream::initFilter's four fields (TcpStream.h:32-37) */
+  uint32_t src_ip;                /* network order (inet_pton); 0 = wildcard ("0.0.0.0") */
+  uint32_t dst_ip;
+  uint16_t src_port;              /* network order (htons); 0 = wildcard */
+  uint16_t dst_port;
+  uint32_t _pad;
+} pn_stream_filter;
+
+/* stream_ids[i] = index of the first filter frame i passes, PN_NO_STREAM if none.  A
+ * frame passes filter k exactly when TcpStream::filterPacket would (TcpStream.h:39-52):
+ * etherType 0x0800, protocol 6, and every non-zero field of filter k equal to the
+ * frame's (IP header assumed 20 B).  frames/slot_stride/frame_off as pn_classify
+ * (frame_off >= 2); frames in device or pinned host memory; filters in host memory
+ * (copied into the launch), n_filters <= PN_MAX_STREAM_FILTERS.  Reads one header line
+ * per frame.  Asynchronous on `stream`; needs no conn table. */
+int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                     const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream);
+
 /* Wait for the last stream used by this ctx. */
 int pn_sync(pn_ctx* ctx);
 

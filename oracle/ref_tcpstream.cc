@@ -62,18 +62,43 @@ struct ref_stream_log {
   uint32_t cap_calls;
 };
 
-void* ref_stream_new(void) { return new Stream(); }
-void ref_stream_free(void* s) { delete static_cast<Stream*>(s); }
+}
 
+namespace {
+// The reference's TcpStream in the instantiations the tests drive, behind one interface.
+struct AnyStream {
+  virtual ~AnyStream() = default;
+  virtual int handle(const uint8_t* eth, uint32_t size, uint32_t msg_len, ref_stream_log* log) = 0;
+};
+template <bool W, uint32_t B>
+struct StreamT final : AnyStream {
+  TcpStream<W, B> s;
+  int handle(const uint8_t* eth, uint32_t size, uint32_t msg_len, ref_stream_log* log) override {
+    return s.handlePacket(eth, size, [&](const uint8_t* data, uint32_t n) -> uint32_t {
+      const uint32_t keep = msg_len ? n % msg_len : 0;
+      if (log->n_calls < log->cap_calls) log->call_sizes[log->n_calls] = n;
+      log->n_calls++;
+      const uint32_t take = n - keep;
+      if (log->n_bytes + take <= log->cap_bytes) std::memcpy(log->bytes + log->n_bytes, data, take);
+      log->n_bytes += take;
+      return keep;
+    }) ? 1 : 0;
+  }
+};
+} // namespace
+
+extern "C" {
+// TcpStream<true, 1 MiB>
+void* ref_stream_new(void) { return static_cast<AnyStream*>(new StreamT<true, (1u << 20)>()); }
+// TcpStream<wait_for_resend, small_buf ? 4 KiB : 1 MiB>
+void* ref_stream_new2(int wait_for_resend, int small_buf) {
+  AnyStream* s;
+  if (wait_for_resend) s = small_buf ? (AnyStream*)new StreamT<true, 4096>() : new StreamT<true, (1u << 20)>();
+  else s = small_buf ? (AnyStream*)new StreamT<false, 4096>() : new StreamT<false, (1u << 20)>();
+  return s;
+}
+void ref_stream_free(void* s) { delete static_cast<AnyStream*>(s); }
 int ref_stream_handle(void* s, const uint8_t* eth, uint32_t size, uint32_t msg_len, ref_stream_log* log) {
-  return static_cast<Stream*>(s)->handlePacket(eth, size, [&](const uint8_t* data, uint32_t n) -> uint32_t {
-    const uint32_t keep = msg_len ? n % msg_len : 0;
-    if (log->n_calls < log->cap_calls) log->call_sizes[log->n_calls] = n;
-    log->n_calls++;
-    const uint32_t take = n - keep;
-    if (log->n_bytes + take <= log->cap_bytes) std::memcpy(log->bytes + log->n_bytes, data, take);
-    log->n_bytes += take;
-    return keep;
-  }) ? 1 : 0;
+  return static_cast<AnyStream*>(s)->handle(eth, size, msg_len, log);
 }
 }

@@ -1,0 +1,37 @@
+// Host-side internals shared by the library's translation units: the pn_ctx
+// definition (opaque in include/pollnet_amd.h) and the error plumbing behind
+// pn_last_error (the reference's const char* / getLastError convention, Core.h:253-383).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/pollnet_amd.h"
+
+struct pn_ctx {
+  int device = 0;
+  pn_conn_entry* tbl_dev = nullptr;
+  uint32_t n_entries = 0;
+  uint64_t mask = 0;
+  uint32_t max_conn = 0;
+  hipStream_t last_stream = nullptr;
+  std::string err;
+};
+
+namespace pn_internal {
+
+inline thread_local std::string g_err; // last error of calls made without a ctx
+
+inline int set_err(pn_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  g_err = msg;
+  return code;
+}
+
+inline int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
+  return set_err(ctx, PN_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+} // namespace pn_internal

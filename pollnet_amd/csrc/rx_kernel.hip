@@ -35,8 +35,15 @@
 #include <string>
 
 #include "../../include/pollnet_amd.h"
+#include "device_common.hpp"
+#include "pn_internal.hpp"
 
 namespace {
+
+using namespace pn_dev;
+using pn_internal::g_err;
+using pn_internal::hip_err;
+using pn_internal::set_err;
 
 constexpr int kWave = 64;
 constexpr int kFramesPerWave = 64; // one wave per 64-thread workgroup: +3 % over 4 waves/WG (profiles/r01_experiments)
@@ -46,9 +53,6 @@ constexpr int kBatch = 8;        // frames per stream batch: 16 x 1-KiB loads in
 // (sc1) stores.  Together -1.1..1.3 % kernel time (profiles/r01_experiments).
 constexpr int kLoadAux = 2;
 constexpr int kStoreAux = 16;
-
-using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
-using u16x2 = __attribute__((ext_vector_type(2))) unsigned short;
 
 struct KArgs {
   const uint8_t* frames;
@@ -63,80 +67,6 @@ struct KArgs {
   uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
   const uint64_t* offs; // indexed layout: frame i's Ethernet header at frames + offs[i] (nullptr: strided)
 };
-
-__device__ __forceinline__ uint32_t dot2(uint32_t w, uint32_t sel, uint32_t acc) {
-  // acc + w.lo*sel.lo + w.hi*sel.hi ; sel halves are 0/1 -> masked sum of u16 halves
-  return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, w), __builtin_bit_cast(u16x2, sel), acc, false);
-}
-
-__device__ __forceinline__ uint32_t bswap16(uint32_t v) { return ((v & 0xff) << 8) | ((v >> 8) & 0xff); }
-
-// CSum::fold (Core.h:94-98) on an exact (non-overflowing) u32 sum.
-__device__ __forceinline__ uint32_t csum_fold(uint32_t s) {
-  uint32_t r = (s >> 16) + (s & 0xffff);
-  r += r >> 16;
-  return (~r) & 0xffff;
-}
-
-template <int DPP>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP, 0xf, 0xf, false);
-}
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
-}
-
-// Header-window accessors at compile-time byte offsets O relative to the
-// 16-B aligned window start (MIS + field offset).
-template <int NW>
-struct Win {
-  uint32_t d[NW];
-  template <int O>
-  __device__ __forceinline__ uint32_t b8() const { return (d[O / 4] >> (8 * (O % 4))) & 0xff; }
-  template <int O>
-  __device__ __forceinline__ uint32_t u16() const {
-    static_assert(O % 2 == 0, "even offset");
-    return (d[O / 4] >> (8 * (O % 4))) & 0xffff;
-  }
-  template <int O>
-  __device__ __forceinline__ uint32_t u32() const {
-    static_assert(O % 2 == 0, "even offset");
-    if constexpr (O % 4 == 0) return d[O / 4];
-    else return __builtin_amdgcn_alignbyte(d[O / 4 + 1], d[O / 4], 2);
-  }
-  // exact sum of the u16 words in [LO, HI) (both even, compile-time)
-  template <int LO, int HI>
-  __device__ __forceinline__ uint32_t sum16() const {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int q = LO / 4; q < (HI + 3) / 4; ++q) {
-      const uint32_t sel = ((4 * q >= LO && 4 * q < HI) ? 1u : 0u) | ((4 * q + 2 >= LO && 4 * q + 2 < HI) ? 0x10000u : 0u);
-      acc = dot2(d[q], sel, acc);
-    }
-    return acc;
-  }
-  // sum of u16 words in [LO, lim) for runtime lim <= HI (RFC option bytes)
-  template <int LO, int HI>
-  __device__ __forceinline__ uint32_t sum16_upto(uint32_t lim) const {
-    uint32_t acc = 0;
-#pragma unroll
-    for (int q = LO / 4; q < (HI + 3) / 4; ++q) {
-      const uint32_t o0 = 4 * q, o1 = 4 * q + 2;
-      const uint32_t sel = ((o0 >= LO && o0 < lim) ? 1u : 0u) | ((o1 >= LO && o1 < lim) ? 0x10000u : 0u);
-      acc = dot2(d[q], sel, acc);
-    }
-    return acc;
-  }
-};
-
-// Masked dot2 selector for dword k of a chunk whose first byte is `o` bytes into
-// the window; halves at window offsets >= end are excluded.  end and o even.
-__device__ __forceinline__ uint32_t tail_sel(int end, int o) {
-  int t = end - o;
-  t = t < 0 ? 0 : (t > 4 ? 4 : t); // 0, 2 or 4 valid bytes
-  return (uint32_t)((t >> 1) + (t >> 2) * 0xffff);
-}
 
 // Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
 // header.  112 B ends on the slot's first 128-B line for the default layout (ip at
@@ -531,29 +461,7 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_kernel(const uint8_t* b
 } // namespace
 
 // ============================ C-ABI ============================
-struct pn_ctx {
-  int device = 0;
-  pn_conn_entry* tbl_dev = nullptr;
-  uint32_t n_entries = 0;
-  uint64_t mask = 0;
-  uint32_t max_conn = 0;
-  hipStream_t last_stream = nullptr;
-  std::string err;
-};
-
 namespace {
-thread_local std::string g_err;
-
-int set_err(pn_ctx* ctx, int code, const std::string& msg) {
-  if (ctx) ctx->err = msg;
-  g_err = msg;
-  return code;
-}
-
-int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
-  return set_err(ctx, PN_EHIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
 // Whether the cooperative header-window load applies: 128-B aligned slot lines
 // with the IP header's 16-B chunk at line offset 16 (the default frame_off = 2
 // layout, and ef_vi's 10 + prefix for prefix <= 5).
