@@ -6,8 +6,10 @@ TAG=${1:-run}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/gpu_tests.log 2>&1
-echo "pytest rc=$?" | tee -a $OUT/gpu_tests.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/gpu_tests.log 2>&1
+RC=$?
+echo "pytest rc=$RC" | tee -a $OUT/gpu_tests.log
+[ $RC -le 1 ] || { tail -30 $OUT/gpu_tests.log; exit $RC; }
 tail -3 $OUT/gpu_tests.log
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
