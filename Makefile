@@ -6,9 +6,9 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CFLAGS_ORACLE = -O3 -march=x86-64-v3 -fPIC -Wall -std=c11
 
 LIB = pollnet_amd/libpollnet_amd.so
-SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
+SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
 HDRS = include/pollnet_amd.h
-KHDRS = pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp
+KHDRS = pollnet_amd/csrc/frame_pass.hpp pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp
 
 ORACLE = oracle/liboracle.so
 REFDIR ?= /root/reference
@@ -63,8 +63,8 @@ $(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(L
 $(LIB): $(SRCS) $(HDRS) $(KHDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lpthread
 
-$(ORACLE): oracle/pn_oracle.c oracle/pn_oracle.h $(HDRS)
-	gcc $(CFLAGS_ORACLE) -shared -o $@ oracle/pn_oracle.c -lpthread
+$(ORACLE): oracle/pn_oracle.c oracle/pn_tx_oracle.c oracle/pn_oracle.h $(HDRS)
+	gcc $(CFLAGS_ORACLE) -shared -o $@ oracle/pn_oracle.c oracle/pn_tx_oracle.c -lpthread
 
 ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi

@@ -179,6 +179,40 @@ typedef struct pn_stream_filter { /* TcpStream::initFilter's four fields (TcpStr
 int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                      const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream);
 
+/* ---- TX checksum fill over a batch of outgoing frames ----
+ * Replaces the reference's per-frame checksum finalisation on the send side:
+ *   PN_TX_TCP      efvitcp: SendBuf::setOptDataLen (Core.h:157-163) at the end of
+ *                  TcpConn::sendBuf (TcpConn.h:310-323), of sumRst for RST / TIME_WAIT
+ *                  ACKs (Core.h:385-398), and resendUna's in-place patch
+ *                  (TcpConn.h:771-785).  Writes ip->checksum (IP header assumed 20 B, as
+ *                  every efvitcp frame is) and tcp->checksum over the pseudo-header and
+ *                  tot_len - 20 bytes at ip + 20 (odd length zero-padded, as copyAndSum
+ *                  sums it, TcpConn.h:291-295).  The values equal the reference's
+ *                  incrementally folded ones for every frame its send path builds
+ *                  (DESIGN.md §12).
+ *   PN_TX_UDP_EFVI Efvi's UDP sender: update_udp_pkt (Efvi.h:611-621) with the cached
+ *                  IPv4 header sum (Efvi.h:405-411), its fold reproduced exactly — including
+ *                  the carry it counts twice when the cached sum's first fold carries,
+ *                  which leaves those headers with a checksum that does not verify
+ *                  (DESIGN.md §12).  Writes ip->checksum; the UDP checksum is left as is
+ *                  (Efvi sends 0).
+ *   PN_TX_UDP      the same fields with CSum::fold (Core.h:94-98): a verifying IPv4
+ *                  header checksum for every header; equal to PN_TX_UDP_EFVI wherever
+ *                  Efvi's own is valid.
+ * lens (optional, device-readable u16 per frame): when given, tot_len is set first —
+ * htons(40 + lens[i]) for TCP (setOptDataLen's opt + data length), htons(28 + lens[i])
+ * and udp_len = htons(8 + lens[i]) for the UDP modes (update_udp_pkt's paylen); otherwise the
+ * frame's own tot_len is used.  A frame whose tot_len is below the bare headers
+ * (40 / 28) or runs past its slot (14 + tot_len > slot_stride - frame_off) is left
+ * untouched.  Only the length and checksum fields are written.
+ * Layout as pn_classify (frames in device memory, 16-byte aligned; SendBuf slots:
+ * frame_off = 14, slot_stride = SendBufSize, Core.h:147-156, 232).  Asynchronous. */
+#define PN_TX_TCP 0u
+#define PN_TX_UDP_EFVI 1u
+#define PN_TX_UDP 2u
+int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n, const uint16_t* lens,
+               uint32_t mode, void* stream);
+
 /* Wait for the last stream used by this ctx. */
 int pn_sync(pn_ctx* ctx);
 

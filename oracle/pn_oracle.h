@@ -73,6 +73,26 @@ void orc_refsum_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame
                       const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
                       pn_result* out, int n_threads);
 
+/* ---- TX checksum generation (pn_tx_oracle.c) ---- */
+/* n frames built the way a reference sender builds them (incremental CSum state:
+ * TcpConn.h:149-323, 771-785; Core.h:157-163, 385-446; Efvi.h:405-411, 590-636).
+ * mode PN_TX_TCP mixes SYNs, data segments (copyAndSum pieces), retransmissions,
+ * RSTs and TIME_WAIT ACKs over 64 connections; PN_TX_UDP_EFVI builds Efvi UDP frames.
+ * lens[i] = setOptDataLen's len (tot_len - 40) / update_udp_pkt's paylen;
+ * kinds[i] = 0 data, 1 SYN, 2 retransmitted data, 3 RST, 4 TW ACK, 5 UDP.
+ * Bytes of each slot past the frame are zero except what the reference's buffers leave
+ * there.  0 on success. */
+int orc_tx_build_batch(uint64_t seed, uint32_t n, uint8_t* slots, uint32_t stride, uint32_t frame_off, uint32_t mode,
+                       uint16_t* lens, uint8_t* kinds);
+/* pn_tx_fill's contract recomputed from the bytes (RFC 1071); 1 = filled, 0 = untouched. */
+int orc_tx_fill_frame(uint8_t* eth, uint32_t avail, int has_len, uint16_t len, uint32_t mode);
+void orc_tx_fill_batch(uint8_t* slots, uint32_t stride, uint32_t frame_off, uint32_t n, const uint16_t* lens,
+                       uint32_t mode, int n_threads);
+/* The reference's own TX byte work per segment (copyAndSum into a send buffer +
+ * setOptDataLen) over a batch: the CPU baseline of the TX leg. */
+void orc_tx_copy_and_sum_batch(const uint8_t* slots, uint8_t* out, uint32_t stride, uint32_t frame_off, uint32_t n,
+                               int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

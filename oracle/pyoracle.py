@@ -52,6 +52,13 @@ _frame = _sig("orc_classify_frame", None, _vp, _u32, _vp, _u32, _u64, _u32, _vp)
 _batch = _sig("orc_classify_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 _release = _sig("orc_release_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 _refsum = _sig("orc_refsum_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
+_tx_build = _sig("orc_tx_build_batch", _i32, _u64, _u32, _vp, _u32, _u32, _u32, _vp, _vp)
+_tx_fill_frame = _sig("orc_tx_fill_frame", _i32, _vp, _u32, _i32, C.c_uint16, _u32)
+_tx_fill_batch = _sig("orc_tx_fill_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _i32)
+_tx_cas = _sig("orc_tx_copy_and_sum_batch", None, _vp, _vp, _u32, _u32, _u32, _i32)
+
+TX_TCP, TX_UDP_EFVI, TX_UDP = 0, 1, 2
+TX_KINDS = {0: "data", 1: "syn", 2: "resend", 3: "rst", 4: "tw_ack", 5: "udp"}
 
 
 class Csum:
@@ -169,3 +176,25 @@ def ref_handle_packet(eth: bytes):
     off, ln = _u32(), _u32()
     ok = _ref_lib().ref_handle_packet(b, len(eth), C.byref(off), C.byref(ln))
     return (off.value, ln.value) if ok else None
+
+
+# ---- TX checksum generation (pn_tx_oracle.c) ----
+def tx_build_batch(seed: int, n: int, stride: int = 2048, frame_off: int = 14, mode: int = TX_TCP):
+    """Frames a reference sender would put on the wire (incremental CSum path): (slots, lens, kinds)."""
+    slots = np.zeros((n, stride), dtype=np.uint8)
+    lens = np.zeros(n, dtype=np.uint16)
+    kinds = np.zeros(n, dtype=np.uint8)
+    rc = _tx_build(seed, n, slots.ctypes.data, stride, frame_off, mode, lens.ctypes.data, kinds.ctypes.data)
+    assert rc == 0, "orc_tx_build_batch: bad layout"
+    return slots, lens, kinds
+
+
+def tx_fill_batch(slots: np.ndarray, stride: int, frame_off: int, n: int, lens=None, mode: int = TX_TCP, threads: int = 1):
+    """pn_tx_fill's contract recomputed from the bytes, in place."""
+    assert slots.flags.c_contiguous and slots.dtype == np.uint8
+    lp = None if lens is None else np.ascontiguousarray(lens, dtype=np.uint16)
+    _tx_fill_batch(slots.ctypes.data, stride, frame_off, n, None if lp is None else lp.ctypes.data, mode, threads)
+
+
+def tx_copy_and_sum_batch(slots: np.ndarray, out: np.ndarray, stride: int, frame_off: int, n: int, threads: int = 1):
+    _tx_cas(slots.ctypes.data, out.ctypes.data, stride, frame_off, n, threads)

@@ -12,6 +12,9 @@ from .rx import (  # noqa: F401
     LIB_PATH,
     PN_EMPTY_KEY,
     PN_MISS,
+    PN_TX_TCP,
+    PN_TX_UDP_EFVI,
+    PN_TX_UDP,
     RESULT_DTYPE,
     ENTRY_DTYPE,
     F,

@@ -1,0 +1,216 @@
+// The wave-per-64-slots frame pass shared by the RX classify kernel (rx_kernel.hip)
+// and the TX checksum fill (tx_kernel.hip): the 112-B header window of each slot
+// (cooperative line-0 LDS tile or per-lane loads) and the wave-wide stream of every
+// frame's summed extent past the window, with exact u16-word sums (v_dot2_u32_u16)
+// transpose-reduced onto the frame's own lane.  Design and measurements: DESIGN.md §4.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace pn_dev {
+
+constexpr int kWave = 64;
+constexpr int kFramesPerWave = 64; // one wave per 64-thread workgroup: +3 % over 4 waves/WG (profiles/r01_experiments)
+constexpr int kBatch = 8;        // frames per stream batch: 16 x 1-KiB loads in flight per wave
+// Cache policy (buffer-instruction aux bits on gfx950: 1 sc0, 2 nt, 16 sc1).  Frame
+// bytes are read once: non-temporal loads.  Records are written once: write-through
+// (sc1) stores.  Together -1.1..1.3 % kernel time (profiles/r01_experiments).
+constexpr int kLoadAux = 2;
+constexpr int kStoreAux = 16;
+
+// Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
+// header.  112 B ends on the slot's first 128-B line for the default layout (ip at
+// slot+16), so the wave-wide stream starts on a fresh line.
+constexpr int kWinChunks = 7;
+constexpr int kWinBytes = 16 * kWinChunks;
+using Window = Win<4 * kWinChunks>;
+
+constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
+
+// Timing-only ablations (scripts/variants.py; records are wrong when set):
+// bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
+// masks, bit3 no record store.
+enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8 };
+
+// Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
+// r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the
+// slot's ether_type as stored (0x0008 = IPv4).
+// COOP = 1: 8 lanes per slot load its first 128-B line (exactly one request per line,
+// the line the window lives in) into an XOR-swizzled LDS tile that each lane reads
+// back; needs 128-B aligned lines with the window at line + 16.
+// COOP = 0: each lane loads its own window (any layout).
+// The cooperative window's LDS tile: 64 slots x 128 B (8 KiB), chunk p of slot r at
+// r*8 + (p ^ (r&7)).  One static allocation per kernel; the TX fill writes patched lines
+// back from it.
+__device__ __forceinline__ u32x4* coop_tile() {
+  __shared__ u32x4 tile[kFramesPerWave * 8];
+  return tile;
+}
+
+template <int MIS, int COOP, int LAUX>
+__device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t rs, int lane, uint32_t stride,
+                                                        uint32_t ipa_off, Window& h) {
+  uint32_t ether_type;
+  if constexpr (COOP) {
+    static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
+    u32x4* tile = coop_tile();
+    const uint32_t line0 = ipa_off & ~127u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+      tile[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + line0 + 16 * part, 0, LAUX);
+    }
+    const uint32_t p0 = (ipa_off & 127u) >> 4; // == 1 on this path
+#pragma unroll
+    for (int c = 0; c < kWinChunks; ++c) {
+      const u32x4 v = tile[lane * 8 + ((p0 + c) ^ (lane & 7))];
+      h.d[4 * c + 0] = v.x;
+      h.d[4 * c + 1] = v.y;
+      h.d[4 * c + 2] = v.z;
+      h.d[4 * c + 3] = v.w;
+    }
+    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+    else ether_type = tile[lane * 8 + ((p0 - 1) ^ (lane & 7))].w >> 16;
+  } else {
+    const uint32_t lo = (uint32_t)lane * stride + ipa_off;
+#pragma unroll
+    for (int c = 0; c < kWinChunks; ++c) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + 16 * c, 0, LAUX);
+      h.d[4 * c + 0] = v.x;
+      h.d[4 * c + 1] = v.y;
+      h.d[4 * c + 2] = v.z;
+      h.d[4 * c + 3] = v.w;
+    }
+    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+    else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, LAUX) >> 16; // ipa_off >= 16 here
+  }
+  return ether_type;
+}
+
+// Exact u16-word sum of the window's bytes in [lo, end) (lo compile-time, end even).
+template <int LO>
+__device__ __forceinline__ uint32_t window_sum_from(const Window& h, int end) {
+  uint32_t t = 0;
+#pragma unroll
+  for (int q = LO / 4; q < 4 * kWinChunks; ++q) {
+    const uint32_t start_sel = ((4 * q >= LO) ? 1u : 0u) | ((4 * q + 2 >= LO) ? 0x10000u : 0u);
+    t = dot2(h.d[q], tail_sel(end, 4 * q) & start_sel, t);
+  }
+  return t;
+}
+
+// ---- phase 2: the wave streams every frame's region past the window ----
+// group_ipa: window start of the group's first slot; frame fi's window is at
+// group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
+// frame with readlane); the total of frame fi lands on lane fi.
+template <int ABL, int LAUX, int IDX>
+__device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
+                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
+  // window start of frame fi: strided from the group's first slot, or (indexed) the
+  // address its own lane computed, broadcast with two readlanes
+  auto frame_win = [&](uint32_t fi) -> const uint8_t* {
+    if constexpr (IDX) {
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_win, fi & 63);
+      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_win >> 32), fi & 63);
+      return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+    } else {
+      return group_ipa + (uint64_t)fi * stride;
+    }
+  };
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    uint32_t acc[kBatch];
+    int ends[kBatch];
+    u32x4 w0s[kBatch], w1s[kBatch];
+    // issue all 2*kBatch loads of the batch before consuming any of them
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const uint32_t fi = b0 + j; // wave-uniform
+      const int end = __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1; // bit 0 = odd tcp_len, read below
+      ends[j] = end;
+      const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi), end16);
+      // out-of-range chunks of a buffer load return 0 and fetch nothing
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, LAUX);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, LAUX);
+    }
+    __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
+    auto sel = [](int e, int o) -> uint32_t {
+      if constexpr (ABL & kAblNoMask) return 0x10001u;
+      else return tail_sel(e, o);
+    };
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int end = ends[j];
+      const u32x4 w0 = w0s[j], w1 = w1s[j];
+      const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
+      uint32_t sum = 0;
+      sum = dot2(w0.x, sel(end, o0), sum);
+      sum = dot2(w0.y, sel(end, o0 + 4), sum);
+      sum = dot2(w0.z, sel(end, o0 + 8), sum);
+      sum = dot2(w0.w, sel(end, o0 + 12), sum);
+      sum = dot2(w1.x, sel(end, o1), sum);
+      sum = dot2(w1.y, sel(end, o1 + 4), sum);
+      sum = dot2(w1.z, sel(end, o1 + 8), sum);
+      sum = dot2(w1.w, sel(end, o1 + 12), sum);
+      acc[j] = sum;
+      // odd tcp_len: the RFC verdict needs the byte the reference sums past the segment (window
+      // offset end - 1); take it from the lane that streamed it instead of re-reading the line later
+      const int p = end - 1;
+      if ((__builtin_amdgcn_readlane(end_rel, (b0 + j) & 63) & 1) && p >= kWinBytes && p < kWinBytes + 2048) {
+        const int q = p - kWinBytes;                 // wave-uniform
+        const u32x4 w = (q < 1024) ? w0 : w1;
+        const int dw = (q >> 2) & 3;
+        const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
+        const uint32_t b = __builtin_amdgcn_readlane((d >> (8 * (q & 3))) & 0xff, (q & 1023) >> 4);
+        if ((uint32_t)lane == b0 + j) pad = b;
+      }
+    }
+    // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const int end = ends[j];
+      if (end > kWinBytes + 2048) {
+        const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(b0 + j), (uint32_t)(end + 15) & ~15u);
+        uint32_t sum = acc[j];
+        for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
+          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
+          const int o = kb + lane * 16;
+          sum = dot2(w.x, tail_sel(end, o), sum);
+          sum = dot2(w.y, tail_sel(end, o + 4), sum);
+          sum = dot2(w.z, tail_sel(end, o + 8), sum);
+          sum = dot2(w.w, tail_sel(end, o + 12), sum);
+        }
+        acc[j] = sum;
+      }
+    }
+    // transpose-reduce 8 frames x 64 lanes: lane l ends with the total of frame (l>>3)&7
+    if constexpr (ABL & kAblNoReduce) {
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) x += acc[j];
+      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += x;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { // xor 32: v_permlane32_swap
+        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
+        acc[i] = r[0] + r[1];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) { // xor 16: v_permlane16_swap
+        const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
+        acc[i] = r[0] + r[1];
+      }
+      const bool b3 = lane & 8; // xor 8: keep one, send the other
+      const uint32_t keep = b3 ? acc[1] : acc[0];
+      const uint32_t send = b3 ? acc[0] : acc[1];
+      uint32_t v = keep + dpp<0x128>(send); // row_ror:8           -> lane ^ 8
+      v += dpp<0xB1>(v);                    // quad_perm [1,0,3,2]  -> lane ^ 1
+      v += dpp<0x4E>(v);                    // quad_perm [2,3,0,1]  -> lane ^ 2
+      v += dpp<0x141>(v);                   // row_half_mirror      -> other quad of the 8
+      const uint32_t tot = __shfl(v, (lane & 7) * 8);
+      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
+    }
+  }
+}
+
+} // namespace pn_dev

@@ -17,6 +17,9 @@ struct pn_ctx {
   uint64_t mask = 0;
   uint32_t max_conn = 0;
   hipStream_t last_stream = nullptr;
+  void* tx_patch = nullptr;       // pn_tx_fill's per-frame patch records (8 B each)
+  uint32_t tx_patch_n = 0;
+  hipStream_t tx_stream = nullptr; // stream of the last pn_tx_fill (the scratch is reused)
   std::string err;
 };
 

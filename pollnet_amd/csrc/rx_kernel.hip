@@ -36,6 +36,7 @@
 
 #include "../../include/pollnet_amd.h"
 #include "device_common.hpp"
+#include "frame_pass.hpp"
 #include "pn_internal.hpp"
 
 namespace {
@@ -44,15 +45,6 @@ using namespace pn_dev;
 using pn_internal::g_err;
 using pn_internal::hip_err;
 using pn_internal::set_err;
-
-constexpr int kWave = 64;
-constexpr int kFramesPerWave = 64; // one wave per 64-thread workgroup: +3 % over 4 waves/WG (profiles/r01_experiments)
-constexpr int kBatch = 8;        // frames per stream batch: 16 x 1-KiB loads in flight per wave
-// Cache policy (buffer-instruction aux bits on gfx950: 1 sc0, 2 nt, 16 sc1).  Frame
-// bytes are read once: non-temporal loads.  Records are written once: write-through
-// (sc1) stores.  Together -1.1..1.3 % kernel time (profiles/r01_experiments).
-constexpr int kLoadAux = 2;
-constexpr int kStoreAux = 16;
 
 struct KArgs {
   const uint8_t* frames;
@@ -68,13 +60,6 @@ struct KArgs {
   const uint64_t* offs; // indexed layout: frame i's Ethernet header at frames + offs[i] (nullptr: strided)
 };
 
-// Header window: kWinChunks x 16 B from the 16-B aligned chunk holding the IP
-// header.  112 B ends on the slot's first 128-B line for the default layout (ip at
-// slot+16), so the wave-wide stream starts on a fresh line.
-constexpr int kWinChunks = 7;
-constexpr int kWinBytes = 16 * kWinChunks;
-using Window = Win<4 * kWinChunks>;
-
 // Per-frame state the header lane keeps from phase 1 to phase 3.
 struct FrameState {
   uint32_t flags, ihl, tot_len, src_ip, dst_ip, seq_raw, doff, tflags, s_ip20, s_opt, tcp_len, conn_id;
@@ -83,12 +68,6 @@ struct FrameState {
   uint32_t pad;   // odd tcp_len: the byte after the segment (kPadUnknown until phase 2 captured it)
   bool trunc;
 };
-constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
-
-// Timing-only ablations (scripts/variants.py; records are wrong when set):
-// bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
-// masks, bit3 no record store.
-enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8 };
 
 // ---- phase 1: decode one frame from its header window (lane f <-> frame f) ----
 template <int MIS, int ABL>
@@ -130,13 +109,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   st.pad = kPadUnknown;
 
   // the part of the region inside the window, summed from registers
-  uint32_t t = 0;
-#pragma unroll
-  for (int q = MIS / 4; q < 4 * kWinChunks; ++q) {
-    const uint32_t start_sel = ((4 * q >= MIS) ? 1u : 0u) | ((4 * q + 2 >= MIS) ? 0x10000u : 0u);
-    t = dot2(h.d[q], tail_sel(st.end_rel & ~1, 4 * q) & start_sel, t);
-  }
-  st.t_all = t;
+  st.t_all = window_sum_from<MIS>(h, st.end_rel & ~1);
 
   // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
   st.conn_id = PN_MISS;
@@ -162,120 +135,6 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   }
   st.flags = flags;
   return st;
-}
-
-// ---- phase 2: the wave streams every frame's region past the window ----
-// group_ipa: window start of the group's first slot; frame fi's window is at
-// group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
-// frame with readlane); the total of frame fi lands on lane fi.
-template <int ABL, int LAUX, int IDX>
-__device__ __forceinline__ void stream_phase(const KArgs& a, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
-                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
-  // window start of frame fi: strided from the group's first slot, or (indexed) the
-  // address its own lane computed, broadcast with two readlanes
-  auto frame_win = [&](uint32_t fi) -> const uint8_t* {
-    if constexpr (IDX) {
-      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_win, fi & 63);
-      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_win >> 32), fi & 63);
-      return (const uint8_t*)(((uint64_t)hi << 32) | lo);
-    } else {
-      return group_ipa + (uint64_t)fi * a.stride;
-    }
-  };
-  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
-    uint32_t acc[kBatch];
-    int ends[kBatch];
-    u32x4 w0s[kBatch], w1s[kBatch];
-    // issue all 2*kBatch loads of the batch before consuming any of them
-#pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
-      const uint32_t fi = b0 + j; // wave-uniform
-      const int end = __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1; // bit 0 = odd tcp_len, read below
-      ends[j] = end;
-      const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
-      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi), end16);
-      // out-of-range chunks of a buffer load return 0 and fetch nothing
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, LAUX);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, LAUX);
-    }
-    __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
-    auto sel = [](int e, int o) -> uint32_t {
-      if constexpr (ABL & kAblNoMask) return 0x10001u;
-      else return tail_sel(e, o);
-    };
-#pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
-      const int end = ends[j];
-      const u32x4 w0 = w0s[j], w1 = w1s[j];
-      const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
-      uint32_t sum = 0;
-      sum = dot2(w0.x, sel(end, o0), sum);
-      sum = dot2(w0.y, sel(end, o0 + 4), sum);
-      sum = dot2(w0.z, sel(end, o0 + 8), sum);
-      sum = dot2(w0.w, sel(end, o0 + 12), sum);
-      sum = dot2(w1.x, sel(end, o1), sum);
-      sum = dot2(w1.y, sel(end, o1 + 4), sum);
-      sum = dot2(w1.z, sel(end, o1 + 8), sum);
-      sum = dot2(w1.w, sel(end, o1 + 12), sum);
-      acc[j] = sum;
-      // odd tcp_len: the RFC verdict needs the byte the reference sums past the segment (window
-      // offset end - 1); take it from the lane that streamed it instead of re-reading the line later
-      const int p = end - 1;
-      if ((__builtin_amdgcn_readlane(end_rel, (b0 + j) & 63) & 1) && p >= kWinBytes && p < kWinBytes + 2048) {
-        const int q = p - kWinBytes;                 // wave-uniform
-        const u32x4 w = (q < 1024) ? w0 : w1;
-        const int dw = (q >> 2) & 3;
-        const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
-        const uint32_t b = __builtin_amdgcn_readlane((d >> (8 * (q & 3))) & 0xff, (q & 1023) >> 4);
-        if ((uint32_t)lane == b0 + j) pad = b;
-      }
-    }
-    // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
-#pragma unroll
-    for (int j = 0; j < kBatch; ++j) {
-      const int end = ends[j];
-      if (end > kWinBytes + 2048) {
-        const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(b0 + j), (uint32_t)(end + 15) & ~15u);
-        uint32_t sum = acc[j];
-        for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
-          const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
-          const int o = kb + lane * 16;
-          sum = dot2(w.x, tail_sel(end, o), sum);
-          sum = dot2(w.y, tail_sel(end, o + 4), sum);
-          sum = dot2(w.z, tail_sel(end, o + 8), sum);
-          sum = dot2(w.w, tail_sel(end, o + 12), sum);
-        }
-        acc[j] = sum;
-      }
-    }
-    // transpose-reduce 8 frames x 64 lanes: lane l ends with the total of frame (l>>3)&7
-    if constexpr (ABL & kAblNoReduce) {
-      uint32_t x = 0;
-#pragma unroll
-      for (int j = 0; j < kBatch; ++j) x += acc[j];
-      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += x;
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { // xor 32: v_permlane32_swap
-        const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 4], false, false);
-        acc[i] = r[0] + r[1];
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) { // xor 16: v_permlane16_swap
-        const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 2], false, false);
-        acc[i] = r[0] + r[1];
-      }
-      const bool b3 = lane & 8; // xor 8: keep one, send the other
-      const uint32_t keep = b3 ? acc[1] : acc[0];
-      const uint32_t send = b3 ? acc[0] : acc[1];
-      uint32_t v = keep + dpp<0x128>(send); // row_ror:8           -> lane ^ 8
-      v += dpp<0xB1>(v);                    // quad_perm [1,0,3,2]  -> lane ^ 1
-      v += dpp<0x4E>(v);                    // quad_perm [2,3,0,1]  -> lane ^ 2
-      v += dpp<0x141>(v);                   // row_half_mirror      -> other quad of the 8
-      const uint32_t tot = __shfl(v, (lane & 7) * 8);
-      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
-    }
-  }
 }
 
 // ---- phase 3: fold and write the record on the frame's lane ----
@@ -370,42 +229,12 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
         else ether_type = *reinterpret_cast<const uint32_t*>(win - 4) >> 16; // eth + 10 - MIS >= eth
       }
     }
-  } else if constexpr (COOP) {
-    static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
-    __shared__ u32x4 tile[kFramesPerWave * 8]; // 8 KiB: 64 slots x 128 B, chunk p of slot r at r*8 + (p ^ (r&7))
-    const uint32_t line0 = a.ipa_off & ~127u;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-      tile[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + line0 + 16 * part, 0, LAUX);
-    }
-    const uint32_t p0 = (a.ipa_off & 127u) >> 4; // == 1 on this path
-#pragma unroll
-    for (int c = 0; c < kWinChunks; ++c) {
-      const u32x4 v = tile[lane * 8 + ((p0 + c) ^ (lane & 7))];
-      h.d[4 * c + 0] = v.x;
-      h.d[4 * c + 1] = v.y;
-      h.d[4 * c + 2] = v.z;
-      h.d[4 * c + 3] = v.w;
-    }
-    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
-    else ether_type = tile[lane * 8 + ((p0 - 1) ^ (lane & 7))].w >> 16;
   } else {
-    const uint32_t lo = (uint32_t)lane * a.stride + a.ipa_off;
-#pragma unroll
-    for (int c = 0; c < kWinChunks; ++c) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lo + 16 * c, 0, LAUX);
-      h.d[4 * c + 0] = v.x;
-      h.d[4 * c + 1] = v.y;
-      h.d[4 * c + 2] = v.z;
-      h.d[4 * c + 3] = v.w;
-    }
-    if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
-    else ether_type = __builtin_amdgcn_raw_buffer_load_b32(rs, lo - 4, 0, LAUX) >> 16; // ipa_off >= 16 here
+    ether_type = load_window_strided<MIS, COOP, LAUX>(rs, lane, a.stride, a.ipa_off, h);
   }
   if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, a);
-  stream_phase<ABL, LAUX, IDX>(a, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
+  stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
   if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off);
 }
 
@@ -510,9 +339,11 @@ int pn_open(int device, pn_ctx** out) {
 
 void pn_close(pn_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->tbl_dev) {
+  if (ctx->tbl_dev || ctx->tx_patch) {
     (void)hipSetDevice(ctx->device);
-    (void)hipFree(ctx->tbl_dev);
+    if (ctx->tx_patch) (void)hipStreamSynchronize(ctx->tx_stream);
+    if (ctx->tbl_dev) (void)hipFree(ctx->tbl_dev);
+    if (ctx->tx_patch) (void)hipFree(ctx->tx_patch);
   }
   delete ctx;
 }

@@ -20,6 +20,9 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpollnet_
 PN_EMPTY_KEY = 1 << 63
 PN_MISS = 0xFFFFFFFF
 PN_RECV_BUF_SIZE = 2048
+PN_TX_TCP = 0       # efvitcp SendBuf::setOptDataLen / sumRst / resendUna (Core.h:157-163, 385-398; TcpConn.h:771-785)
+PN_TX_UDP_EFVI = 1  # Efvi update_udp_pkt with the cached IPv4 sum (Efvi.h:405-411, 611-621), bit-exact
+PN_TX_UDP = 2       # the same fields with CSum::fold (Core.h:94-98): always a verifying header checksum
 
 
 class F:
@@ -103,6 +106,8 @@ _pn_device_count = _sig("pn_device_count", _i32, _c.POINTER(_i32))
 _pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
 _pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_classify_indexed = _sig("pn_classify_indexed", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
+_pn_tx_fill = _sig("pn_tx_fill", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp)
+_pn_tx_variant = _sig("pn_tx_fill_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _i32, _vp)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
@@ -251,6 +256,21 @@ class RxContext:
             self._h,
             "pn_classify_indexed",
         )
+
+    def tx_fill(self, frames_dev, slot_stride: int, frame_off: int, n: int, lens=None, mode: int = PN_TX_TCP,
+                stream=None):
+        """TX checksum fill in place (pn_tx_fill): IP + TCP checksums of n outgoing frames
+        (mode PN_TX_TCP), or the IPv4 checksum of UDP frames (PN_TX_UDP_EFVI: Efvi's
+        cached fold bit for bit; PN_TX_UDP: CSum::fold).  lens (device u16 per
+        frame, optional) sets tot_len first, as setOptDataLen / update_udp_pkt do.
+        Asynchronous on `stream`."""
+        _check(_pn_tx_fill(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), mode,
+                           _stream_handle(stream)), self._h, "pn_tx_fill")
+
+    def tx_fill_variant(self, frames_dev, slot_stride, frame_off, n, lens, variant, stream=None):
+        """Tuning-only TX fill shapes (scripts/tx_variants.py); not part of the C header."""
+        _check(_pn_tx_variant(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), variant,
+                              _stream_handle(stream)), self._h, "pn_tx_fill_variant")
 
     def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, store_bytes=0):
         _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, store_bytes, _ptr(sink_dev),
