@@ -30,7 +30,7 @@ constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
 // Timing-only ablations (scripts/variants.py; records are wrong when set):
 // bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
 // masks, bit3 no record store.
-enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8 };
+enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8, kAblStore8 = 16, kAblGlobalStore = 32 };
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the

@@ -172,6 +172,10 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   if (bad_off) rec = u32x4{PN_MISS, 0, 0, PN_F_BADOFF}; // outside the launch's alignment class: not parsed
   if constexpr (ABL & kAblNoStore) {
     if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
+  } else if constexpr (ABL & kAblStore8) { // timing only: half the record bytes
+    reinterpret_cast<uint2*>(a.out)[f] = uint2{rec.x ^ rec.y, rec.z ^ rec.w};
+  } else if constexpr (ABL & kAblGlobalStore) { // the record through a plain global store (SAUX ignored)
+    *reinterpret_cast<u32x4*>(a.out + f) = rec;
   } else {
     // one coalesced 1-KiB store per wave; the descriptor covers this wave's 64 records
     const __amdgpu_buffer_rsrc_t rs = frame_rsrc((const uint8_t*)(a.out + (f & ~63u)), 64 * 16);
@@ -186,7 +190,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // COOP = 0: each lane loads its own 112-B window (any layout).
 // IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
 // class); per-lane bounds-checked window loads, per-frame stream descriptors.
-template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0>
+template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 // 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
 // default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
 __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
@@ -230,7 +234,7 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
       }
     }
   } else {
-    ether_type = load_window_strided<MIS, COOP, LAUX>(rs, lane, a.stride, a.ipa_off, h);
+    ether_type = load_window_strided<MIS, COOP, LWIN>(rs, lane, a.stride, a.ipa_off, h);
   }
   if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, a);
@@ -298,9 +302,9 @@ bool coop_layout(const KArgs& a) {
   return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
 }
 
-template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0>
+template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 void launch_one(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX>),
+  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>),
                      dim3((a.n + kFramesPerWave - 1) / kFramesPerWave), dim3(kWave), 0, s, a);
 }
 
@@ -485,6 +489,12 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 1: launch_one<0, 1>(a, s); break;                         // cooperative window (production here)
     case 2: launch_one<0, 0, 0, 0, 0>(a, s); break;                // per-lane, default cache policy
     case 3: launch_one<0, 1, 0, 0, 0>(a, s); break;                // cooperative, default cache policy
+    case 4: launch_one<0, 1, 0, kLoadAux, kStoreAux, 0, 0>(a, s); break; // line-0 window default policy
+    case 5: launch_one<0, 1, 0, kLoadAux, 0>(a, s); break;         // default-policy record stores
+    case 6: launch_one<0, 1, 0, kLoadAux, 0, 0, 0>(a, s); break;   // both
+    case 7: launch_one<0, 1, 0, kLoadAux, 2>(a, s); break;         // nt record stores
+    case 8: launch_one<0, 1, kAblGlobalStore>(a, s); break;        // plain global record store
+    case 19: launch_one<0, 1, kAblStore8>(a, s); break;            // timing only: 8-B stores
     case 11: launch_one<0, 1, kAblNoProbe>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;

@@ -141,6 +141,13 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
       const uint2 rec = {ip_chk | (l4 << 16), tot_word | (ok ? kPatchOk : 0u) | (has_len ? kPatchLen : 0u)};
       a.patch[f] = rec; // one coalesced 512-B store per wave
     }
+  } else if constexpr (WB == -3) { // timing only: a 16-B record per frame (RX's record size), plain store
+    if (live) reinterpret_cast<u32x4*>(a.patch)[f] = u32x4{ip_chk, l4, tot_word, f};
+  } else if constexpr (WB == -4) { // timing only: the 16-B record through RX's buffer store (sc1)
+    if (live) {
+      const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.patch + 2 * (f & ~63u)), 64 * 16);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{ip_chk, l4, tot_word, f}, ro, (f & 63u) * 16, 0, kStoreAux);
+    }
   } else {
     constexpr int L4 = UDP ? 24 : 36;
     constexpr bool kTile = COOP && WB > 0;
@@ -304,7 +311,7 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
   a.frame_off = frame_off;
   if (!coop_layout(a)) return set_err(ctx, PN_EINVAL, "tx variant: needs the cooperative layout");
   hipStream_t s = (hipStream_t)stream;
-  int rc = ensure_patch(ctx, n, s);
+  int rc = ensure_patch(ctx, variant >= 15 ? 2 * n : n, s); // 16-B record variants need 2 patch slots per frame
   if (rc) return rc;
   a.patch = (uint2*)ctx->tx_patch;
   const dim3 grid((n + kFramesPerWave - 1) / kFramesPerWave), block(kWave), pgrid((n + 255) / 256), pblock(256);
@@ -325,6 +332,8 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         return 0;
       case 13: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a); return 0; // phase 1 only
       case 14: hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a); return 0;    // phase 2 only
+      case 15: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -3>), grid, block, 0, s, a); return 0;  // phase 1, 16-B records
+      case 16: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -4>), grid, block, 0, s, a); return 0;  // phase 1, RX-style store
       default: return -1;
     }
   };

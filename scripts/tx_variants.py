@@ -13,8 +13,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 NAMES = {0: "inplace_u16_stores", 2: "inplace_tile_wb128_sc1", 9: "ABL_nowrite",
-         10: "twophase_line0_nt", 11: "twophase_production", 13: "phase1_only", 14: "phase2_only"}
-TIMING_ONLY = {9, 13, 14}
+         10: "twophase_line0_nt", 11: "twophase_production", 13: "phase1_only", 14: "phase2_only",
+         15: "phase1_rec16_global", 16: "phase1_rec16_buffer_sc1"}
+TIMING_ONLY = {9, 13, 14, 15, 16}
 
 
 def main():
