@@ -152,7 +152,10 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
  *   eth_mod16 : offsets[i] % 16, the same for every frame (even): the kernel is
  *               specialised on it; a frame outside the class gets a PN_F_BADOFF record.
  *   avail     : readable bytes from each Ethernet header, in [96, 65536] (ef_vi:
- *               RecvBufSize - sizeof(RecvBuf) - receive_prefix_len); bounds every read.
+ *               RecvBufSize - sizeof(RecvBuf) - receive_prefix_len); bounds every read
+ *               past the header.  A frame whose header window starts 16 B into a
+ *               128-B line (2-KiB slots with frame_off 2, ef_vi with a prefix <= 7) may
+ *               also be read from that line's start, never below base.
  * Records are written in offsets order, identical to pn_classify's for the same frame
  * bytes and avail.  Asynchronous on `stream`. */
 int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,

@@ -189,7 +189,8 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // the header lanes read back; needs 128-B aligned lines with ip at line + 16..31.
 // COOP = 0: each lane loads its own 112-B window (any layout).
 // IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
-// class); per-lane bounds-checked window loads, per-frame stream descriptors.
+// class); per-frame stream descriptors; with COOP, waves whose frames all have their
+// window at line + 16 load lines cooperatively, other waves per-lane bounds-checked windows.
 template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 // 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
 // default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
@@ -209,14 +210,50 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
   const uint8_t* win = nullptr; // this lane's window start (ip - MIS)
   bool bad_off = false;
   if constexpr (IDX) {
-    static_assert(!COOP, "indexed frames use per-lane windows");
     ether_type = 0;
 #pragma unroll
     for (int q = 0; q < 4 * kWinChunks; ++q) h.d[q] = 0;
-    if (live) {
-      const uint64_t o = a.offs[f];
-      bad_off = ((o + 14) & 15) != (uint64_t)MIS;
-      win = a.frames + o + 14 - MIS;
+    const uint64_t o = live ? a.offs[f] : 0;
+    bad_off = live && ((o + 14) & 15) != (uint64_t)MIS;
+    win = a.frames + o + 14 - MIS;
+    bool coop_done = false;
+    if constexpr (COOP) {
+      // Cooperative window for line-aligned frames (ef_vi rings with a short prefix, 2-KiB
+      // batches): the window is the frame's line from offset 16 on, and the whole line lies
+      // inside [base, eth + avail).  When every frame of the wave qualifies, 8 lanes per
+      // frame load its line coalesced into the LDS tile (one request per line), as the
+      // strided kernel does; otherwise the wave falls back to per-lane windows.
+      const bool use = live && !bad_off;
+      const bool elig = !use || ((((uintptr_t)win & 127u) == 16) && o + 14 >= (uint64_t)(MIS + 16) &&
+                                 (uint32_t)(14 - MIS + kWinBytes) <= a.avail);
+      if (__all(elig)) {
+        __shared__ uint64_t line_addr[kFramesPerWave];
+        line_addr[lane] = use ? (uint64_t)(win - 16) : 0ull;
+        __syncthreads();
+        u32x4* tile = coop_tile();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+          const uint64_t la = line_addr[r];
+          u32x4 v = {0u, 0u, 0u, 0u};
+          if (la) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
+          tile[r * 8 + (part ^ (r & 7))] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < kWinChunks; ++c) {
+          const u32x4 v = tile[lane * 8 + ((1 + c) ^ (lane & 7))];
+          h.d[4 * c + 0] = v.x;
+          h.d[4 * c + 1] = v.y;
+          h.d[4 * c + 2] = v.z;
+          h.d[4 * c + 3] = v.w;
+        }
+        if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+        else ether_type = tile[lane * 8 + (0 ^ (lane & 7))].w >> 16;
+        coop_done = true;
+      }
+    }
+    if (live && !coop_done) {
       if (!bad_off) {
         // window chunk c spans eth + (14 - MIS) + 16c .. +16: load it only inside avail
 #pragma unroll
@@ -449,17 +486,44 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 2: launch_one<2, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 4: launch_one<4, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 6: launch_one<6, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 8: launch_one<8, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 10: launch_one<10, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 12: launch_one<12, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    default: launch_one<14, 0, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 0: launch_one<0, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 2: launch_one<2, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 4: launch_one<4, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 6: launch_one<6, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 8: launch_one<8, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 10: launch_one<10, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 12: launch_one<12, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    default: launch_one<14, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+// Tuning: the indexed kernel with the cooperative line window (variant 1) or without (0),
+// A/B-timed by scripts/bench_indexed.py; not part of the public header.
+int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
+                                uint32_t avail, void* results_dev, void* stream, int variant) {
+  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 1)
+    return set_err(ctx, PN_EINVAL, "indexed variant: bad args");
+  KArgs a;
+  a.frames = (const uint8_t*)base;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.n = n;
+  a.stride = 0;
+  a.ipa_off = 0;
+  a.avail = avail;
+  a.offs = offsets;
+  hipStream_t s = (hipStream_t)stream;
+  if (variant == 1) launch_one<0, 1, 0, kLoadAux, kStoreAux, 1>(a, s);
+  else launch_one<0, 0, 0, kLoadAux, kStoreAux, 1>(a, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
   ctx->last_stream = s;
   return PN_OK;
 }

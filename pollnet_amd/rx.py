@@ -111,6 +111,7 @@ _pn_tx_variant = _sig("pn_tx_fill_variant", _i32, _vp, _vp, _u32, _u32, _u32, _v
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
+_pn_idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
 _pn_gen_conn_table = _sig("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)
@@ -271,6 +272,11 @@ class RxContext:
         """Tuning-only TX fill shapes (scripts/tx_variants.py); not part of the C header."""
         _check(_pn_tx_variant(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), variant,
                               _stream_handle(stream)), self._h, "pn_tx_fill_variant")
+
+    def classify_indexed_variant(self, base, offsets, eth_mod16, n, avail, results, stream, variant):
+        """Tuning-only indexed kernel shapes (scripts/bench_indexed.py); not part of the C header."""
+        _check(_pn_idx_variant(self._h, _ptr(base), _ptr(offsets), eth_mod16, n, avail, _ptr(results),
+                               _stream_handle(stream), variant), self._h, "pn_classify_indexed_variant")
 
     def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, store_bytes=0):
         _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, store_bytes, _ptr(sink_dev),

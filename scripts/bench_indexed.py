@@ -45,12 +45,15 @@ def main():
         "strided": lambda: ctx.classify(frames, stride, off, n, out, st),
         "indexed_in_order": lambda: ctx.classify_indexed(frames, ident, off, n, stride - off, out, st),
         "indexed_permuted": lambda: ctx.classify_indexed(frames, perm, off, n, stride - off, out, st),
+        "indexed_in_order_perlane": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 0),
+        "indexed_in_order_coop": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 1),
+        "indexed_permuted_coop": lambda: ctx.classify_indexed_variant(frames, perm, off, n, stride - off, out, st, 1),
     }
     for name, f in runs.items():  # parity first
         f()
         torch.cuda.synchronize()
         g = out.cpu().numpy().view(pa.RESULT_DTYPE)
-        exp = r[perm_ids] if name == "indexed_permuted" else r
+        exp = r[perm_ids] if "permuted" in name else r
         assert np.array_equal(g, exp), name
     times = {k: [] for k in runs}
     for _ in range(a.rounds):

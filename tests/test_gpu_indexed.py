@@ -119,6 +119,37 @@ def test_packed_layout_vs_oracle(torch_cuda, ctx, eth_mod16):
     assert np.array_equal(got, exp), _first_diff(got, exp)
 
 
+def test_cooperative_window_eligibility(torch_cuda, ctx):
+    """The indexed kernel loads each frame's line cooperatively when every frame of a wave
+    has its header window at line + 16 inside [base, eth + avail); otherwise that wave
+    loads per-lane windows.  Waves all eligible, mixed (same eth_mod16 class, window at
+    line + 32), the ring base off the 128-B grid, and a first frame whose line starts at
+    base: every record equals the oracle's."""
+    R, stride, avail = 4096, 2048, 2048 - 18
+    p = pa.rx.GenParams.for_config(5)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    ctx.set_conn_table(t)
+    a = pa.gen_frames(p, R, stride, 2)
+    b = pa.gen_frames(p, R, stride, 18, first_index=R)
+    rng = np.random.default_rng(11)
+    use_b = np.zeros(R, dtype=bool)
+    use_b[64 * 16:] = rng.random(R - 64 * 16) < 0.3  # first 16 waves all eligible, the rest mixed
+    use_b[64 * 40:64 * 41] = True                     # one wave all at line + 32
+    slots = np.where(use_b[:, None], b, a)
+    offs = np.arange(R, dtype=np.uint64) * stride + np.where(use_b, 18, 2).astype(np.uint64)
+    exp = np.empty(R, dtype=pa.RESULT_DTYPE)
+    flat = slots.reshape(-1)
+    for i in range(R):
+        o = int(offs[i])
+        exp[i] = orc.classify_frame(flat[o:o + avail].tobytes(), avail, e, m, t.max_conn_cnt)
+    dev = torch_cuda.from_numpy(np.concatenate([np.zeros(16, np.uint8), flat])).cuda()
+    got = _indexed(torch_cuda, ctx, dev[16:], offs, 2, avail)  # base 16 B off the allocation's 128-B grid
+    assert np.array_equal(got, exp), _first_diff(got, exp)
+    got = _indexed(torch_cuda, ctx, torch_cuda.from_numpy(flat).cuda(), offs, 2, avail)
+    assert np.array_equal(got, exp), _first_diff(got, exp)
+
+
 def test_offsets_outside_the_class_get_badoff(torch_cuda, ctx):
     R, stride, off = 512, 2048, 2
     p = pa.rx.GenParams.for_config(2)
