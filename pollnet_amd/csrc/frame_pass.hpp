@@ -31,6 +31,11 @@ constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
 // bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
 // masks, bit3 no record store.
 enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8, kAblStore8 = 16, kAblGlobalStore = 32 };
+// Not an ablation: kExactRange bounds each frame's stream descriptor at its extent rounded
+// up to a dword, so the hardware's per-dword range check zeroes the bytes past the extent
+// and the per-dword tail masks go; a 2-mod-4 extent leaves 2 bytes of the last dword,
+// subtracted on the lane that loaded them.
+enum : int { kExactRange = 64 };
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the
@@ -127,7 +132,8 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       const uint32_t fi = b0 + j; // wave-uniform
       const int end = __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1; // bit 0 = odd tcp_len, read below
       ends[j] = end;
-      const uint32_t end16 = (uint32_t)(end + 15) & ~15u; // 0 for frames past n (end_rel = 0 there)
+      const uint32_t end16 = (ABL & kExactRange) ? ((uint32_t)(end + 3) & ~3u)  // dword-exact extent
+                                                 : ((uint32_t)(end + 15) & ~15u); // 0 for frames past n (end_rel = 0 there)
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi), end16);
       // out-of-range chunks of a buffer load return 0 and fetch nothing
       w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, LAUX);
@@ -135,7 +141,7 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
     auto sel = [](int e, int o) -> uint32_t {
-      if constexpr (ABL & kAblNoMask) return 0x10001u;
+      if constexpr (ABL & (kAblNoMask | kExactRange)) return 0x10001u;
       else return tail_sel(e, o);
     };
 #pragma unroll
@@ -152,6 +158,16 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       sum = dot2(w1.y, sel(end, o1 + 4), sum);
       sum = dot2(w1.z, sel(end, o1 + 8), sum);
       sum = dot2(w1.w, sel(end, o1 + 12), sum);
+      if constexpr (ABL & kExactRange) {
+        // end % 4 == 2: the last dword loaded holds the 2 bytes after the extent (its high half)
+        const int q = end - 2 - kWinBytes; // wave-uniform
+        if ((end & 2) && q >= 0 && q < 2048) {
+          const u32x4 w = (q < 1024) ? w0 : w1;
+          const int dw = (q >> 2) & 3;
+          const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
+          if (lane == ((q & 1023) >> 4)) sum -= d >> 16;
+        }
+      }
       acc[j] = sum;
       // odd tcp_len: the RFC verdict needs the byte the reference sums past the segment (window
       // offset end - 1); take it from the lane that streamed it instead of re-reading the line later

@@ -191,7 +191,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
 // class); per-frame stream descriptors; with COOP, waves whose frames all have their
 // window at line + 16 load lines cooperatively, other waves per-lane bounds-checked windows.
-template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
+template <int MIS, int COOP, int ABL = kExactRange, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 // 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
 // default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
 __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
@@ -339,7 +339,7 @@ bool coop_layout(const KArgs& a) {
   return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
 }
 
-template <int MIS, int COOP, int ABL = 0, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
+template <int MIS, int COOP, int ABL = kExactRange, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 void launch_one(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>),
                      dim3((a.n + kFramesPerWave - 1) / kFramesPerWave), dim3(kWave), 0, s, a);
@@ -486,14 +486,14 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 2: launch_one<2, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 4: launch_one<4, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 6: launch_one<6, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 8: launch_one<8, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 10: launch_one<10, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 12: launch_one<12, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
-    default: launch_one<14, 1, 0, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 0: launch_one<0, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 2: launch_one<2, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 4: launch_one<4, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 6: launch_one<6, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 8: launch_one<8, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 10: launch_one<10, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 12: launch_one<12, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    default: launch_one<14, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
@@ -520,8 +520,8 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   a.avail = avail;
   a.offs = offsets;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 1) launch_one<0, 1, 0, kLoadAux, kStoreAux, 1>(a, s);
-  else launch_one<0, 0, 0, kLoadAux, kStoreAux, 1>(a, s);
+  if (variant == 1) launch_one<0, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s);
+  else launch_one<0, 0, kExactRange, kLoadAux, kStoreAux, 1>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
   ctx->last_stream = s;
@@ -551,18 +551,19 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   switch (variant) {
     case 0: launch_one<0, 0>(a, s); break;                         // per-lane window
     case 1: launch_one<0, 1>(a, s); break;                         // cooperative window (production here)
-    case 2: launch_one<0, 0, 0, 0, 0>(a, s); break;                // per-lane, default cache policy
-    case 3: launch_one<0, 1, 0, 0, 0>(a, s); break;                // cooperative, default cache policy
-    case 4: launch_one<0, 1, 0, kLoadAux, kStoreAux, 0, 0>(a, s); break; // line-0 window default policy
-    case 5: launch_one<0, 1, 0, kLoadAux, 0>(a, s); break;         // default-policy record stores
-    case 6: launch_one<0, 1, 0, kLoadAux, 0, 0, 0>(a, s); break;   // both
-    case 7: launch_one<0, 1, 0, kLoadAux, 2>(a, s); break;         // nt record stores
-    case 8: launch_one<0, 1, kAblGlobalStore>(a, s); break;        // plain global record store
-    case 19: launch_one<0, 1, kAblStore8>(a, s); break;            // timing only: 8-B stores
-    case 11: launch_one<0, 1, kAblNoProbe>(a, s); break;           // timing-only ablations from here
-    case 12: launch_one<0, 1, kAblNoReduce>(a, s); break;
+    case 2: launch_one<0, 0, kExactRange, 0, 0>(a, s); break;                // per-lane, default cache policy
+    case 3: launch_one<0, 1, kExactRange, 0, 0>(a, s); break;                // cooperative, default cache policy
+    case 4: launch_one<0, 1, kExactRange, kLoadAux, kStoreAux, 0, 0>(a, s); break; // line-0 window default policy
+    case 5: launch_one<0, 1, kExactRange, kLoadAux, 0>(a, s); break;         // default-policy record stores
+    case 6: launch_one<0, 1, kExactRange, kLoadAux, 0, 0, 0>(a, s); break;   // both
+    case 7: launch_one<0, 1, kExactRange, kLoadAux, 2>(a, s); break;         // nt record stores
+    case 8: launch_one<0, 1, kAblGlobalStore | kExactRange>(a, s); break;        // plain global record store
+    case 9: launch_one<0, 1, 0>(a, s); break;                      // 16-B stream descriptors + per-dword tail masks
+    case 19: launch_one<0, 1, kAblStore8 | kExactRange>(a, s); break;            // timing only: 8-B stores
+    case 11: launch_one<0, 1, kAblNoProbe | kExactRange>(a, s); break;           // timing-only ablations from here
+    case 12: launch_one<0, 1, kAblNoReduce | kExactRange>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
-    case 18: launch_one<0, 1, kAblNoStore>(a, s); break;
+    case 18: launch_one<0, 1, kAblNoStore | kExactRange>(a, s); break;
     default: return set_err(ctx, PN_EINVAL, "variant: unknown");
   }
   hipError_t e = hipGetLastError();
