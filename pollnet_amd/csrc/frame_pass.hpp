@@ -36,6 +36,16 @@ enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8,
 // and the per-dword tail masks go; a 2-mod-4 extent leaves 2 bytes of the last dword,
 // subtracted on the lane that loaded them.
 enum : int { kExactRange = 64 };
+// kCompact: the stream phase walks a wave-wide list of the 1-KiB chunks that hold bytes
+// (frame-major, popped from two ballots on the scalar unit) 16 loads at a time, instead of
+// 2 loads per frame for 8 frames; short frames then no longer issue empty loads, so every
+// batch carries up to 16 KiB (stream_phase_compact).
+enum : int { kCompact = 128 };
+// kCoopProbe: conn-table lookups that continue past the home slot are finished by the whole
+// wave, 64 entries per round trip (header_phase in rx_kernel.hip).
+enum : int { kCoopProbe = 256 };
+// The production RX configuration.
+constexpr int kProdAbl = kExactRange | kCoopProbe;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the
@@ -104,6 +114,157 @@ __device__ __forceinline__ uint32_t window_sum_from(const Window& h, int end) {
   return t;
 }
 
+// Exact sum of v over the wave, returned on every lane (jumbo tails only).
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+  v += dpp<0xB1>(v);  // lane ^ 1
+  v += dpp<0x4E>(v);  // lane ^ 2
+  v += dpp<0x141>(v); // other quad of the 8
+  v += dpp<0x128>(v); // lane ^ 8 (row_ror:8)
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+
+// Compacted stream (ABL & kCompact): the wave's chunk list is every (frame, KiB) pair
+// whose KiB holds bytes of the frame's extent past the window (KiBs 0 and 1; jumbo KiBs
+// after the list), frame-major.  Chunks are popped from the ballots m1 (frames with >= 1
+// chunk) and m2 (2 chunks) on the scalar unit, 16 per batch; the 16 per-lane partials are
+// transpose-reduced so chunk c's total lands on lane 4c, which adds it to its frame's LDS
+// cell (ds_add_u32); lane f collects its cell at the end.
+template <int ABL, int LAUX, int IDX>
+__device__ __forceinline__ void stream_phase_compact(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win,
+                                                     int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
+  constexpr int kC = 16; // chunks per batch
+  __shared__ uint32_t cell[kFramesPerWave + 1]; // + a sink for the empty chunks of the last batch
+  auto frame_win = [&](uint32_t fi) -> const uint8_t* {
+    if constexpr (IDX) {
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_win, fi);
+      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_win >> 32), fi);
+      return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+    } else {
+      return group_ipa + (uint64_t)fi * stride;
+    }
+  };
+  cell[lane] = 0;
+  if (lane == 0) cell[kFramesPerWave] = 0;
+  const int my_end = end_rel & ~1;
+  uint64_t m1 = __ballot(my_end > kWinBytes);
+  const uint64_t m2 = __ballot(my_end > kWinBytes + 1024);
+  const uint64_t mj = __ballot(my_end > kWinBytes + 2048);
+  __syncthreads();
+  bool pend = false; // chunk 1 of frame fp is next
+  uint32_t fp = 0;
+  while (m1 != 0 || pend) { // wave-uniform
+    u32x4 w[kC];
+    uint32_t fr[kC], kb[kC];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      uint32_t f, k;
+      if (pend) {
+        f = fp;
+        k = 1;
+        pend = false;
+      } else if (m1 != 0) {
+        f = (uint32_t)__builtin_ctzll(m1);
+        m1 &= m1 - 1;
+        k = 0;
+        pend = (m2 >> f) & 1;
+        fp = f;
+      } else {
+        f = kFramesPerWave; // empty chunk: fetches nothing, lands in the sink cell
+        k = 0;
+      }
+      fr[j] = f;
+      kb[j] = k;
+      const int end = f < kFramesPerWave ? (__builtin_amdgcn_readlane(end_rel, f) & ~1) : 0;
+      const uint32_t ext = (uint32_t)(end + 3) & ~3u; // dword-exact extent (0: nothing)
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(f < kFramesPerWave ? frame_win(f) : group_ipa, ext);
+      w[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 * k + lane * 16, 0, LAUX);
+    }
+    __builtin_amdgcn_sched_barrier(0); // the whole batch in flight before the first wait
+    uint32_t acc[kC];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      uint32_t sum = 0;
+      sum = dot2(w[j].x, 0x10001u, sum);
+      sum = dot2(w[j].y, 0x10001u, sum);
+      sum = dot2(w[j].z, 0x10001u, sum);
+      sum = dot2(w[j].w, 0x10001u, sum);
+      const uint32_t f = fr[j];
+      if (f < kFramesPerWave) { // wave-uniform
+        const int er = __builtin_amdgcn_readlane(end_rel, f);
+        const int end = er & ~1;
+        const int c0 = kWinBytes + 1024 * (int)kb[j]; // window offset of this chunk
+        // end % 4 == 2: the last dword loaded holds the 2 bytes after the extent (its high half)
+        const int q = end - 2 - c0;
+        if ((end & 2) && q >= 0 && q < 1024) {
+          const int dw = (q >> 2) & 3;
+          const uint32_t d = dw == 0 ? w[j].x : dw == 1 ? w[j].y : dw == 2 ? w[j].z : w[j].w;
+          if (lane == (q >> 4)) sum -= d >> 16;
+        }
+        // odd tcp_len: the byte after the segment (window offset end - 1), from the lane that loaded it
+        const int p = end - 1 - c0;
+        if ((er & 1) && p >= 0 && p < 1024) {
+          const int dw = (p >> 2) & 3;
+          const uint32_t d = dw == 0 ? w[j].x : dw == 1 ? w[j].y : dw == 2 ? w[j].z : w[j].w;
+          const uint32_t b = __builtin_amdgcn_readlane((d >> (8 * (p & 3))) & 0xff, p >> 4);
+          if ((uint32_t)lane == f) pad = b;
+        }
+      }
+      acc[j] = sum;
+    }
+    // transpose-reduce 16 chunks x 64 lanes: chunk c's total on lanes 4c..4c+3
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { // xor 32
+      const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 8], false, false);
+      acc[i] = r[0] + r[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { // xor 16
+      const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 4], false, false);
+      acc[i] = r[0] + r[1];
+    }
+    const bool b3 = lane & 8, b2 = lane & 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { // xor 8: keep one, send the other
+      const uint32_t keep = b3 ? acc[i + 2] : acc[i];
+      const uint32_t send = b3 ? acc[i] : acc[i + 2];
+      acc[i] = keep + dpp<0x128>(send); // row_ror:8
+    }
+    {
+      const uint32_t keep = b2 ? acc[1] : acc[0];
+      const uint32_t send = b2 ? acc[0] : acc[1];
+      uint32_t v = keep + dpp<0x141>(send); // row_half_mirror: lane i <-> 7 - i of its 8
+      v += dpp<0xB1>(v);                    // lane ^ 1
+      v += dpp<0x4E>(v);                    // lane ^ 2
+      // lane 4c holds chunk c = b2 + 2*b3 + 4*b4 + 8*b5 = lane >> 2; hand it its frame index
+      uint32_t fv = kFramesPerWave;
+#pragma unroll
+      for (int j = 0; j < kC; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(fv) : "s"(fr[j]), "i"(4 * j));
+      if ((lane & 3) == 0) atomicAdd(&cell[fv], v);
+    }
+  }
+  // jumbo slots only (extent past window + 2 KiB): the remaining KiBs, frame by frame
+  for (uint64_t m = mj; m != 0; m &= m - 1) {
+    const uint32_t f = (uint32_t)__builtin_ctzll(m);
+    const int end = __builtin_amdgcn_readlane(end_rel, f) & ~1;
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(f), (uint32_t)(end + 15) & ~15u);
+    uint32_t sum = 0;
+    for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
+      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
+      const int o = kb + lane * 16;
+      sum = dot2(w.x, tail_sel(end, o), sum);
+      sum = dot2(w.y, tail_sel(end, o + 4), sum);
+      sum = dot2(w.z, tail_sel(end, o + 8), sum);
+      sum = dot2(w.w, tail_sel(end, o + 12), sum);
+    }
+    const uint32_t tot = wave_sum(sum);
+    if ((uint32_t)lane == f) t_all += tot;
+  }
+  __syncthreads();
+  t_all += cell[lane];
+}
+
 // ---- phase 2: the wave streams every frame's region past the window ----
 // group_ipa: window start of the group's first slot; frame fi's window is at
 // group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
@@ -111,6 +272,11 @@ __device__ __forceinline__ uint32_t window_sum_from(const Window& h, int end) {
 template <int ABL, int LAUX, int IDX>
 __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
                                              int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
+  if constexpr (ABL & kCompact) {
+    (void)n_here; // lanes past n have end_rel = 0: no chunks
+    stream_phase_compact<ABL, LAUX, IDX>(stride, group_ipa, my_win, lane, end_rel, t_all, pad);
+    return;
+  }
   // window start of frame fi: strided from the group's first slot, or (indexed) the
   // address its own lane computed, broadcast with two readlanes
   auto frame_win = [&](uint32_t fi) -> const uint8_t* {

@@ -113,21 +113,91 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 
   // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
   st.conn_id = PN_MISS;
-  if (live && !(ABL & kAblNoProbe)) {
+  if constexpr (!(ABL & kAblNoProbe)) {
     const uint32_t ip_h = __builtin_bswap32(st.src_ip);
     const uint32_t port_h = bswap16(src_port);
     const uint64_t key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
     uint32_t e = (uint32_t)(key & a.mask);
     uint64_t k = PN_EMPTY_KEY;
     uint32_t cid = 0;
-    while (e < a.n_entries) {
+    if (live && e < a.n_entries) { // the home slot: almost every lookup ends here
       const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
       k = ((uint64_t)ent.y << 32) | ent.x;
       cid = ent.z;
-      if (k >= key) break;
-      ++e;
     }
-    if (e < a.n_entries && k == key) {
+    if constexpr (ABL & kCoopProbe) {
+      // Lanes whose run continues past the home slot are served one at a time by the whole
+      // wave (all 64 lanes reach here): 64 consecutive entries per round trip, the first with
+      // key >= the lane's key (or the array end) found by a ballot -- the entry the scalar
+      // walk stops at.
+      const uint32_t lane = threadIdx.x;
+      bool srch = live && e < a.n_entries && k < key;
+      if (__ballot(srch) != 0) {
+        // short runs (the common case past the home slot): every searching lane fetches its
+        // next kAhead entries at once -- one round trip for all of them, in parallel
+        constexpr int kAhead = 2;
+        u32x4 nx[kAhead];
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j) {
+          nx[j] = u32x4{0u, 0u, 0u, 0u};
+          if (srch && e + 1 + j < a.n_entries) nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + e + 1 + j);
+        }
+        uint32_t step = 0, cid2 = 0;
+        uint64_t k2 = 0;
+#pragma unroll
+        for (int j = kAhead - 1; j >= 0; --j) { // the first entry (in order) that stops the walk
+          const uint64_t kk = ((uint64_t)nx[j].y << 32) | nx[j].x;
+          if (e + 1 + j >= a.n_entries || kk >= key) {
+            step = j + 1;
+            k2 = kk;
+            cid2 = nx[j].z;
+          }
+        }
+        if (srch) {
+          if (step != 0) {
+            e += step;
+            k = k2;
+            cid = cid2;
+            srch = false;
+          } else {
+            e += kAhead; // every fetched key < key: the run goes on
+          }
+        }
+      }
+      uint64_t need = __ballot(srch);
+      while (need != 0) { // wave-uniform
+        const uint32_t L = (uint32_t)__builtin_ctzll(need);
+        need &= need - 1;
+        const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L); // readlane returns int
+        for (uint32_t base = __builtin_amdgcn_readlane(e, L) + 1;; base += kWave) {
+          const uint32_t idx = base + lane;
+          u32x4 ent = {0u, 0u, 0u, 0u};
+          if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
+          const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
+          const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
+          if (stop != 0) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(stop);
+            const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
+            const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
+            if (lane == L) {
+              e = base + first;
+              k = ((uint64_t)khi << 32) | klo;
+              cid = c;
+            }
+            break;
+          }
+        }
+      }
+    } else {
+      while (live && e < a.n_entries && k < key) {
+        if (++e >= a.n_entries) break;
+        const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
+        k = ((uint64_t)ent.y << 32) | ent.x;
+        cid = ent.z;
+      }
+    }
+    if (live && e < a.n_entries && k == key) {
       st.conn_id = cid;
       flags |= PN_F_HIT;
       if (cid >= a.max_conn) flags |= PN_F_TW;
@@ -191,7 +261,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
 // class); per-frame stream descriptors; with COOP, waves whose frames all have their
 // window at line + 16 load lines cooperatively, other waves per-lane bounds-checked windows.
-template <int MIS, int COOP, int ABL = kExactRange, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
+template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 // 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
 // default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
 __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
@@ -224,7 +294,7 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
       // frame load its line coalesced into the LDS tile (one request per line), as the
       // strided kernel does; otherwise the wave falls back to per-lane windows.
       const bool use = live && !bad_off;
-      const bool elig = !use || ((((uintptr_t)win & 127u) == 16) && o + 14 >= (uint64_t)(MIS + 16) &&
+      const bool elig = !use || ((((uintptr_t)win & 15u) == 0) && o + 14 >= (uint64_t)(MIS + 16) &&
                                  (uint32_t)(14 - MIS + kWinBytes) <= a.avail);
       if (__all(elig)) {
         __shared__ uint64_t line_addr[kFramesPerWave];
@@ -339,7 +409,7 @@ bool coop_layout(const KArgs& a) {
   return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
 }
 
-template <int MIS, int COOP, int ABL = kExactRange, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
+template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
 void launch_one(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>),
                      dim3((a.n + kFramesPerWave - 1) / kFramesPerWave), dim3(kWave), 0, s, a);
@@ -486,14 +556,14 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 2: launch_one<2, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 4: launch_one<4, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 6: launch_one<6, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 8: launch_one<8, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 10: launch_one<10, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 12: launch_one<12, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
-    default: launch_one<14, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
@@ -520,8 +590,8 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   a.avail = avail;
   a.offs = offsets;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 1) launch_one<0, 1, kExactRange, kLoadAux, kStoreAux, 1>(a, s);
-  else launch_one<0, 0, kExactRange, kLoadAux, kStoreAux, 1>(a, s);
+  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s);
+  else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
   ctx->last_stream = s;
@@ -551,19 +621,22 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   switch (variant) {
     case 0: launch_one<0, 0>(a, s); break;                         // per-lane window
     case 1: launch_one<0, 1>(a, s); break;                         // cooperative window (production here)
-    case 2: launch_one<0, 0, kExactRange, 0, 0>(a, s); break;                // per-lane, default cache policy
-    case 3: launch_one<0, 1, kExactRange, 0, 0>(a, s); break;                // cooperative, default cache policy
-    case 4: launch_one<0, 1, kExactRange, kLoadAux, kStoreAux, 0, 0>(a, s); break; // line-0 window default policy
-    case 5: launch_one<0, 1, kExactRange, kLoadAux, 0>(a, s); break;         // default-policy record stores
-    case 6: launch_one<0, 1, kExactRange, kLoadAux, 0, 0, 0>(a, s); break;   // both
-    case 7: launch_one<0, 1, kExactRange, kLoadAux, 2>(a, s); break;         // nt record stores
-    case 8: launch_one<0, 1, kAblGlobalStore | kExactRange>(a, s); break;        // plain global record store
+    case 2: launch_one<0, 0, kProdAbl, 0, 0>(a, s); break;                // per-lane, default cache policy
+    case 3: launch_one<0, 1, kProdAbl, 0, 0>(a, s); break;                // cooperative, default cache policy
+    case 4: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, 0>(a, s); break; // line-0 window default policy
+    case 5: launch_one<0, 1, kProdAbl, kLoadAux, 0>(a, s); break;         // default-policy record stores
+    case 6: launch_one<0, 1, kProdAbl, kLoadAux, 0, 0, 0>(a, s); break;   // both
+    case 7: launch_one<0, 1, kProdAbl, kLoadAux, 2>(a, s); break;         // nt record stores
+    case 8: launch_one<0, 1, kAblGlobalStore | kProdAbl>(a, s); break;        // plain global record store
     case 9: launch_one<0, 1, 0>(a, s); break;                      // 16-B stream descriptors + per-dword tail masks
-    case 19: launch_one<0, 1, kAblStore8 | kExactRange>(a, s); break;            // timing only: 8-B stores
-    case 11: launch_one<0, 1, kAblNoProbe | kExactRange>(a, s); break;           // timing-only ablations from here
-    case 12: launch_one<0, 1, kAblNoReduce | kExactRange>(a, s); break;
+    case 19: launch_one<0, 1, kAblStore8 | kProdAbl>(a, s); break;            // timing only: 8-B stores
+    case 20: launch_one<0, 1, kProdAbl | kCompact>(a, s); break;              // compacted chunk list
+    case 21: launch_one<0, 0, kProdAbl | kCompact>(a, s); break;              // per-lane window + compacted
+    case 22: launch_one<0, 1, kExactRange>(a, s); break;                         // scalar probe walk (before kCoopProbe)
+    case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
+    case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
-    case 18: launch_one<0, 1, kAblNoStore | kExactRange>(a, s); break;
+    case 18: launch_one<0, 1, kAblNoStore | kProdAbl>(a, s); break;
     default: return set_err(ctx, PN_EINVAL, "variant: unknown");
   }
   hipError_t e = hipGetLastError();

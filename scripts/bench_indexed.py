@@ -41,7 +41,22 @@ def main():
     ctx.classify(frames, stride, off, n, ref, st)
     torch.cuda.synchronize()
     r = ref.cpu().numpy().view(pa.RESULT_DTYPE)
+    # packed capture layout: each frame (+ its pad byte, zero) copied back to back, the next
+    # Ethernet header at the next 16-B boundary + 2 (same alignment class as the slots)
+    tl = (s[:, off + 16].astype(np.int64) << 8) | s[:, off + 17]
+    ln = 14 + tl + 1
+    starts = np.empty(n, np.int64)
+    pos = off
+    for i in range(n):
+        starts[i] = pos
+        pos = ((pos + int(ln[i]) + 15) & ~15) + off
+    packed = np.zeros(pos + stride, np.uint8)
+    for i in range(n):
+        packed[starts[i]:starts[i] + ln[i]] = s[i, off:off + ln[i]]
+    packed_dev = torch.from_numpy(packed).cuda()
+    poffs = torch.from_numpy(starts.astype(np.uint64).view(np.int64)).cuda()
     runs = {
+        "indexed_packed": lambda: ctx.classify_indexed(packed_dev, poffs, off, n, stride - off, out, st),
         "strided": lambda: ctx.classify(frames, stride, off, n, out, st),
         "indexed_in_order": lambda: ctx.classify_indexed(frames, ident, off, n, stride - off, out, st),
         "indexed_permuted": lambda: ctx.classify_indexed(frames, perm, off, n, stride - off, out, st),
@@ -66,7 +81,7 @@ def main():
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) / a.reps)
     algo = wire + 16 * n
-    res = {"config": a.config, "frames": n, "records_equal": True}
+    res = {"config": a.config, "frames": n, "records_equal": True, "packed_bytes": int(pos), "slot_bytes": n * stride}
     for k, v in times.items():
         ms = statistics.median(v)
         res[k] = {"ms_median": round(ms, 4), "algo_tbps": round(algo / (ms * 1e-3) / 1e12, 3),

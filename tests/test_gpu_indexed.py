@@ -120,11 +120,11 @@ def test_packed_layout_vs_oracle(torch_cuda, ctx, eth_mod16):
 
 
 def test_cooperative_window_eligibility(torch_cuda, ctx):
-    """The indexed kernel loads each frame's line cooperatively when every frame of a wave
-    has its header window at line + 16 inside [base, eth + avail); otherwise that wave
-    loads per-lane windows.  Waves all eligible, mixed (same eth_mod16 class, window at
-    line + 32), the ring base off the 128-B grid, and a first frame whose line starts at
-    base: every record equals the oracle's."""
+    """The indexed kernel loads each frame's 128-B window block (from the 16-B chunk before
+    the IP header's) cooperatively when every frame of a wave has that block 16-B aligned
+    inside [base, eth + avail); otherwise that wave loads per-lane windows.  Waves with
+    the block on the line grid, off it (line + 32), mixed, the ring base off the 128-B
+    grid, and a first frame whose block starts at base: every record equals the oracle's."""
     R, stride, avail = 4096, 2048, 2048 - 18
     p = pa.rx.GenParams.for_config(5)
     t = pa.gen_conn_table(p)
@@ -148,6 +148,29 @@ def test_cooperative_window_eligibility(torch_cuda, ctx):
     assert np.array_equal(got, exp), _first_diff(got, exp)
     got = _indexed(torch_cuda, ctx, torch_cuda.from_numpy(flat).cuda(), offs, 2, avail)
     assert np.array_equal(got, exp), _first_diff(got, exp)
+
+
+def test_window_fallback_at_ring_start(torch_cuda, ctx):
+    """eth_mod16 = 0 puts the IP header's chunk at eth + 14 - 14: frame 0 at base + 0 has no
+    16 B before its window inside the ring, so its wave falls back to per-lane windows
+    (bounds-checked at base); the other waves load cooperatively.  Records equal the
+    oracle's and the strided kernel's."""
+    R, stride = 2048, 2048
+    p = pa.rx.GenParams.for_config(3)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    ctx.set_conn_table(t)
+    slots = pa.gen_frames(p, R, stride, 0)
+    offs = np.arange(R, dtype=np.uint64) * stride
+    flat = slots.reshape(-1)
+    exp = np.empty(R, dtype=pa.RESULT_DTYPE)
+    for i in range(R):
+        o = int(offs[i])
+        exp[i] = orc.classify_frame(flat[o:o + stride].tobytes(), stride, e, m, t.max_conn_cnt)
+    got = _indexed(torch_cuda, ctx, torch_cuda.from_numpy(flat).cuda(), offs, 0, stride)
+    assert np.array_equal(got, exp), _first_diff(got, exp)
+    ref, _ = _strided(torch_cuda, ctx, slots, stride, 0, R)
+    assert np.array_equal(got, ref), _first_diff(got, ref)
 
 
 def test_offsets_outside_the_class_get_badoff(torch_cuda, ctx):

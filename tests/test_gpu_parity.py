@@ -204,6 +204,69 @@ def test_probe_runs_to_array_end_and_tiny_tables(torch_cuda, ctx):
     assert got[3]["conn_id"] == 0 and np.count_nonzero(got["flags"] & pa.F.HIT) == 1
 
 
+def _key_to_src(key):
+    """Inverse of connHashKey (Core.h:167-172): (ip, port) in host order for a 48-bit key."""
+    ip = (key >> 15) & 0xFFFFFFFF
+    port = (key & 0x7FFF) | (((key >> 47) & 1) << 15)
+    return f"{ip >> 24}.{(ip >> 16) & 255}.{(ip >> 8) & 255}.{ip & 255}", port
+
+
+@pytest.mark.parametrize("layout", ["sentinel", "array_end", "ordered_table"])
+def test_long_probe_runs(torch_cuda, ctx, layout):
+    """Probe runs far longer than one wave-cooperative pass (the kernel walks a run past
+    the home slot 2 entries per lane, then 64 entries per round trip for the whole wave):
+    hits at every depth of 300-entry runs, misses that stop on a larger key, runs that end
+    on the EmptyKey sentinel or at the array end, every lane of a wave searching at once."""
+    rng = np.random.default_rng(77)
+    keys = sorted({int(k) for k in rng.integers(1, 1 << 48, 420, dtype=np.int64)})[:400]
+    ip, port = _key_to_src(keys[5])
+    ip_be = int.from_bytes(bytes(int(x) for x in ip.split(".")), "little")
+    assert pa.conn_hash_key(ip_be, int.from_bytes(port.to_bytes(2, "big"), "little")) == keys[5]
+    present = keys[:300] if layout != "ordered_table" else keys[:320]
+    max_conn = 1 << 12
+    if layout == "ordered_table":  # the product table (addConnEntry): 4 clusters of one home slot each
+        t = pa.ConnTable(1024, 1024)
+        clustered = []
+        for i, k in enumerate(present):
+            k = (k & ~0xFFF) | (0x100 * (i % 4) + 7)  # same low 12 bits per cluster
+            clustered.append(k)
+            t.add(k, i)
+        present = clustered
+        ents, mask = t.snapshot()
+        max_conn = t.max_conn_cnt
+    else:
+        n_ent = len(present) + (20 if layout == "sentinel" else 0)
+        ents = np.zeros(n_ent, pa.ENTRY_DTYPE)
+        ents["key"] = pa.PN_EMPTY_KEY
+        ents["key"][: len(present)] = present
+        ents["conn_id"][: len(present)] = np.arange(len(present))
+        mask = 0  # every key's home is entry 0: one run of 300
+    pset = set(present)
+    absent = [k for k in keys if k not in pset]
+    pick = []
+    for i in range(4096):
+        r = i % 10
+        if r < 5:
+            pick.append(present[int(rng.integers(len(present)))])
+        elif r < 8:
+            pick.append(absent[int(rng.integers(len(absent)))])
+        else:
+            pick.append(int(rng.integers(1, 1 << 48)))
+    pick[:64] = [present[-1 - j] for j in range(64)]  # one wave whose 64 lanes all walk deep
+    frames = []
+    for k in pick:
+        ip, port = _key_to_src(k)
+        frames.append(make_frame(ip, port, payload=bytes(10)))
+    slots = to_slots(frames)
+    n = len(frames)
+    exp = orc.classify_batch(slots, STRIDE, FRAME_OFF, n, ents, mask, max_conn, threads=8)
+    got = gpu_classify(torch_cuda, ctx, slots, STRIDE, FRAME_OFF, n, ents, mask, max_conn, canary=5)
+    assert_same(got, exp)
+    hits = got["conn_id"][(got["flags"] & pa.F.HIT) != 0]
+    assert len(hits) > 1500 and int(hits.max()) >= 250  # hits deep in the runs happened
+    assert np.count_nonzero((got["flags"] & pa.F.HIT) == 0) > 1000
+
+
 def test_boundary_errors(torch_cuda, ctx):
     c = pa.RxContext(0)
     frames = torch_cuda.zeros(8192, dtype=torch_cuda.uint8, device="cuda")
