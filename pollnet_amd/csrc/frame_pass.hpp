@@ -50,13 +50,16 @@ constexpr int kProdAbl = kExactRange | kCoopProbe;
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the
 // slot's ether_type as stored (0x0008 = IPv4).
-// COOP = 1: 8 lanes per slot load its first 128-B line (exactly one request per line,
-// the line the window lives in) into an XOR-swizzled LDS tile that each lane reads
-// back; needs 128-B aligned lines with the window at line + 16.
-// COOP = 0: each lane loads its own window (any layout).
+// COOP = 1: 8 lanes per slot load its 128-B window block -- the 16-B chunk before the
+// window (ether_type) and the window -- into an XOR-swizzled LDS tile that each lane
+// reads back.  When the window sits at line + 16 (the default frame_off = 2 layout) the
+// block is the slot's first line: exactly one request per line.  Elsewhere it straddles
+// two lines, still 8 slots per instruction instead of one window per lane.
+// COOP = 0: each lane loads its own window (frame_off = 0, where no chunk precedes it).
 // The cooperative window's LDS tile: 64 slots x 128 B (8 KiB), chunk p of slot r at
-// r*8 + (p ^ (r&7)).  One static allocation per kernel; the TX fill writes patched lines
-// back from it.
+// r*8 + (p ^ (r&7)).  One static allocation per kernel; the TX fill writes patched
+// blocks back from it.
+__device__ __host__ __forceinline__ constexpr uint32_t coop_block(uint32_t ipa_off) { return ipa_off - 16; }
 __device__ __forceinline__ u32x4* coop_tile() {
   __shared__ u32x4 tile[kFramesPerWave * 8];
   return tile;
@@ -67,15 +70,15 @@ __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t r
                                                         uint32_t ipa_off, Window& h) {
   uint32_t ether_type;
   if constexpr (COOP) {
-    static_assert(MIS + 16 + kWinBytes <= 128 + 16, "window must sit in the slot's first line");
+    static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
     u32x4* tile = coop_tile();
-    const uint32_t line0 = ipa_off & ~127u;
+    const uint32_t blk = coop_block(ipa_off);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-      tile[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + line0 + 16 * part, 0, LAUX);
+      tile[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + blk + 16 * part, 0, LAUX);
     }
-    const uint32_t p0 = (ipa_off & 127u) >> 4; // == 1 on this path
+    constexpr uint32_t p0 = 1; // the window starts at the block's second chunk
 #pragma unroll
     for (int c = 0; c < kWinChunks; ++c) {
       const u32x4 v = tile[lane * 8 + ((p0 + c) ^ (lane & 7))];

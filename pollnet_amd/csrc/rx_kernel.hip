@@ -402,11 +402,12 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_kernel(const uint8_t* b
 
 // ============================ C-ABI ============================
 namespace {
-// Whether the cooperative header-window load applies: 128-B aligned slot lines
-// with the IP header's 16-B chunk at line offset 16 (the default frame_off = 2
-// layout, and ef_vi's 10 + prefix for prefix <= 5).
+// Whether the cooperative header-window load applies: a 16-B chunk precedes the
+// window inside the slot (frame_off >= 2) and blocks are 16-B aligned.  One request
+// per block line: a single line for the default frame_off = 2 layout and ef_vi's
+// 10 + prefix for prefix <= 5, two otherwise.
 bool coop_layout(const KArgs& a) {
-  return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
+  return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }
 
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
@@ -417,9 +418,7 @@ void launch_one(const KArgs& a, hipStream_t s) {
 
 template <int MIS>
 void launch(const KArgs& a, hipStream_t s) {
-  if constexpr (MIS + 16 + kWinBytes <= 128 + 16) {
-    if (coop_layout(a)) return launch_one<MIS, 1>(a, s);
-  }
+  if (coop_layout(a)) return launch_one<MIS, 1>(a, s);
   launch_one<MIS, 0>(a, s);
 }
 } // namespace
@@ -615,7 +614,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   a.avail = slot_stride - frame_off;
   a.offs = nullptr;
   hipStream_t s = (hipStream_t)stream;
-  if ((variant & 1) && !coop_layout(a)) return set_err(ctx, PN_EINVAL, "variant: needs ip at line+16");
+  if ((variant & 1) && !coop_layout(a)) return set_err(ctx, PN_EINVAL, "variant: needs the cooperative layout");
   // Tuning variants of the MIS = 0 (ip at slot+16) kernel, A/B-timed in one process by
   // scripts/variants.py; not part of the public header.  History: profiles/r01_experiments.
   switch (variant) {

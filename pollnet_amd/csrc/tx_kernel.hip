@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
     if constexpr (kTile) { // write the patched lines back, 8 lanes per 128-B line
       __syncthreads();
       u32x4* tile = coop_tile();
-      const uint32_t line0 = a.ipa_off & ~127u;
+      const uint32_t line0 = coop_block(a.ipa_off);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
@@ -197,17 +197,15 @@ __global__ __launch_bounds__(256) void tx_patch_kernel(TArgs a) {
 }
 
 bool coop_layout(const TArgs& a) {
-  return (a.stride % 128) == 0 && ((((uintptr_t)a.frames + a.ipa_off) & 127u) >> 4) == 1;
+  return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }
 
 template <int MIS, int MODE>
 void launch(const TArgs& a, hipStream_t s) {
   const dim3 grid((a.n + kFramesPerWave - 1) / kFramesPerWave), block(kWave);
-  if constexpr (MIS + 16 + kWinBytes <= 128 + 16) {
-    if (coop_layout(a)) {
-      hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE>), grid, block, 0, s, a);
-      return;
-    }
+  if (coop_layout(a)) {
+    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE>), grid, block, 0, s, a);
+    return;
   }
   hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE>), grid, block, 0, s, a);
 }
@@ -309,7 +307,8 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
   a.frame_off = frame_off;
-  if (!coop_layout(a)) return set_err(ctx, PN_EINVAL, "tx variant: needs the cooperative layout");
+  if (!coop_layout(a) || a.stride < a.ipa_off + kWinBytes)  // block write-back variants stay inside the slot
+    return set_err(ctx, PN_EINVAL, "tx variant: needs the cooperative layout");
   hipStream_t s = (hipStream_t)stream;
   int rc = ensure_patch(ctx, variant >= 15 ? 2 * n : n, s); // 16-B record variants need 2 patch slots per frame
   if (rc) return rc;

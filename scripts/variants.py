@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=15)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="0,1,2,3,18")
+    ap.add_argument("--frame-off", type=int, default=2, help="2 or 18 (the variant kernels are the MIS = 0 class)")
     ap.add_argument("--uncached", action="store_true", help="frame ring from hipExtMallocWithFlags(Uncached)")
     a = ap.parse_args()
     import numpy as np
@@ -33,9 +34,9 @@ def main():
     import pollnet_amd as pa
 
     p = pa.rx.GenParams.for_config(a.config)
-    s = pa.gen_frames(p, a.frames)
+    s = pa.gen_frames(p, a.frames, 2048, a.frame_off)
     t = pa.gen_conn_table(p)
-    wire = pa.wire_bytes(s, 2048, 2, a.frames)
+    wire = pa.wire_bytes(s, 2048, a.frame_off, a.frames)
     ctx = pa.RxContext(0)
     ctx.set_conn_table(t)
     frames = torch.from_numpy(s.reshape(-1)).cuda()
@@ -61,11 +62,11 @@ def main():
     res = torch.empty_like(ref)
     sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
-    ctx.classify(frames, 2048, 2, a.frames, ref, st)
+    ctx.classify(frames, 2048, a.frame_off, a.frames, ref, st)
     vs = [int(x) for x in a.variants.split(",")]
     for v in vs:
         res.zero_()
-        ctx.classify_variant(frames, 2048, 2, a.frames, res, st, v)
+        ctx.classify_variant(frames, 2048, a.frame_off, a.frames, res, st, v)
         torch.cuda.synchronize()
         if v not in TIMING_ONLY:
             assert torch.equal(res, ref), f"variant {v} differs from production"
@@ -93,13 +94,13 @@ def main():
         for b, wpg in SLOT_MODES:
             tgt = res if wpg else sink
             times[f"slotread_{b}_store{wpg}"].append(timed(lambda: ctx.calib_slot_read(frames, a.frames, 2048, b, tgt, st, wpg)))
-        times["prod"].append(timed(lambda: ctx.classify(frames, 2048, 2, a.frames, res, st)))
+        times["prod"].append(timed(lambda: ctx.classify(frames, 2048, a.frame_off, a.frames, res, st)))
         r0 = a.reps
         a.reps = 50
-        times["prod_b2b50"].append(timed(lambda: ctx.classify(frames, 2048, 2, a.frames, res, st)))
+        times["prod_b2b50"].append(timed(lambda: ctx.classify(frames, 2048, a.frame_off, a.frames, res, st)))
         a.reps = r0
         for v in vs:
-            times[v].append(timed(lambda: ctx.classify_variant(frames, 2048, 2, a.frames, res, st, v)))
+            times[v].append(timed(lambda: ctx.classify_variant(frames, 2048, a.frame_off, a.frames, res, st, v)))
     algo = wire + 16 * a.frames
     out = {"config": a.config, "frames": a.frames,
            "calib_stream_read_tbps": round(frames.numel() / (statistics.median(times["calib"]) * 1e-3) / 1e12, 3)}
