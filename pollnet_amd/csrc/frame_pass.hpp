@@ -36,11 +36,6 @@ enum : int { kAblNoProbe = 1, kAblNoReduce = 2, kAblNoMask = 4, kAblNoStore = 8,
 // and the per-dword tail masks go; a 2-mod-4 extent leaves 2 bytes of the last dword,
 // subtracted on the lane that loaded them.
 enum : int { kExactRange = 64 };
-// kCompact: the stream phase walks a wave-wide list of the 1-KiB chunks that hold bytes
-// (frame-major, popped from two ballots on the scalar unit) 16 loads at a time, instead of
-// 2 loads per frame for 8 frames; short frames then no longer issue empty loads, so every
-// batch carries up to 16 KiB (stream_phase_compact).
-enum : int { kCompact = 128 };
 // kCoopProbe: conn-table lookups that continue past the home slot are finished by the whole
 // wave, 64 entries per round trip (header_phase in rx_kernel.hip).
 enum : int { kCoopProbe = 256 };
@@ -65,9 +60,19 @@ __device__ __forceinline__ u32x4* coop_tile() {
   return tile;
 }
 
+// Whether 16-B part `part` of a window block starting at an address with low bits
+// `blk_lo` is loaded.  When the header fields (ip .. ip+64) end in the block's first line,
+// the parts in its second line are left out (zero in the tile): the stream starts at that
+// line (stream_start) and would request it a second time.
+template <int MIS>
+__device__ __forceinline__ bool block_part_needed(uint32_t blk_lo, uint32_t part) {
+  const uint32_t lo = blk_lo & 112u, s0 = 112u - lo;
+  return MIS + 64 > (int)s0 || 16 * part < 128 - lo;
+}
+
 template <int MIS, int COOP, int LAUX>
 __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t rs, int lane, uint32_t stride,
-                                                        uint32_t ipa_off, Window& h) {
+                                                        uint32_t ipa_off, uint32_t base_lo, Window& h) {
   uint32_t ether_type;
   if constexpr (COOP) {
     static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
@@ -76,7 +81,10 @@ __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t r
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-      tile[r * 8 + (part ^ (r & 7))] = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + blk + 16 * part, 0, LAUX);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (block_part_needed<MIS>(base_lo + r * stride + blk, part))
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + blk + 16 * part, 0, LAUX);
+      tile[r * 8 + (part ^ (r & 7))] = v;
     }
     constexpr uint32_t p0 = 1; // the window starts at the block's second chunk
 #pragma unroll
@@ -117,169 +125,32 @@ __device__ __forceinline__ uint32_t window_sum_from(const Window& h, int end) {
   return t;
 }
 
-// Exact sum of v over the wave, returned on every lane (jumbo tails only).
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  v += dpp<0xB1>(v);  // lane ^ 1
-  v += dpp<0x4E>(v);  // lane ^ 2
-  v += dpp<0x141>(v); // other quad of the 8
-  v += dpp<0x128>(v); // lane ^ 8 (row_ror:8)
-  v += __shfl_xor(v, 16);
-  v += __shfl_xor(v, 32);
-  return v;
+// The header lane's share of the summed region [MIS, end): the window's words below the
+// stream start s0; when s0 = 0 < MIS the stream also sums [0, MIS), taken back here.
+template <int MIS>
+__device__ __forceinline__ uint32_t window_part(const Window& h, int end, uint32_t s0) {
+  uint32_t t = window_sum_from<MIS>(h, min(end, (int)s0));
+  if constexpr (MIS > 0) {
+    if (s0 == 0 && end > 0) t -= h.template sum16<0, MIS>();
+  }
+  return t;
 }
 
-// Compacted stream (ABL & kCompact): the wave's chunk list is every (frame, KiB) pair
-// whose KiB holds bytes of the frame's extent past the window (KiBs 0 and 1; jumbo KiBs
-// after the list), frame-major.  Chunks are popped from the ballots m1 (frames with >= 1
-// chunk) and m2 (2 chunks) on the scalar unit, 16 per batch; the 16 per-lane partials are
-// transpose-reduced so chunk c's total lands on lane 4c, which adds it to its frame's LDS
-// cell (ds_add_u32); lane f collects its cell at the end.
-template <int ABL, int LAUX, int IDX>
-__device__ __forceinline__ void stream_phase_compact(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win,
-                                                     int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
-  constexpr int kC = 16; // chunks per batch
-  __shared__ uint32_t cell[kFramesPerWave + 1]; // + a sink for the empty chunks of the last batch
-  auto frame_win = [&](uint32_t fi) -> const uint8_t* {
-    if constexpr (IDX) {
-      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_win, fi);
-      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_win >> 32), fi);
-      return (const uint8_t*)(((uint64_t)hi << 32) | lo);
-    } else {
-      return group_ipa + (uint64_t)fi * stride;
-    }
-  };
-  cell[lane] = 0;
-  if (lane == 0) cell[kFramesPerWave] = 0;
-  const int my_end = end_rel & ~1;
-  uint64_t m1 = __ballot(my_end > kWinBytes);
-  const uint64_t m2 = __ballot(my_end > kWinBytes + 1024);
-  const uint64_t mj = __ballot(my_end > kWinBytes + 2048);
-  __syncthreads();
-  bool pend = false; // chunk 1 of frame fp is next
-  uint32_t fp = 0;
-  while (m1 != 0 || pend) { // wave-uniform
-    u32x4 w[kC];
-    uint32_t fr[kC], kb[kC];
-#pragma unroll
-    for (int j = 0; j < kC; ++j) {
-      uint32_t f, k;
-      if (pend) {
-        f = fp;
-        k = 1;
-        pend = false;
-      } else if (m1 != 0) {
-        f = (uint32_t)__builtin_ctzll(m1);
-        m1 &= m1 - 1;
-        k = 0;
-        pend = (m2 >> f) & 1;
-        fp = f;
-      } else {
-        f = kFramesPerWave; // empty chunk: fetches nothing, lands in the sink cell
-        k = 0;
-      }
-      fr[j] = f;
-      kb[j] = k;
-      const int end = f < kFramesPerWave ? (__builtin_amdgcn_readlane(end_rel, f) & ~1) : 0;
-      const uint32_t ext = (uint32_t)(end + 3) & ~3u; // dword-exact extent (0: nothing)
-      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(f < kFramesPerWave ? frame_win(f) : group_ipa, ext);
-      w[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 * k + lane * 16, 0, LAUX);
-    }
-    __builtin_amdgcn_sched_barrier(0); // the whole batch in flight before the first wait
-    uint32_t acc[kC];
-#pragma unroll
-    for (int j = 0; j < kC; ++j) {
-      uint32_t sum = 0;
-      sum = dot2(w[j].x, 0x10001u, sum);
-      sum = dot2(w[j].y, 0x10001u, sum);
-      sum = dot2(w[j].z, 0x10001u, sum);
-      sum = dot2(w[j].w, 0x10001u, sum);
-      const uint32_t f = fr[j];
-      if (f < kFramesPerWave) { // wave-uniform
-        const int er = __builtin_amdgcn_readlane(end_rel, f);
-        const int end = er & ~1;
-        const int c0 = kWinBytes + 1024 * (int)kb[j]; // window offset of this chunk
-        // end % 4 == 2: the last dword loaded holds the 2 bytes after the extent (its high half)
-        const int q = end - 2 - c0;
-        if ((end & 2) && q >= 0 && q < 1024) {
-          const int dw = (q >> 2) & 3;
-          const uint32_t d = dw == 0 ? w[j].x : dw == 1 ? w[j].y : dw == 2 ? w[j].z : w[j].w;
-          if (lane == (q >> 4)) sum -= d >> 16;
-        }
-        // odd tcp_len: the byte after the segment (window offset end - 1), from the lane that loaded it
-        const int p = end - 1 - c0;
-        if ((er & 1) && p >= 0 && p < 1024) {
-          const int dw = (p >> 2) & 3;
-          const uint32_t d = dw == 0 ? w[j].x : dw == 1 ? w[j].y : dw == 2 ? w[j].z : w[j].w;
-          const uint32_t b = __builtin_amdgcn_readlane((d >> (8 * (p & 3))) & 0xff, p >> 4);
-          if ((uint32_t)lane == f) pad = b;
-        }
-      }
-      acc[j] = sum;
-    }
-    // transpose-reduce 16 chunks x 64 lanes: chunk c's total on lanes 4c..4c+3
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { // xor 32
-      const auto r = __builtin_amdgcn_permlane32_swap(acc[i], acc[i + 8], false, false);
-      acc[i] = r[0] + r[1];
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { // xor 16
-      const auto r = __builtin_amdgcn_permlane16_swap(acc[i], acc[i + 4], false, false);
-      acc[i] = r[0] + r[1];
-    }
-    const bool b3 = lane & 8, b2 = lane & 4;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) { // xor 8: keep one, send the other
-      const uint32_t keep = b3 ? acc[i + 2] : acc[i];
-      const uint32_t send = b3 ? acc[i] : acc[i + 2];
-      acc[i] = keep + dpp<0x128>(send); // row_ror:8
-    }
-    {
-      const uint32_t keep = b2 ? acc[1] : acc[0];
-      const uint32_t send = b2 ? acc[0] : acc[1];
-      uint32_t v = keep + dpp<0x141>(send); // row_half_mirror: lane i <-> 7 - i of its 8
-      v += dpp<0xB1>(v);                    // lane ^ 1
-      v += dpp<0x4E>(v);                    // lane ^ 2
-      // lane 4c holds chunk c = b2 + 2*b3 + 4*b4 + 8*b5 = lane >> 2; hand it its frame index
-      uint32_t fv = kFramesPerWave;
-#pragma unroll
-      for (int j = 0; j < kC; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(fv) : "s"(fr[j]), "i"(4 * j));
-      if ((lane & 3) == 0) atomicAdd(&cell[fv], v);
-    }
-  }
-  // jumbo slots only (extent past window + 2 KiB): the remaining KiBs, frame by frame
-  for (uint64_t m = mj; m != 0; m &= m - 1) {
-    const uint32_t f = (uint32_t)__builtin_ctzll(m);
-    const int end = __builtin_amdgcn_readlane(end_rel, f) & ~1;
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(f), (uint32_t)(end + 15) & ~15u);
-    uint32_t sum = 0;
-    for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
-      const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
-      const int o = kb + lane * 16;
-      sum = dot2(w.x, tail_sel(end, o), sum);
-      sum = dot2(w.y, tail_sel(end, o + 4), sum);
-      sum = dot2(w.z, tail_sel(end, o + 8), sum);
-      sum = dot2(w.w, tail_sel(end, o + 12), sum);
-    }
-    const uint32_t tot = wave_sum(sum);
-    if ((uint32_t)lane == f) t_all += tot;
-  }
-  __syncthreads();
-  t_all += cell[lane];
-}
+// Stream start of the window at w, relative to w: the first 128-B line boundary past the
+// window's 16-B block start (w - 16).  112 (the window end) for the default layout, where the
+// block is the slot's first line; less where the block straddles two lines, so the stream's
+// 1-KiB loads still cover whole lines and no line is requested by two of them.  The header
+// lane sums the window below it.  A multiple of 16 (word parity kept for any w).
+__device__ __forceinline__ uint32_t stream_start(uint64_t w) { return 112u - (((uint32_t)w - 16u) & 112u); }
 
-// ---- phase 2: the wave streams every frame's region past the window ----
+// ---- phase 2: the wave streams every frame's region from its stream start on ----
 // group_ipa: window start of the group's first slot; frame fi's window is at
 // group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
-// frame with readlane); the total of frame fi lands on lane fi.
+// frame with readlane); the total of frame fi lands on lane fi.  The header lane
+// has summed the window below stream_start (window_part).
 template <int ABL, int LAUX, int IDX>
 __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
                                              int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
-  if constexpr (ABL & kCompact) {
-    (void)n_here; // lanes past n have end_rel = 0: no chunks
-    stream_phase_compact<ABL, LAUX, IDX>(stride, group_ipa, my_win, lane, end_rel, t_all, pad);
-    return;
-  }
   // window start of frame fi: strided from the group's first slot, or (indexed) the
   // address its own lane computed, broadcast with two readlanes
   auto frame_win = [&](uint32_t fi) -> const uint8_t* {
@@ -293,7 +164,7 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
   };
   for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
     uint32_t acc[kBatch];
-    int ends[kBatch];
+    int ends[kBatch], s0s[kBatch];
     u32x4 w0s[kBatch], w1s[kBatch];
     // issue all 2*kBatch loads of the batch before consuming any of them
 #pragma unroll
@@ -303,10 +174,13 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       ends[j] = end;
       const uint32_t end16 = (ABL & kExactRange) ? ((uint32_t)(end + 3) & ~3u)  // dword-exact extent
                                                  : ((uint32_t)(end + 15) & ~15u); // 0 for frames past n (end_rel = 0 there)
-      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi), end16);
+      const uint8_t* fw = frame_win(fi);
+      const int s0 = (int)stream_start((uint64_t)fw);
+      s0s[j] = s0;
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(fw, end16);
       // out-of-range chunks of a buffer load return 0 and fetch nothing
-      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + lane * 16, 0, LAUX);
-      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, kWinBytes + 1024 + lane * 16, 0, LAUX);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX);
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
     auto sel = [](int e, int o) -> uint32_t {
@@ -315,9 +189,9 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
     };
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
-      const int end = ends[j];
+      const int end = ends[j], s0 = s0s[j];
       const u32x4 w0 = w0s[j], w1 = w1s[j];
-      const int o0 = kWinBytes + lane * 16, o1 = o0 + 1024;
+      const int o0 = s0 + lane * 16, o1 = o0 + 1024;
       uint32_t sum = 0;
       sum = dot2(w0.x, sel(end, o0), sum);
       sum = dot2(w0.y, sel(end, o0 + 4), sum);
@@ -329,7 +203,7 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       sum = dot2(w1.w, sel(end, o1 + 12), sum);
       if constexpr (ABL & kExactRange) {
         // end % 4 == 2: the last dword loaded holds the 2 bytes after the extent (its high half)
-        const int q = end - 2 - kWinBytes; // wave-uniform
+        const int q = end - 2 - s0; // wave-uniform
         if ((end & 2) && q >= 0 && q < 2048) {
           const u32x4 w = (q < 1024) ? w0 : w1;
           const int dw = (q >> 2) & 3;
@@ -341,8 +215,8 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       // odd tcp_len: the RFC verdict needs the byte the reference sums past the segment (window
       // offset end - 1); take it from the lane that streamed it instead of re-reading the line later
       const int p = end - 1;
-      if ((__builtin_amdgcn_readlane(end_rel, (b0 + j) & 63) & 1) && p >= kWinBytes && p < kWinBytes + 2048) {
-        const int q = p - kWinBytes;                 // wave-uniform
+      if ((__builtin_amdgcn_readlane(end_rel, (b0 + j) & 63) & 1) && p >= s0 && p < s0 + 2048) {
+        const int q = p - s0;                        // wave-uniform
         const u32x4 w = (q < 1024) ? w0 : w1;
         const int dw = (q >> 2) & 3;
         const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
@@ -353,11 +227,11 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
     // jumbo slots only (slot_stride > 2048): KiBs past the two streamed above, wave-uniform
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
-      const int end = ends[j];
-      if (end > kWinBytes + 2048) {
+      const int end = ends[j], s0 = s0s[j];
+      if (end > s0 + 2048) {
         const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(b0 + j), (uint32_t)(end + 15) & ~15u);
         uint32_t sum = acc[j];
-        for (int kb = kWinBytes + 2048; kb < end; kb += 1024) {
+        for (int kb = s0 + 2048; kb < end; kb += 1024) {
           const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(rs, kb + lane * 16, 0, LAUX);
           const int o = kb + lane * 16;
           sum = dot2(w.x, tail_sel(end, o), sum);

@@ -71,7 +71,8 @@ struct FrameState {
 
 // ---- phase 1: decode one frame from its header window (lane f <-> frame f) ----
 template <int MIS, int ABL>
-__device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t ether_type, bool live, const KArgs& a) {
+__device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t ether_type, bool live, uint32_t s0,
+                                                   const KArgs& a) {
   static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
   FrameState st;
   // IpHeader (Core.h:57-69), fields relative to ip = window + MIS
@@ -108,8 +109,8 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   st.end_rel = (live && !st.trunc) ? (int)((MIS + 20 + seg_even) | (st.tcp_len & 1)) : 0;
   st.pad = kPadUnknown;
 
-  // the part of the region inside the window, summed from registers
-  st.t_all = window_sum_from<MIS>(h, st.end_rel & ~1);
+  // the part of the region in the window below the stream start, summed from registers
+  st.t_all = window_part<MIS>(h, st.end_rel & ~1, s0);
 
   // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
   st.conn_id = PN_MISS;
@@ -288,11 +289,11 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
     win = a.frames + o + 14 - MIS;
     bool coop_done = false;
     if constexpr (COOP) {
-      // Cooperative window for line-aligned frames (ef_vi rings with a short prefix, 2-KiB
-      // batches): the window is the frame's line from offset 16 on, and the whole line lies
-      // inside [base, eth + avail).  When every frame of the wave qualifies, 8 lanes per
-      // frame load its line coalesced into the LDS tile (one request per line), as the
-      // strided kernel does; otherwise the wave falls back to per-lane windows.
+      // Cooperative window: when every frame of the wave has its 128-B window block (the
+      // 16-B chunk before the window, and the window) 16-B aligned inside [base, eth + avail),
+      // 8 lanes per frame load the block coalesced into the LDS tile, as the strided kernel
+      // does (one request per line; the second line of a straddling block only when the
+      // header fields reach it); otherwise the wave falls back to per-lane windows.
       const bool use = live && !bad_off;
       const bool elig = !use || ((((uintptr_t)win & 15u) == 0) && o + 14 >= (uint64_t)(MIS + 16) &&
                                  (uint32_t)(14 - MIS + kWinBytes) <= a.avail);
@@ -306,7 +307,8 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
           const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
           const uint64_t la = line_addr[r];
           u32x4 v = {0u, 0u, 0u, 0u};
-          if (la) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
+          if (la && block_part_needed<MIS>((uint32_t)la, part))
+            v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
           tile[r * 8 + (part ^ (r & 7))] = v;
         }
         __syncthreads();
@@ -341,10 +343,10 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
       }
     }
   } else {
-    ether_type = load_window_strided<MIS, COOP, LWIN>(rs, lane, a.stride, a.ipa_off, h);
+    ether_type = load_window_strided<MIS, COOP, LWIN>(rs, lane, a.stride, a.ipa_off, (uint32_t)(uintptr_t)wave_slot, h);
   }
   if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
-  FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, a);
+  FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, stream_start((uint64_t)win), a);
   stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
   if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off);
 }
@@ -629,8 +631,6 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 8: launch_one<0, 1, kAblGlobalStore | kProdAbl>(a, s); break;        // plain global record store
     case 9: launch_one<0, 1, 0>(a, s); break;                      // 16-B stream descriptors + per-dword tail masks
     case 19: launch_one<0, 1, kAblStore8 | kProdAbl>(a, s); break;            // timing only: 8-B stores
-    case 20: launch_one<0, 1, kProdAbl | kCompact>(a, s); break;              // compacted chunk list
-    case 21: launch_one<0, 0, kProdAbl | kCompact>(a, s); break;              // per-lane window + compacted
     case 22: launch_one<0, 1, kExactRange>(a, s); break;                         // scalar probe walk (before kCoopProbe)
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   // LAUX0: the line-0 window loads keep the default policy (not nt), so the line the
   // patch kernel later writes is still in the memory-side cache
   Window h;
-  (void)load_window_strided<MIS, COOP, LAUX0>(rs, lane, a.stride, a.ipa_off, h);
+  (void)load_window_strided<MIS, COOP, LAUX0>(rs, lane, a.stride, a.ipa_off, (uint32_t)(uintptr_t)wave_slot, h);
   uint8_t* ip = wave_slot + (uint64_t)lane * a.stride + a.ipa_off + MIS;
 
   // IpHeader (Core.h:57-69): tot_len at ip+2, checksum at ip+10
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
     // adds a trailing odd byte as the low byte of a word, TcpConn.h:291-295)
     const uint32_t even_end = MIS + ((tot + 1) & ~1u);
     const int end_rel = ok ? (int)(even_end | (tot & 1)) : 0;
-    uint32_t t_all = window_sum_from<MIS>(h, end_rel & ~1);
+    uint32_t t_all = window_part<MIS>(h, end_rel & ~1, stream_start((uint64_t)(ip - MIS)));
     uint32_t pad = kPadUnknown;
     stream_phase<kExactRange, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
     if (ok && (tot & 1) && pad == kPadUnknown) pad = ip[tot]; // pad byte inside the window
@@ -307,7 +307,8 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
   a.frame_off = frame_off;
-  if (!coop_layout(a) || a.stride < a.ipa_off + kWinBytes)  // block write-back variants stay inside the slot
+  // block write-back variants: the block is the slot's first line (every part loaded) inside the slot
+  if (!coop_layout(a) || a.stride < a.ipa_off + kWinBytes || (a.stride % 128) || (((uintptr_t)a.frames + a.ipa_off) & 127u) != 16)
     return set_err(ctx, PN_EINVAL, "tx variant: needs the cooperative layout");
   hipStream_t s = (hipStream_t)stream;
   int rc = ensure_patch(ctx, variant >= 15 ? 2 * n : n, s); // 16-B record variants need 2 patch slots per frame

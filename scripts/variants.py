@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 NAMES = {0: "perlane_window", 1: "coop_window", 2: "perlane_defaultpolicy", 3: "coop_defaultpolicy",
          4: "coop_win_default", 5: "coop_store_default", 6: "coop_win_store_default", 7: "coop_store_nt",
          8: "coop_global_store", 9: "coop_tail_masks", 19: "ABL_store8",
-         20: "coop_compact", 21: "perlane_compact", 22: "scalar_probe_walk",
+         22: "scalar_probe_walk",
          11: "ABL_noprobe", 12: "ABL_noreduce", 14: "ABL_nomask", 18: "ABL_nostore"}
 TIMING_ONLY = {11, 12, 14, 18, 19}
 
