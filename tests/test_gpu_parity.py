@@ -103,10 +103,13 @@ def test_full_size_digest(torch_cuda, ctx, golden_dir, cfg):
         assert counts[1] == n - n // 1024
 
 
-@pytest.mark.parametrize("frame_off", [0, 2, 4, 6, 8, 10, 12, 14, 16, 24, 34, 38])
+@pytest.mark.parametrize("frame_off", [0, 2, 4, 6, 8, 10, 12, 14, 16, 24, 34, 38, 18, 50, 66, 82, 98, 114, 120, 126])
 def test_every_alignment_specialisation(torch_cuda, ctx, frame_off):
     """(frame_off + 14) % 16 selects one of 8 kernel specialisations; ef_vi's layout is
-    frame_off = 10 + receive_prefix_len (Core.h:505)."""
+    frame_off = 10 + receive_prefix_len (Core.h:505).  frame_off >= 18 moves the window
+    block off the line grid: the stream starts at the next line, and the block's
+    second-line parts are skipped (header fields in the first line: 18, 34, 38, 50) or
+    loaded (66 .. 98); at 114 .. 126 the block starts at line + 112 (stream start 0)."""
     p = pa.rx.GenParams.for_config(5)
     t = pa.gen_conn_table(p)
     e, m = t.snapshot()

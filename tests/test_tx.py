@@ -219,13 +219,17 @@ def test_gpu_fill_equals_reference_frames(mode, frame_off, lens_too):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_gpu_fill_random_bytes_all_layouts(mode):
     """Arbitrary bytes (any tot_len, incl. out-of-range ones left untouched), every
-    (frame_off + 14) % 16 class, line-aligned and not, jumbo slots, ragged n."""
+    (frame_off + 14) % 16 class, every line offset of the window block, jumbo slots, ragged n."""
     torch, pa = _gpu()
     ctx = pa.RxContext(0)
     rng = np.random.default_rng(mode + 100)
     for stride, frame_off, n in [(2048, 2, 4099), (2048, 14, 1000), (2048, 0, 777), (2048, 4, 65), (2048, 6, 64),
                                  (2048, 8, 63), (2048, 10, 1), (2048, 12, 300), (2064, 2, 513), (4096, 34, 200),
-                                 (16384, 2, 130), (112, 2, 200), (1024, 2, 333)]:
+                                 (16384, 2, 130), (112, 2, 200), (1024, 2, 333),
+                                 # window block off the line grid: stream from the next line, header in
+                                 # the first line (18, 50) or across both (66, 98), block at line + 112 (114, 126)
+                                 (2048, 18, 300), (2048, 50, 64), (2048, 66, 200), (2048, 98, 70), (2048, 114, 150),
+                                 (2048, 126, 129)]:
         avail = stride - frame_off
         slots = rng.integers(0, 256, (n, stride), dtype=np.uint8)
         tot = rng.integers(0, avail + 64, n)
