@@ -225,7 +225,8 @@ int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void*
 /* Ceiling for a slot layout: the first `bytes` (<= 2048) of each of n_slots slots,
  * read with the RX kernel's own load pattern and no arithmetic; store_bytes = 16 / 8
  * also writes that many bytes per slot to sink_dev (n_slots x 16 B) like the RX
- * kernel's records, 0 writes nothing. */
+ * kernel's records, 0 writes nothing; 16 | G << 8 (G = 1, 4, 16) writes the 16-B records of
+ * G consecutive 64-slot groups in one burst per workgroup (write-grouping probe). */
 int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
                        int store_bytes, void* sink_dev, void* stream);
 

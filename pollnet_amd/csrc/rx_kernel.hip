@@ -210,7 +210,8 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 
 // ---- phase 3: fold and write the record on the frame's lane ----
 template <int MIS, int ABL, int SAUX>
-__device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f, const uint8_t* win, bool bad_off) {
+__device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f, const uint8_t* win, bool bad_off,
+                                       u32x4* lds_rec) {
   uint32_t flags = st.flags;
   uint32_t tcp_fold = 0xffff;
   if (!st.trunc) {
@@ -241,7 +242,9 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
   rec.w = flags | (tcp_fold << 16);
   if (bad_off) rec = u32x4{PN_MISS, 0, 0, PN_F_BADOFF}; // outside the launch's alignment class: not parsed
-  if constexpr (ABL & kAblNoStore) {
+  if (lds_rec) { // grouped launches write the workgroup's records in one burst at its end
+    *lds_rec = rec;
+  } else if constexpr (ABL & kAblNoStore) {
     if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
   } else if constexpr (ABL & kAblStore8) { // timing only: half the record bytes
     reinterpret_cast<uint2*>(a.out)[f] = uint2{rec.x ^ rec.y, rec.z ^ rec.w};
@@ -255,19 +258,18 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 }
 
 // ---- the kernel: one 64-frame group per 64-thread workgroup ----
-// COOP = 1: 8 lanes per slot load its first 128-B line (exactly one request per
-// line, the line the header window lives in) into an XOR-swizzled LDS tile that
-// the header lanes read back; needs 128-B aligned lines with ip at line + 16..31.
-// COOP = 0: each lane loads its own 112-B window (any layout).
+// COOP = 1: 8 lanes per slot load its 128-B window block (the 16-B chunk before the
+// window + the window; the slot's first line in the default layout) into an
+// XOR-swizzled LDS tile that the header lanes read back (load_window_strided).
+// COOP = 0: each lane loads its own 112-B window (frame_off = 0).
 // IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
 // class); per-frame stream descriptors; with COOP, waves whose frames all have their
-// window at line + 16 load lines cooperatively, other waves per-lane bounds-checked windows.
-template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
+// block 16-B aligned inside the ring load blocks cooperatively, other waves per-lane
+// bounds-checked windows.
 // 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
 // default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
-__global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
-  const int lane = threadIdx.x;
-  const uint32_t wave_base = blockIdx.x * kFramesPerWave;
+template <int MIS, int COOP, int ABL, int LAUX, int SAUX, int IDX, int LWIN>
+__device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wave_base, const int lane, u32x4* lds_recs) {
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
   const bool live = f < a.n;
@@ -348,7 +350,42 @@ __global__ __launch_bounds__(kWave, (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_clas
   if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, stream_start((uint64_t)win), a);
   stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
-  if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off);
+  if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
+}
+
+// GRP = 1: one 64-frame group per workgroup, records stored as each group finishes.
+// GRP > 1 (tuning variants): GRP consecutive groups per workgroup, their records kept in
+// LDS and written in one GRP-KiB burst at the end (scripts/write_grouping.py probe).
+// GOPT (tuning): bit 0 = GRP groups per workgroup but records stored per group (no LDS);
+// bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 5;
+// GOPT >> 4 = KiB of LDS padding (caps workgroups per CU: an occupancy probe).
+template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
+          int GRP = 1, int GOPT = 0>
+__global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
+  const int lane = threadIdx.x;
+  if constexpr ((GOPT >> 4) > 0) {
+    __shared__ uint32_t pad_lds[(GOPT >> 4) * 256];
+    pad_lds[lane] = lane;
+    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never: keeps the padding allocated
+  }
+  if constexpr (GRP == 1 || (GOPT & 1)) {
+#pragma nounroll
+    for (int g = 0; g < GRP; ++g)
+      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, (blockIdx.x * GRP + g) * kFramesPerWave, lane, nullptr);
+  } else {
+    __shared__ u32x4 recs[GRP * kFramesPerWave];
+    const uint32_t first = blockIdx.x * GRP * kFramesPerWave;
+#pragma nounroll
+    for (int g = 0; g < GRP; ++g) // not unrolled: two groups' live ranges overlapping would halve occupancy
+      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, first + g * kFramesPerWave, lane, recs + g * kFramesPerWave);
+    __syncthreads();
+    if (first >= a.n) return;
+    const uint32_t cnt = min((uint32_t)(GRP * kFramesPerWave), a.n - first);
+    const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.out + first), cnt * 16); // stores past n dropped
+#pragma unroll
+    for (int g = 0; g < GRP; ++g)
+      __builtin_amdgcn_raw_buffer_store_b128(recs[g * kFramesPerWave + lane], ro, (g * kFramesPerWave + lane) * 16, 0, SAUX);
+  }
 }
 
 __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src, uint64_t n16, uint32_t* sink) {
@@ -400,6 +437,55 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_kernel(const uint8_t* b
   }
 }
 
+// Write-grouping probe: the slot-read ceiling with each 64-thread workgroup owning G
+// consecutive 64-slot groups and writing their G x 64 16-B records (G KiB, contiguous) in
+// one burst at the end instead of 1 KiB after each group.
+// EACH = true: the same G-group loop, records written after each group (separates the
+// effect of fewer, longer workgroups from that of the write bursts).
+template <int G, bool EACH = false>
+__global__ __launch_bounds__(kWave) void calib_slot_read_grouped_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                                       uint32_t bytes, uint32_t* sink) {
+  __shared__ u32x4 recs[EACH ? 1 : G * kFramesPerWave];
+  const int lane = threadIdx.x;
+  for (int g = 0; g < G; ++g) {
+    const uint32_t wave_base = (blockIdx.x * G + g) * kFramesPerWave;
+    uint32_t acc = 0;
+    if (wave_base < n) {
+      const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+      const uint8_t* wb = base + (uint64_t)wave_base * stride;
+      for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+        u32x4 w0s[kBatch], w1s[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          const uint32_t nb = (b0 + j < n_here) ? bytes : 0u;
+          const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
+          w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, kLoadAux);
+          w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, kLoadAux);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+      }
+    }
+    if constexpr (EACH) {
+      if (wave_base + lane < n) {
+        const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(sink + 4 * (uint64_t)wave_base), 64 * 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{acc, acc ^ 1u, acc ^ 2u, acc ^ 3u}, ro, lane * 16, 0, kStoreAux);
+      }
+    } else {
+      recs[g * kFramesPerWave + lane] = u32x4{acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+    }
+  }
+  if constexpr (EACH) return;
+  __syncthreads();
+  const uint32_t first = blockIdx.x * G * kFramesPerWave;
+  const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(sink + 4 * (uint64_t)first),
+                                               16 * min((uint32_t)(G * kFramesPerWave), n - first));
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    __builtin_amdgcn_raw_buffer_store_b128(recs[g * kFramesPerWave + lane], ro, (g * kFramesPerWave + lane) * 16, 0, kStoreAux);
+}
+
 } // namespace
 
 // ============================ C-ABI ============================
@@ -412,10 +498,11 @@ bool coop_layout(const KArgs& a) {
   return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }
 
-template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX>
+template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
+          int GRP = 1, int GOPT = 0>
 void launch_one(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>),
-                     dim3((a.n + kFramesPerWave - 1) / kFramesPerWave), dim3(kWave), 0, s, a);
+  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN, GRP, GOPT>),
+                     dim3((a.n + GRP * kFramesPerWave - 1) / (GRP * kFramesPerWave)), dim3(kWave), 0, s, a);
 }
 
 template <int MIS>
@@ -632,6 +719,17 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 9: launch_one<0, 1, 0>(a, s); break;                      // 16-B stream descriptors + per-dword tail masks
     case 19: launch_one<0, 1, kAblStore8 | kProdAbl>(a, s); break;            // timing only: 8-B stores
     case 22: launch_one<0, 1, kExactRange>(a, s); break;                         // scalar probe walk (before kCoopProbe)
+    case 23: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2>(a, s); break;  // 2 groups per WG, burst records
+    case 24: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 4>(a, s); break;  // 4
+    case 25: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8>(a, s); break;  // 8
+    case 26: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 16>(a, s); break; // 16
+    case 27: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, 1>(a, s); break;  // 8 groups, records per group
+    case 28: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2 << 4>(a, s); break;  // 1 group, +2 KiB LDS
+    case 29: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 6 << 4>(a, s); break;  // 1 group, +6 KiB LDS
+    case 30: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, (2 << 4) | 1>(a, s); break;  // 27 + 2 KiB
+    case 31: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2>(a, s); break;  // 1 group, 3-wave budget
+    case 32: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 4>(a, s); break;  // 1 group, 2-wave budget
+    case 33: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, 4>(a, s); break;  // 2 groups burst, 2-wave budget
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
@@ -653,6 +751,12 @@ int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint3
   const uint8_t* src = (const uint8_t*)src_dev;
   uint32_t* sink = (uint32_t*)sink_dev;
   switch (store_bytes) {
+    // 16 B records written per G groups (probe): store_bytes = 16 | G << 8
+    case 16 | (4 << 8): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<4>), dim3((waves + 3) / 4), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (16 << 8): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<16>), dim3((waves + 15) / 16), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (1 << 8): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<1>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (4 << 8) | (1 << 16): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<4, true>), dim3((waves + 3) / 4), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (16 << 8) | (1 << 16): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<16, true>), dim3((waves + 15) / 16), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
     case 16: hipLaunchKernelGGL((calib_slot_read_kernel<16>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
     case 8: hipLaunchKernelGGL((calib_slot_read_kernel<8>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
     default: hipLaunchKernelGGL((calib_slot_read_kernel<0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink);
