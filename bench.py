@@ -81,6 +81,7 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s):
             if el >= secs:
                 return passes * sample / el, passes * wire * 8 / el / 1e9, passes
 
+    c1 = c1_socket_loopback()
     fr_mt, gb_mt, p_mt = rate(threads, False, budget_s * 0.5)
     fr_1, gb_1, p_1 = rate(1, False, budget_s * 0.3)
     fr_rel, gb_rel, _ = rate(1, True, budget_s * 0.2)
@@ -98,7 +99,27 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s):
         "release_path_no_checksum_1t": {"value": round(gb_rel, 2), "unit": "Gbit/s",
                                         "mframes_per_s": round(fr_rel / 1e6, 3), "cores": 1},
         "host_cpu": _cpu_model(),
+        "c1_socket_loopback_ref": c1,
     }
+
+
+def c1_socket_loopback(seconds=1.5):
+    """BASELINE config C1 beside it: the reference's own Socket.h server + client
+    (oracle/_ref/ref_socket_c1, built from /root/reference by oracle/ref.mk) echoing
+    1500-B messages over 127.0.0.1, window 1 (ping-pong RTT) and 8."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_socket_c1")
+    if not os.path.exists(exe):
+        return {"error": "oracle/_ref/ref_socket_c1 not built"}
+    out = {}
+    for w, port in ((1, 23411), (8, 23412)):
+        try:
+            r = subprocess.run([exe, str(seconds), str(w), str(port)], capture_output=True, text=True, timeout=30)
+            out[f"window_{w}"] = json.loads(r.stdout.strip().splitlines()[-1])
+        except Exception as ex:  # measured extra; never blocks the bench line
+            out[f"window_{w}"] = {"error": str(ex)}
+    return out
 
 
 def _cpu_model():

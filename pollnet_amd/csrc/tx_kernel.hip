@@ -334,6 +334,11 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
       case 14: hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a); return 0;    // phase 2 only
       case 15: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -3>), grid, block, 0, s, a); return 0;  // phase 1, 16-B records
       case 16: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -4>), grid, block, 0, s, a); return 0;  // phase 1, RX-style store
+      // in place with the line-0 window at the default policy: the line is still in L2 when its
+      // fields are written, so the 2-byte stores (or the patched line) merge there
+      case 17: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, 0>), grid, block, 0, s, a); return 0;
+      case 18: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 0, 0>), grid, block, 0, s, a); return 0;
+      case 19: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, 0>), grid, block, 0, s, a); return 0;
       default: return -1;
     }
   };

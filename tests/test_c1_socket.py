@@ -1,0 +1,18 @@
+"""BASELINE config C1 (CPU plumbing): the reference's own Socket.h TCP server and client,
+compiled unmodified into oracle/_ref/ref_socket_c1 (oracle/ref.mk), echo 1500-B messages
+over loopback; the driver reports round trips and payload rate."""
+import json
+import os
+import subprocess
+
+import pytest
+
+EXE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "ref_socket_c1")
+
+
+@pytest.mark.skipif(not os.path.exists(EXE), reason="oracle/_ref/ref_socket_c1 not built (needs /root/reference)")
+def test_c1_socket_echo_runs():
+    r = subprocess.run([EXE, "0.3", "4", "23499"], capture_output=True, text=True, timeout=30)
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "error" not in d, d
+    assert d["messages_echoed"] > 100 and d["payload_gbit_per_s_each_way"] > 0
