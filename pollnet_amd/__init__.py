@@ -17,6 +17,9 @@ from .rx import (  # noqa: F401
     PN_TX_UDP,
     RESULT_DTYPE,
     ENTRY_DTYPE,
+    STREAM_FILTER_DTYPE,
+    PN_NO_STREAM,
+    PN_MAX_STREAM_FILTERS,
     F,
     ConnTable,
     PollnetError,

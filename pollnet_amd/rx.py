@@ -49,7 +49,12 @@ RESULT_DTYPE = np.dtype(
     [("conn_id", "<u4"), ("seq", "<u4"), ("payload_off", "<u2"), ("payload_len", "<i2"), ("flags", "<u2"), ("tcp_fold", "<u2")]
 )
 ENTRY_DTYPE = np.dtype([("key", "<u8"), ("conn_id", "<u4"), ("_pad", "<u4")])
-assert RESULT_DTYPE.itemsize == 16 and ENTRY_DTYPE.itemsize == 16
+# pn_stream_filter: TcpStream::initFilter's fields, network order, 0 = wildcard (TcpStream.h:32-37)
+STREAM_FILTER_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("src_port", "<u2"), ("dst_port", "<u2"),
+                                ("_pad", "<u4")])
+PN_NO_STREAM = 0xFFFFFFFF
+PN_MAX_STREAM_FILTERS = 64
+assert RESULT_DTYPE.itemsize == 16 and ENTRY_DTYPE.itemsize == 16 and STREAM_FILTER_DTYPE.itemsize == 16
 
 
 class PollnetError(RuntimeError):
@@ -109,6 +114,7 @@ _pn_classify_indexed = _sig("pn_classify_indexed", _i32, _vp, _vp, _vp, _u32, _u
 _pn_tx_fill = _sig("pn_tx_fill", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp)
 _pn_tx_variant = _sig("pn_tx_fill_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _i32, _vp)
 _pn_sync = _sig("pn_sync", _i32, _vp)
+_pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
 _pn_idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
@@ -272,6 +278,14 @@ class RxContext:
         """Tuning-only TX fill shapes (scripts/tx_variants.py); not part of the C header."""
         _check(_pn_tx_variant(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), variant,
                               _stream_handle(stream)), self._h, "pn_tx_fill_variant")
+
+    def match_streams(self, frames, slot_stride: int, frame_off: int, n: int, filters: np.ndarray, stream_ids,
+                      stream=None):
+        """pn_match_streams: stream_ids[i] (u32, device or pinned memory) = the first filter
+        (STREAM_FILTER_DTYPE, host array) frame i passes, PN_NO_STREAM if none."""
+        flt = np.ascontiguousarray(filters, dtype=STREAM_FILTER_DTYPE)
+        _check(_pn_match_streams(self._h, _ptr(frames), slot_stride, frame_off, n, flt.ctypes.data, len(flt),
+                                 _ptr(stream_ids), _stream_handle(stream)), self._h, "pn_match_streams")
 
     def classify_indexed_variant(self, base, offsets, eth_mod16, n, avail, results, stream, variant):
         """Tuning-only indexed kernel shapes (scripts/bench_indexed.py); not part of the C header."""
