@@ -309,8 +309,10 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
           const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
           const uint64_t la = line_addr[r];
           u32x4 v = {0u, 0u, 0u, 0u};
-          if (la && block_part_needed<MIS>((uint32_t)la, part))
-            v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
+          if (la && block_part_needed<MIS>((uint32_t)la, part)) {
+            if constexpr (LWIN == 0) v = reinterpret_cast<const u32x4*>(la)[part]; // default policy (tuning)
+            else v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
+          }
           tile[r * 8 + (part ^ (r & 7))] = v;
         }
         __syncthreads();
@@ -498,6 +500,13 @@ bool coop_layout(const KArgs& a) {
   return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }
 
+// Indexed launches load the cooperative window blocks at the default cache policy: in a
+// packed capture a frame's last line is the next frame's window line, and a block loaded
+// with default policy is still in L2 when the previous frame's stream asks for it
+// (packed C2/C3/C5 -8..-10 %, permuted ef_vi event runs -2 %, in-order slot runs +1 %;
+// profiles/r01_experiments/indexed_window_policy_c{2,3,5}.json).
+constexpr int kIdxWin = 0;
+
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
           int GRP = 1, int GOPT = 0>
 void launch_one(const KArgs& a, hipStream_t s) {
@@ -644,14 +653,14 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
-    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s); break;
+    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
@@ -663,7 +672,7 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
 // A/B-timed by scripts/bench_indexed.py; not part of the public header.
 int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
                                 uint32_t avail, void* results_dev, void* stream, int variant) {
-  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 1)
+  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 3)
     return set_err(ctx, PN_EINVAL, "indexed variant: bad args");
   KArgs a;
   a.frames = (const uint8_t*)base;
@@ -678,7 +687,9 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   a.avail = avail;
   a.offs = offsets;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1>(a, s);
+  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux>(a, s); // window non-temporal
+  else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0>(a, s);  // window at default policy (production)
+  else if (variant == 3) launch_one<0, 1, kProdAbl, 0, kStoreAux, 1, 0>(a, s);         // + stream at default policy
   else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");

@@ -57,12 +57,14 @@ def main():
     poffs = torch.from_numpy(starts.astype(np.uint64).view(np.int64)).cuda()
     runs = {
         "indexed_packed": lambda: ctx.classify_indexed(packed_dev, poffs, off, n, stride - off, out, st),
+        "indexed_packed_all_default": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 3),
         "strided": lambda: ctx.classify(frames, stride, off, n, out, st),
         "indexed_in_order": lambda: ctx.classify_indexed(frames, ident, off, n, stride - off, out, st),
         "indexed_permuted": lambda: ctx.classify_indexed(frames, perm, off, n, stride - off, out, st),
         "indexed_in_order_perlane": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 0),
-        "indexed_in_order_coop": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 1),
-        "indexed_permuted_coop": lambda: ctx.classify_indexed_variant(frames, perm, off, n, stride - off, out, st, 1),
+        "indexed_in_order_coop_win_nt": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 1),
+        "indexed_permuted_coop_win_nt": lambda: ctx.classify_indexed_variant(frames, perm, off, n, stride - off, out, st, 1),
+        "indexed_packed_win_nt": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 1),
     }
     for name, f in runs.items():  # parity first
         f()
