@@ -360,15 +360,19 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
 // LDS and written in one GRP-KiB burst at the end (scripts/write_grouping.py probe).
 // GOPT (tuning): bit 0 = GRP groups per workgroup but records stored per group (no LDS);
 // bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 5;
-// GOPT >> 4 = KiB of LDS padding (caps workgroups per CU: an occupancy probe).
+// GOPT >> 4 = KiB of LDS padding, which caps workgroups per CU.  Production pads 2 KiB:
+// with the 8-KiB window tile that is 10 KiB per workgroup, 16 per CU = 4 waves/SIMD where
+// registers would allow 5 -- C2 -1.2 %, C3 -2.5 %, C5 -0.3 % (3 waves: C3 +9 %, C5 +13 %;
+// profiles/r01_experiments/occupancy_c{2,3,5}.json).
+constexpr int kProdGopt = 2 << 4;
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
-          int GRP = 1, int GOPT = 0>
+          int GRP = 1, int GOPT = kProdGopt>
 __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
   const int lane = threadIdx.x;
   if constexpr ((GOPT >> 4) > 0) {
     __shared__ uint32_t pad_lds[(GOPT >> 4) * 256];
     pad_lds[lane] = lane;
-    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never: keeps the padding allocated
+    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
   }
   if constexpr (GRP == 1 || (GOPT & 1)) {
 #pragma nounroll
@@ -508,7 +512,7 @@ bool coop_layout(const KArgs& a) {
 constexpr int kIdxWin = 0;
 
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
-          int GRP = 1, int GOPT = 0>
+          int GRP = 1, int GOPT = kProdGopt>
 void launch_one(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN, GRP, GOPT>),
                      dim3((a.n + GRP * kFramesPerWave - 1) / (GRP * kFramesPerWave)), dim3(kWave), 0, s, a);
@@ -653,14 +657,14 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
-    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin>(a, s); break;
+    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
@@ -687,10 +691,10 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   a.avail = avail;
   a.offs = offsets;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux>(a, s); // window non-temporal
-  else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0>(a, s);  // window at default policy (production)
-  else if (variant == 3) launch_one<0, 1, kProdAbl, 0, kStoreAux, 1, 0>(a, s);         // + stream at default policy
-  else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1>(a, s);
+  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s); // window non-temporal
+  else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0, 1, 0>(a, s);  // window at default policy (production)
+  else if (variant == 3) launch_one<0, 1, kProdAbl, 0, kStoreAux, 1, 0, 1, 0>(a, s);         // + stream at default policy
+  else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
   ctx->last_stream = s;
@@ -730,10 +734,10 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 9: launch_one<0, 1, 0>(a, s); break;                      // 16-B stream descriptors + per-dword tail masks
     case 19: launch_one<0, 1, kAblStore8 | kProdAbl>(a, s); break;            // timing only: 8-B stores
     case 22: launch_one<0, 1, kExactRange>(a, s); break;                         // scalar probe walk (before kCoopProbe)
-    case 23: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2>(a, s); break;  // 2 groups per WG, burst records
-    case 24: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 4>(a, s); break;  // 4
-    case 25: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8>(a, s); break;  // 8
-    case 26: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 16>(a, s); break; // 16
+    case 23: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, 0>(a, s); break;  // 2 groups per WG, burst records
+    case 24: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 4, 0>(a, s); break;  // 4
+    case 25: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, 0>(a, s); break;  // 8
+    case 26: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 16, 0>(a, s); break; // 16
     case 27: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, 1>(a, s); break;  // 8 groups, records per group
     case 28: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2 << 4>(a, s); break;  // 1 group, +2 KiB LDS
     case 29: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 6 << 4>(a, s); break;  // 1 group, +6 KiB LDS
@@ -741,6 +745,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 31: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2>(a, s); break;  // 1 group, 3-wave budget
     case 32: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 4>(a, s); break;  // 1 group, 2-wave budget
     case 33: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, 4>(a, s); break;  // 2 groups burst, 2-wave budget
+    case 34: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 0>(a, s); break;  // no LDS pad: 5 waves/SIMD
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
