@@ -364,7 +364,12 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
 // with the 8-KiB window tile that is 10 KiB per workgroup, 16 per CU = 4 waves/SIMD where
 // registers would allow 5 -- C2 -1.2 %, C3 -2.5 %, C5 -0.3 % (3 waves: C3 +9 %, C5 +13 %;
 // profiles/r01_experiments/occupancy_c{2,3,5}.json).
-constexpr int kProdGopt = 2 << 4;
+// Bit 3: XCD-aware order.  Workgroup b is dispatched to XCD b % 8; mapping it to group
+// (b % 8) * ceil(G / 8) + b / 8 gives every XCD one contiguous eighth of the batch (its own
+// L2 and memory-side traffic stays in one region): C2 -1.2 %, C3 -4.2 %, C5 -3.4 %
+// (profiles/r01_experiments/xcd_order_c{2,3,5}.json; records identical).
+constexpr int kXcdOrder = 8;
+constexpr int kProdGopt = (2 << 4) | kXcdOrder;
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
           int GRP = 1, int GOPT = kProdGopt>
 __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
@@ -374,7 +379,13 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 =
     pad_lds[lane] = lane;
     if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
   }
-  if constexpr (GRP == 1 || (GOPT & 1)) {
+  if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
+    // contiguous eighth of the batch instead of every eighth group
+    const uint32_t nwg = gridDim.x, per = (nwg + 7) / 8, x = blockIdx.x % 8, k = blockIdx.x / 8;
+    const uint32_t full = nwg % 8 == 0 ? 8 : nwg % 8; // XCDs that own `per` groups (the rest own per - 1)
+    const uint32_t g = x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
+    classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, g * kFramesPerWave, lane, nullptr);
+  } else if constexpr (GRP == 1 || (GOPT & 1)) {
 #pragma nounroll
     for (int g = 0; g < GRP; ++g)
       classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, (blockIdx.x * GRP + g) * kFramesPerWave, lane, nullptr);
@@ -657,14 +668,14 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
-    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, 0>(a, s); break;
+    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
@@ -691,8 +702,8 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   a.avail = avail;
   a.offs = offsets;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s); // window non-temporal
-  else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0, 1, 0>(a, s);  // window at default policy (production)
+  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, kXcdOrder>(a, s); // window non-temporal
+  else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0, 1, 0>(a, s);  // production window, blockIdx order
   else if (variant == 3) launch_one<0, 1, kProdAbl, 0, kStoreAux, 1, 0, 1, 0>(a, s);         // + stream at default policy
   else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s);
   hipError_t e = hipGetLastError();
@@ -746,6 +757,8 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 32: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 4>(a, s); break;  // 1 group, 2-wave budget
     case 33: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, 4>(a, s); break;  // 2 groups burst, 2-wave budget
     case 34: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 0>(a, s); break;  // no LDS pad: 5 waves/SIMD
+    case 35: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, kProdGopt | 8>(a, s); break;  // XCD-contiguous (production)
+    case 36: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2 << 4>(a, s); break;  // blockIdx order
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;

@@ -67,10 +67,17 @@ __device__ __forceinline__ void st16(uint8_t* p, uint32_t v) { *reinterpret_cast
 constexpr int kWbPatch = -2;
 
 // MODE: PN_TX_TCP, PN_TX_UDP_EFVI or PN_TX_UDP.
-template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0>
+// PADK (tuning): KiB of LDS padding per workgroup (caps workgroups per CU, as the RX
+// kernel's 2-KiB pad does: 10 KiB = 4 waves/SIMD).
+template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0>
 __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   const int lane = threadIdx.x;
   const uint32_t wave_base = blockIdx.x * kFramesPerWave;
+  if constexpr (PADK > 0) {
+    __shared__ uint32_t pad_lds[PADK * 256];
+    pad_lds[lane] = lane;
+    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
+  }
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
   const bool live = f < a.n;
@@ -328,6 +335,10 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         return 0;
       case 11: // two-phase, production
         hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
+        return 0;
+      case 20: // two-phase, fill kernel at 4 waves/SIMD (2-KiB LDS pad)
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 2>), grid, block, 0, s, a);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
         return 0;
       case 13: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a); return 0; // phase 1 only

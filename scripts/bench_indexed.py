@@ -58,6 +58,8 @@ def main():
     runs = {
         "indexed_packed": lambda: ctx.classify_indexed(packed_dev, poffs, off, n, stride - off, out, st),
         "indexed_packed_all_default": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 3),
+        "indexed_packed_blockidx_order": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 2),
+        "indexed_permuted_blockidx_order": lambda: ctx.classify_indexed_variant(frames, perm, off, n, stride - off, out, st, 2),
         "strided": lambda: ctx.classify(frames, stride, off, n, out, st),
         "indexed_in_order": lambda: ctx.classify_indexed(frames, ident, off, n, stride - off, out, st),
         "indexed_permuted": lambda: ctx.classify_indexed(frames, perm, off, n, stride - off, out, st),
