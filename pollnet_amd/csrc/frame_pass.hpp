@@ -136,6 +136,14 @@ __device__ __forceinline__ uint32_t window_part(const Window& h, int end, uint32
   return t;
 }
 
+// XCD-aware group order: workgroup b (dispatched to XCD b % 8) -> group index such that every
+// XCD owns one contiguous eighth of the nwg groups (a bijection on [0, nwg)).
+__device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t nwg) {
+  const uint32_t per = (nwg + 7) / 8, x = b % 8, k = b / 8;
+  const uint32_t full = nwg % 8 == 0 ? 8 : nwg % 8; // XCDs that own `per` groups (the rest own per - 1)
+  return x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
+}
+
 // Stream start of the window at w, relative to w: the first 128-B line boundary past the
 // window's 16-B block start (w - 16).  112 (the window end) for the default layout, where the
 // block is the slot's first line; less where the block straddles two lines, so the stream's

@@ -381,10 +381,8 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 =
   }
   if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
     // contiguous eighth of the batch instead of every eighth group
-    const uint32_t nwg = gridDim.x, per = (nwg + 7) / 8, x = blockIdx.x % 8, k = blockIdx.x / 8;
-    const uint32_t full = nwg % 8 == 0 ? 8 : nwg % 8; // XCDs that own `per` groups (the rest own per - 1)
-    const uint32_t g = x < full ? x * per + k : full * per + (x - full) * (per - 1) + k;
-    classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, g * kFramesPerWave, lane, nullptr);
+    classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, xcd_group(blockIdx.x, gridDim.x) * kFramesPerWave, lane,
+                                                         nullptr);
   } else if constexpr (GRP == 1 || (GOPT & 1)) {
 #pragma nounroll
     for (int g = 0; g < GRP; ++g)

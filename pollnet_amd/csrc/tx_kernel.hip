@@ -69,10 +69,10 @@ constexpr int kWbPatch = -2;
 // MODE: PN_TX_TCP, PN_TX_UDP_EFVI or PN_TX_UDP.
 // PADK (tuning): KiB of LDS padding per workgroup (caps workgroups per CU, as the RX
 // kernel's 2-KiB pad does: 10 KiB = 4 waves/SIMD).
-template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0>
+template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false>
 __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   const int lane = threadIdx.x;
-  const uint32_t wave_base = blockIdx.x * kFramesPerWave;
+  const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * kFramesPerWave;
   if constexpr (PADK > 0) {
     __shared__ uint32_t pad_lds[PADK * 256];
     pad_lds[lane] = lane;
@@ -210,11 +210,12 @@ bool coop_layout(const TArgs& a) {
 template <int MIS, int MODE>
 void launch(const TArgs& a, hipStream_t s) {
   const dim3 grid((a.n + kFramesPerWave - 1) / kFramesPerWave), block(kWave);
+  // XCD-contiguous group order, as the RX kernel: -1.7 % (profiles/r01_experiments/tx_xcd_order_off{2,14}.json)
   if (coop_layout(a)) {
-    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
     return;
   }
-  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE>), grid, block, 0, s, a);
+  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
 }
 
 template <int MODE>
@@ -333,12 +334,16 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, kLoadAux>), grid, block, 0, s, a);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
         return 0;
-      case 11: // two-phase, production
+      case 11: // two-phase, blockIdx order (production before the XCD order)
         hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
         return 0;
       case 20: // two-phase, fill kernel at 4 waves/SIMD (2-KiB LDS pad)
         hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 2>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
+        return 0;
+      case 21: // two-phase, fill kernel in XCD-contiguous order
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
         return 0;
       case 13: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a); return 0; // phase 1 only

@@ -13,10 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 NAMES = {0: "inplace_u16_stores", 2: "inplace_tile_wb128_sc1", 9: "ABL_nowrite",
-         10: "twophase_line0_nt", 11: "twophase_production", 13: "phase1_only", 14: "phase2_only",
+         10: "twophase_line0_nt", 11: "twophase_blockidx_order", 13: "phase1_only", 14: "phase2_only",
          15: "phase1_rec16_global", 16: "phase1_rec16_buffer_sc1", 17: "inplace_u16_line0_default",
          18: "inplace_tile_wb128_line0_default", 19: "inplace_tile_wb128_sc1_line0_default",
-         20: "twophase_4waves"}
+         20: "twophase_4waves", 21: "twophase_xcd_order"}
 TIMING_ONLY = {9, 13, 14, 15, 16}
 
 
