@@ -169,10 +169,12 @@ def e2e_rate(torch, ctx, slots, n, chunk=1 << 16, passes=3, stride=STRIDE):
             "note": f"pinned hipMemcpyAsync H2D of whole {stride}-B slots + kernel + D2H records, 2 streams"}, host_res
 
 
-def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, reps=10):
+def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, lens=None, reps=10):
     """Same-run bandwidth ceilings (no arithmetic): a front-to-back stream read of the
     whole ring, and the RX kernel's own load pattern over the first 1536 B of each slot
-    with and without its 16-B/frame record writes."""
+    with and without its 16-B/frame record writes.  With `lens` (u32 per slot: slot start
+    to the frame's pad byte), the same pattern over each frame's own lines, in the RX
+    kernel's workgroup order and occupancy: the ceiling for mixed-size rings (C3/C5)."""
     sink = torch.zeros(4096, dtype=torch.int32, device=frames.device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
@@ -193,6 +195,12 @@ def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, reps=10):
         t16 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, res, stream, 16))
         out["slot_pattern_read_gbs"] = round(n * 1536 / t0 / 1e9, 1)
         out["slot_pattern_read_plus_16B_records_ms"] = round(t16 * 1e3, 5)
+    if lens is not None:
+        lens_dev = torch.from_numpy(lens).to(frames.device)
+        tv0 = t(lambda: ctx.calib_slot_read_var(frames, n, STRIDE, lens_dev, sink, stream, 0))
+        tv16 = t(lambda: ctx.calib_slot_read_var(frames, n, STRIDE, lens_dev, res, stream, 16))
+        out["frame_lines_read_ms"] = round(tv0 * 1e3, 5)
+        out["frame_lines_read_plus_16B_records_ms"] = round(tv16 * 1e3, 5)
     return out
 
 
@@ -338,9 +346,12 @@ def main():
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
     if rank == 0 and world == 1:  # the slot-pattern ceilings are for 1514-B frames (1536 B of lines per slot)
-        c = ceilings(torch, ctx, frames, n, res, stream, slot_pattern=cfg in (2, 4))
+        tl = slots[:, FRAME_OFF + 16].astype(np.uint32) << 8 | slots[:, FRAME_OFF + 17]  # ip tot_len (BE)
+        lens = (FRAME_OFF + 14 + tl + (tl & 1)).astype(np.uint32)  # through the pad byte of odd segments
+        c = ceilings(torch, ctx, frames, n, res, stream, slot_pattern=cfg in (2, 4), lens=lens)
         if cfg in (2, 4):
             c["kernel_vs_read_plus_records_ceiling"] = round(c["slot_pattern_read_plus_16B_records_ms"] / kern_ms, 4)
+        c["kernel_vs_frame_lines_ceiling"] = round(c["frame_lines_read_plus_16B_records_ms"] / kern_ms, 4)
         out["roofline"]["same_run_ceilings"] = c
     if rank == 0 and world == 1 and not args.no_e2e:
         try:

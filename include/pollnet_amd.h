@@ -229,6 +229,11 @@ int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void*
  * G consecutive 64-slot groups in one burst per workgroup (write-grouping probe). */
 int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
                        int store_bytes, void* sink_dev, void* stream);
+/* Ceiling for variable-length frames: slot i's first lens_dev[i] bytes (u32 per slot, device
+ * memory; clamped to min(stride, 2048)), same load pattern, workgroup order and occupancy as
+ * the RX kernel, no arithmetic; store_bytes 16 also writes a 16-B record per slot, 0 none. */
+int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
+                           int store_bytes, void* sink_dev, void* stream);
 
 /* ======================= synthetic frame generator =======================
  * Deterministic (seed, frame index) generator for the BASELINE configs; writes

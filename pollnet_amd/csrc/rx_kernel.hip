@@ -452,6 +452,45 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_kernel(const uint8_t* b
   }
 }
 
+// Ceiling for variable-length frames (C3/C5 slot rings): slot i's first lens[i] bytes (the
+// frame's lines, from the slot start to the frame's pad byte), read with the RX kernel's load
+// pattern, workgroup order (each XCD a contiguous eighth) and LDS occupancy cap, no arithmetic;
+// STORE = 16 adds the 16-B records.  Out-of-range dwords of a line cost no extra traffic.
+template <int STORE>
+__global__ __launch_bounds__(kWave) void calib_slot_read_var_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                                   const uint32_t* lens, uint32_t* sink) {
+  __shared__ uint32_t pad_lds[512];
+  const int lane = threadIdx.x;
+  pad_lds[lane] = lane;
+  if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) n = 0; // never true: keeps the padding allocated
+  const uint32_t wave_base = xcd_group(blockIdx.x, gridDim.x) * kFramesPerWave;
+  if (wave_base >= n) return;
+  const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+  const uint8_t* wb = base + (uint64_t)wave_base * stride;
+  uint32_t acc = 0;
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    u32x4 w0s[kBatch], w1s[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const uint32_t nb = (b0 + j < n_here) ? min(lens[wave_base + b0 + j], min(stride, 2048u)) : 0u;
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+  }
+  if constexpr (STORE == 16) {
+    if (lane < (int)n_here) {
+      u32x4 r = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+      *reinterpret_cast<u32x4*>(sink + 4 * (uint64_t)(wave_base + lane)) = r;
+    }
+  } else {
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+  }
+}
+
 // Write-grouping probe: the slot-read ceiling with each 64-thread workgroup owning G
 // consecutive 64-slot groups and writing their G x 64 16-B records (G KiB, contiguous) in
 // one burst at the end instead of 1 KiB after each group.
@@ -790,6 +829,28 @@ int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint3
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "calib slot launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
+                           int store_bytes, void* sink_dev, void* stream) {
+  if (!ctx || !src_dev || !lens_dev || !sink_dev || (stride & 15) || n_slots == 0 ||
+      (store_bytes != 0 && store_bytes != 16))
+    return set_err(ctx, PN_EINVAL, "pn_calib_slot_read_var: bad arguments");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t waves = (n_slots + kFramesPerWave - 1) / kFramesPerWave;
+  const uint8_t* src = (const uint8_t*)src_dev;
+  const uint32_t* lens = (const uint32_t*)lens_dev;
+  uint32_t* sink = (uint32_t*)sink_dev;
+  if (store_bytes == 16)
+    hipLaunchKernelGGL((calib_slot_read_var_kernel<16>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, lens, sink);
+  else
+    hipLaunchKernelGGL((calib_slot_read_var_kernel<0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, lens, sink);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "calib slot var launch");
   ctx->last_stream = s;
   return PN_OK;
 }

@@ -117,6 +117,7 @@ _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
+_pn_calib_slot_var = _sig("pn_calib_slot_read_var", _i32, _vp, _vp, _u32, _u32, _vp, _i32, _vp, _vp)
 _pn_idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
@@ -295,6 +296,10 @@ class RxContext:
     def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, store_bytes=0):
         _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, store_bytes, _ptr(sink_dev),
                               _stream_handle(stream)), self._h, "pn_calib_slot_read")
+
+    def calib_slot_read_var(self, src_dev, n_slots, stride, lens_dev, sink_dev, stream=None, store_bytes=0):
+        _check(_pn_calib_slot_var(self._h, _ptr(src_dev), n_slots, stride, _ptr(lens_dev), store_bytes,
+                                  _ptr(sink_dev), _stream_handle(stream)), self._h, "pn_calib_slot_read_var")
 
     def classify_variant(self, frames_dev, slot_stride, frame_off, n, results_dev, stream, variant):
         """Tuning-only kernel shapes (scripts/variants.py); not part of the C header."""
