@@ -229,9 +229,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
+    # PN_BENCH_DIST_BACKEND=gloo rehearses the N>1 flow with several ranks on one GPU (the timing reduction
+    # then runs on CPU tensors); the measured runs use nccl (= RCCL), one rank per GPU
+    backend = os.environ.get("PN_BENCH_DIST_BACKEND", "nccl")
+    dev = local_rank if backend == "nccl" else local_rank % max(1, torch.cuda.device_count())
+    red_dev = f"cuda:{dev}" if backend == "nccl" else "cpu"
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     cfg = args.config
     n = args.frames or ((1 << 21) if cfg == 4 else (1 << 20))
@@ -243,7 +251,7 @@ def main():
     R = max(1, args.batches)
     table = pa.gen_conn_table(params)
     entries, mask = table.snapshot()
-    ctx = pa.RxContext(local_rank)
+    ctx = pa.RxContext(dev)
     ctx.set_conn_table(table)
     # R distinct batches per rank; batch b of rank r holds global frames [(b*world + r)*n, +n)
     frames_b, wires = [], []
@@ -253,7 +261,7 @@ def main():
         first = (b * world + rank) * n if R > 1 else lo
         pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=first, threads=gen_threads, out=host)
         wires.append(pa.wire_bytes(host, STRIDE, FRAME_OFF, n))
-        frames_b.append(torch.from_numpy(host.reshape(-1)).to(f"cuda:{local_rank}"))
+        frames_b.append(torch.from_numpy(host.reshape(-1)).to(f"cuda:{dev}"))
         if b == 0:
             slots = host.copy()  # batch 0 stays on the host: oracle check, CPU baseline, e2e leg
     del host
@@ -261,7 +269,7 @@ def main():
     frames = frames_b[0]
     log(f"[rank {rank}] generated {R} x {n} frames ({sum(wires) / 1e9:.2f} GB wire) in {time.perf_counter() - t0:.1f}s")
 
-    res = torch.empty(n * 16, dtype=torch.uint8, device=f"cuda:{local_rank}")
+    res = torch.empty(n * 16, dtype=torch.uint8, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
 
     # correctness gate on the measured configuration: first 4096 records vs the oracle
@@ -296,7 +304,7 @@ def main():
     wall = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=f"cuda:{local_rank}")
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         wall, kern_ms_max = float(tt[0]), float(tt[1])
     else:
@@ -306,7 +314,7 @@ def main():
     step_wire = float(sum(wires[k % R] for k in range(args.steps)))  # this rank's wire bytes over the K steps
     total_wire = step_wire
     if world > 1:
-        wt = torch.tensor([step_wire], dtype=torch.float64, device=f"cuda:{local_rank}")
+        wt = torch.tensor([step_wire], dtype=torch.float64, device=red_dev)
         dist.all_reduce(wt, op=dist.ReduceOp.SUM)
         total_wire = float(wt[0])
     gbit = total_wire * 8 / wall / 1e9
