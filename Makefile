@@ -17,11 +17,12 @@ CPPTEST = tests/cpp/test_gpu_rx
 RXCONNTEST = tests/cpp/test_rx_conn
 TCPRXTEST = tests/cpp/test_gpu_tcp_rx
 TCPRXBENCH = bench/bench_tcp_rx
+LATBENCH = bench/bench_latency
 RINGTEST = tests/cpp/test_rx_ring
 STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST)
+all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST)
 
 # TcpStream reassembly restated vs the reference's own TcpStream (4 instantiations)
 $(STREAMTEST): tests/cpp/test_tcp_stream.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_stream.hpp $(HDRS) $(LIB) $(ORACLE)
@@ -38,6 +39,10 @@ $(GPUSTREAMTEST): tests/cpp/test_gpu_tcp_stream.cpp tests/cpp/segframes.hpp incl
 $(RINGTEST): tests/cpp/test_rx_ring.cpp include/pollnet_amd/rx_ring.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# batch size vs throughput and latency of pn_classify (resident, host ring in/records out, hipGraph)
+$(LATBENCH): bench/bench_latency.cpp $(HDRS) $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # poll() throughput (GPU-classified) vs the same host loop over the CPU release path
 $(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
@@ -70,6 +75,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST)
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST)
 
 .PHONY: all ref clean

@@ -58,6 +58,7 @@ struct KArgs {
   uint32_t ipa_off; // (frame_off + 14) & ~15: 16-B aligned start of the header window
   uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
   const uint64_t* offs; // indexed layout: frame i's Ethernet header at frames + offs[i] (nullptr: strided)
+  uint32_t fpw = kFramesPerWave; // frames per wave (8..64): small batches spread over more waves (latency)
 };
 
 // Per-frame state the header lane keeps from phase 1 to phase 3.
@@ -272,8 +273,8 @@ template <int MIS, int COOP, int ABL, int LAUX, int SAUX, int IDX, int LWIN>
 __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wave_base, const int lane, u32x4* lds_recs) {
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
-  const bool live = f < a.n;
-  const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
+  const uint32_t n_here = min(a.fpw, a.n - wave_base);
+  const bool live = (uint32_t)lane < n_here;
   const uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
   // one wave-uniform descriptor over the wave's slots; lanes past n read zeros
   const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
@@ -381,12 +382,11 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 =
   }
   if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
     // contiguous eighth of the batch instead of every eighth group
-    classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, xcd_group(blockIdx.x, gridDim.x) * kFramesPerWave, lane,
-                                                         nullptr);
+    classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, xcd_group(blockIdx.x, gridDim.x) * a.fpw, lane, nullptr);
   } else if constexpr (GRP == 1 || (GOPT & 1)) {
 #pragma nounroll
     for (int g = 0; g < GRP; ++g)
-      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, (blockIdx.x * GRP + g) * kFramesPerWave, lane, nullptr);
+      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, (blockIdx.x * GRP + g) * a.fpw, lane, nullptr);
   } else {
     __shared__ u32x4 recs[GRP * kFramesPerWave];
     const uint32_t first = blockIdx.x * GRP * kFramesPerWave;
@@ -563,7 +563,16 @@ template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX =
           int GRP = 1, int GOPT = kProdGopt>
 void launch_one(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN, GRP, GOPT>),
-                     dim3((a.n + GRP * kFramesPerWave - 1) / (GRP * kFramesPerWave)), dim3(kWave), 0, s, a);
+                     dim3((a.n + GRP * a.fpw - 1) / (GRP * a.fpw)), dim3(kWave), 0, s, a);
+}
+
+// Frames per wave for a batch of n: 64 once the batch fills the chip (>= 1024 waves = 4 per CU),
+// else halved down to 8 so a small batch (a poll's worth of RX events) runs on more waves with
+// fewer dependent stream rounds each -- latency, not bandwidth, bounds those launches.
+uint32_t frames_per_wave(uint32_t n) {
+  uint32_t fpw = kFramesPerWave;
+  while (fpw > 8 && (n + fpw - 1) / fpw < 1024) fpw >>= 1;
+  return fpw;
 }
 
 template <int MIS>
@@ -660,6 +669,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
   a.offs = nullptr;
+  a.fpw = frames_per_wave(n);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");

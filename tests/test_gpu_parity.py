@@ -132,7 +132,10 @@ def test_slot_strides(torch_cuda, ctx, stride, frame_off):
     assert_same(got, exp)
 
 
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 4099])
+# pn_classify picks 8/16/32/64 frames per wave from n (frames_per_wave, rx_kernel.hip): the sizes
+# cover every choice and both sides of each threshold (16368/32736/65472 = 1023 waves' worth)
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 63, 64, 65, 255, 256, 257, 1000, 4099, 16368, 16369, 32736, 32737,
+                               65472, 65473])
 def test_ragged_batch_sizes(torch_cuda, ctx, n):
     p = pa.rx.GenParams.for_config(3)
     t = pa.gen_conn_table(p)
@@ -140,6 +143,20 @@ def test_ragged_batch_sizes(torch_cuda, ctx, n):
     s = pa.gen_frames(p, n)
     exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt)
     got = gpu_classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, canary=65)
+    assert_same(got, exp)
+
+
+@pytest.mark.parametrize("n,frame_off,stride", [(9, 18, 2048), (100, 18, 2048), (20000, 18, 2048), (333, 2, 1536),
+                                                (20001, 0, 4096)])
+def test_small_batch_wave_split_layouts(torch_cuda, ctx, n, frame_off, stride):
+    """Small batches (fewer than 64 frames per wave) on other layouts: C5 frames (options, odd
+    lengths, probe cluster) at the ef_vi-style frame_off 18, a tight 1536-B ring, per-lane windows."""
+    p = pa.rx.GenParams.for_config(5)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    s = pa.gen_frames(p, n, stride, frame_off)
+    exp = orc.classify_batch(s, stride, frame_off, n, e, m, t.max_conn_cnt)
+    got = gpu_classify(torch_cuda, ctx, s, stride, frame_off, n, e, m, t.max_conn_cnt, canary=64)
     assert_same(got, exp)
 
 
