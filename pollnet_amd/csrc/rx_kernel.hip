@@ -711,6 +711,7 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   a.ipa_off = 0;
   a.avail = avail;
   a.offs = offsets;
+  a.fpw = frames_per_wave(n);
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");

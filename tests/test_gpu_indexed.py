@@ -220,3 +220,19 @@ def test_indexed_argument_errors(torch_cuda, ctx):
         with pytest.raises(pa.PollnetError):
             ctx.classify_indexed(buf, offs, mod, 4, avail, res)
     ctx.classify_indexed(buf, offs, 2, 0, 2000, res)  # n = 0 is a no-op
+
+
+@pytest.mark.parametrize("n", [5, 100, 20000, 70000])
+def test_permuted_ring_every_wave_split(torch_cuda, ctx, n):
+    """A permuted event run over a 2-KiB slot ring at sizes that give 8, 16 and 64 frames per
+    wave (frames_per_wave in rx_kernel.hip): records in event order == the oracle's."""
+    p = pa.rx.GenParams.for_config(5)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    ctx.set_conn_table(t)
+    slots = pa.gen_frames(p, n, 2048, 2)
+    perm = np.random.default_rng(n).permutation(n)
+    base = torch_cuda.from_numpy(slots.reshape(-1)).cuda()
+    got = _indexed(torch_cuda, ctx, base, perm.astype(np.uint64) * 2048 + 2, 2, 2046)
+    exp = orc.classify_batch(np.ascontiguousarray(slots[perm]), 2048, 2, n, e, m, t.max_conn_cnt)
+    assert np.array_equal(got, exp), _first_diff(got, exp)
