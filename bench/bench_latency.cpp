@@ -4,6 +4,7 @@
 // size n, on one MI355X, with the C2 generator's 1514-B frames in 2-KiB slots:
 //   kernel_us    : back-to-back launches over fresh (rotating) resident slots, HIP events / launch
 //   resident_rt  : one pn_classify + hipStreamSynchronize, host wall clock (median, p99)
+//   resident_spin: the same with the completion busy-polled (hipEventQuery loop)
 //   e2e_rt       : pinned host slots -> H2D -> pn_classify -> D2H records -> sync (median, p99)
 //   e2e_graph_rt : the same three operations captured once in a hipGraph, hipGraphLaunch + sync
 // Prints one JSON line.  Test/bench tool: links the product library only.
@@ -81,6 +82,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
+  hipEvent_t ed;
+  HIP_OK(hipEventCreateWithFlags(&ed, hipEventDisableTiming));
 
   printf("{\"tool\": \"bench/bench_latency\", \"workload\": \"C2 1514-B frames, 2048-B slots, frame_off 2\", "
          "\"resident_slots\": %u, \"rows\": [",
@@ -109,6 +112,18 @@ int main(int argc, char** argv) {
       PN_OK_(pn_classify(ctx, dev + (size_t)(k % groups) * n * kStride, kStride, kOff, n, res, s));
       HIP_OK(hipStreamSynchronize(s));
       if (k >= 5) rt.push_back(us_since(t0));
+    }
+    // the same, completion busy-polled with hipEventQuery (pollnet's own style: spin, never block)
+    std::vector<double> spin;
+    for (int k = 0; k < iters + 5; ++k) {
+      auto t0 = Clock::now();
+      PN_OK_(pn_classify(ctx, dev + (size_t)(k % groups) * n * kStride, kStride, kOff, n, res, s));
+      HIP_OK(hipEventRecord(ed, s));
+      hipError_t q;
+      while ((q = hipEventQuery(ed)) == hipErrorNotReady) {
+      }
+      HIP_OK(q);
+      if (k >= 5) spin.push_back(us_since(t0));
     }
     // host ring in, records out
     for (int k = 0; k < iters + 5; ++k) {
@@ -142,13 +157,14 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < n; ++i)
       bad += !(res_host[i].payload_off == 54 && res_host[i].conn_id == 0 && (res_host[i].flags & 0x4));
 
-    Stat a = stat(rt), b = stat(e2e), c = stat(gr);
+    Stat a = stat(rt), b = stat(e2e), c = stat(gr), d = stat(spin);
     const double wire = 1514.0 * 8 * n;
     printf("%s{\"frames\": %u, \"kernel_us\": %.2f, \"kernel_mframes_per_s\": %.1f, \"kernel_gbit_per_s\": %.1f, "
-           "\"resident_rt_us_median\": %.2f, \"resident_rt_us_p99\": %.2f, \"e2e_rt_us_median\": %.2f, "
+           "\"resident_rt_us_median\": %.2f, \"resident_rt_us_p99\": %.2f, \"resident_spin_rt_us_median\": %.2f, "
+           "\"resident_spin_rt_us_p99\": %.2f, \"e2e_rt_us_median\": %.2f, "
            "\"e2e_rt_us_p99\": %.2f, \"e2e_graph_rt_us_median\": %.2f, \"e2e_graph_rt_us_p99\": %.2f, "
            "\"e2e_gbit_per_s\": %.1f, \"records_unexpected\": %u}",
-           first ? "" : ", ", n, kern_us, n / kern_us, wire / kern_us / 1e3, a.med, a.p99, b.med, b.p99, c.med, c.p99,
+           first ? "" : ", ", n, kern_us, n / kern_us, wire / kern_us / 1e3, a.med, a.p99, d.med, d.p99, b.med, b.p99, c.med, c.p99,
            wire / b.med / 1e3, bad);
     first = false;
     fflush(stdout);
