@@ -138,6 +138,16 @@ __device__ __forceinline__ uint32_t window_part(const Window& h, int end, uint32
 
 // XCD-aware group order: workgroup b (dispatched to XCD b % 8) -> group index such that every
 // XCD owns one contiguous eighth of the nwg groups (a bijection on [0, nwg)).
+// Frames per wave for a batch of n (host side, at launch): 64 once the batch fills the chip
+// (>= 1024 waves = 4 per CU), else halved down to 8, so a small batch (a poll's worth of RX
+// events) runs on more waves with fewer dependent stream rounds each -- latency, not
+// bandwidth, bounds those launches.
+inline uint32_t frames_per_wave(uint32_t n) {
+  uint32_t fpw = kFramesPerWave;
+  while (fpw > 8 && (n + fpw - 1) / fpw < 1024) fpw >>= 1;
+  return fpw;
+}
+
 __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t nwg) {
   const uint32_t per = (nwg + 7) / 8, x = b % 8, k = b / 8;
   const uint32_t full = nwg % 8 == 0 ? 8 : nwg % 8; // XCDs that own `per` groups (the rest own per - 1)

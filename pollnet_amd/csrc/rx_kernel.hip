@@ -566,14 +566,6 @@ void launch_one(const KArgs& a, hipStream_t s) {
                      dim3((a.n + GRP * a.fpw - 1) / (GRP * a.fpw)), dim3(kWave), 0, s, a);
 }
 
-// Frames per wave for a batch of n: 64 once the batch fills the chip (>= 1024 waves = 4 per CU),
-// else halved down to 8 so a small batch (a poll's worth of RX events) runs on more waves with
-// fewer dependent stream rounds each -- latency, not bandwidth, bounds those launches.
-uint32_t frames_per_wave(uint32_t n) {
-  uint32_t fpw = kFramesPerWave;
-  while (fpw > 8 && (n + fpw - 1) / fpw < 1024) fpw >>= 1;
-  return fpw;
-}
 
 template <int MIS>
 void launch(const KArgs& a, hipStream_t s) {

@@ -54,6 +54,7 @@ struct TArgs {
   uint32_t avail;    // stride - frame_off
   uint32_t frame_off;
   uint2* patch;      // n patch records (ctx scratch)
+  uint32_t fpw = kFramesPerWave; // frames per wave (8..64, frames_per_wave)
 };
 
 // Patch record: x = ip checksum | (tcp checksum or udp_len) << 16, y = tot_len word | flags << 16
@@ -72,7 +73,7 @@ constexpr int kWbPatch = -2;
 template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false>
 __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   const int lane = threadIdx.x;
-  const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * kFramesPerWave;
+  const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * a.fpw;
   if constexpr (PADK > 0) {
     __shared__ uint32_t pad_lds[PADK * 256];
     pad_lds[lane] = lane;
@@ -80,8 +81,8 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   }
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
-  const bool live = f < a.n;
-  const uint32_t n_here = min((uint32_t)kFramesPerWave, a.n - wave_base);
+  const uint32_t n_here = min(a.fpw, a.n - wave_base);
+  const bool live = (uint32_t)lane < n_here;
   uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
   const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
 
@@ -209,7 +210,7 @@ bool coop_layout(const TArgs& a) {
 
 template <int MIS, int MODE>
 void launch(const TArgs& a, hipStream_t s) {
-  const dim3 grid((a.n + kFramesPerWave - 1) / kFramesPerWave), block(kWave);
+  const dim3 grid((a.n + a.fpw - 1) / a.fpw), block(kWave);
   // XCD-contiguous group order, as the RX kernel: -1.7 % (profiles/r01_experiments/tx_xcd_order_off{2,14}.json)
   if (coop_layout(a)) {
     hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
@@ -290,6 +291,7 @@ extern "C" int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint3
   a.avail = slot_stride - frame_off;
   a.frame_off = frame_off;
   a.patch = (uint2*)ctx->tx_patch;
+  a.fpw = frames_per_wave(n);
   const uint32_t mis = (frame_off + 14) & 15;
   if (mode == PN_TX_TCP) launch_mode<PN_TX_TCP>(a, mis, s);
   else if (mode == PN_TX_UDP_EFVI) launch_mode<PN_TX_UDP_EFVI>(a, mis, s);

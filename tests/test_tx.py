@@ -229,7 +229,9 @@ def test_gpu_fill_random_bytes_all_layouts(mode):
                                  # window block off the line grid: stream from the next line, header in
                                  # the first line (18, 50) or across both (66, 98), block at line + 112 (114, 126)
                                  (2048, 18, 300), (2048, 50, 64), (2048, 66, 200), (2048, 98, 70), (2048, 114, 150),
-                                 (2048, 126, 129)]:
+                                 (2048, 126, 129),
+                                 # 32 frames per wave (frames_per_wave; 64 in the full-size round trip below)
+                                 (2048, 14, 40000)]:
         avail = stride - frame_off
         slots = rng.integers(0, 256, (n, stride), dtype=np.uint8)
         tot = rng.integers(0, avail + 64, n)
