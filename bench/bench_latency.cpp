@@ -7,6 +7,7 @@
 //   resident_spin: the same with the completion busy-polled (hipEventQuery loop)
 //   e2e_rt       : pinned host slots -> H2D -> pn_classify -> D2H records -> sync (median, p99)
 //   e2e_graph_rt : the same three operations captured once in a hipGraph, hipGraphLaunch + sync
+//   zero_copy_rt : the kernel reads the pinned host slots and writes records to pinned host memory
 // Prints one JSON line.  Test/bench tool: links the product library only.
 #include <hip/hip_runtime.h>
 
@@ -135,6 +136,16 @@ int main(int argc, char** argv) {
       HIP_OK(hipStreamSynchronize(s));
       if (k >= 5) e2e.push_back(us_since(t0));
     }
+    // zero copy: the kernel reads the pinned host slots over PCIe and writes the records into pinned
+    // host memory (GpuRx's zero-copy mode): one launch + sync, no copies
+    std::vector<double> zc;
+    for (int k = 0; k < iters + 5; ++k) {
+      const size_t g = (size_t)(k % groups) * n;
+      auto t0 = Clock::now();
+      PN_OK_(pn_classify(ctx, host + g * kStride, kStride, kOff, n, res_host, s));
+      HIP_OK(hipStreamSynchronize(s));
+      if (k >= 5) zc.push_back(us_since(t0));
+    }
     // the same, captured once as a graph (fixed host slots: the ring's next batch would be a node update)
     hipGraph_t graph;
     hipGraphExec_t exec;
@@ -157,15 +168,16 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < n; ++i)
       bad += !(res_host[i].payload_off == 54 && res_host[i].conn_id == 0 && (res_host[i].flags & 0x4));
 
-    Stat a = stat(rt), b = stat(e2e), c = stat(gr), d = stat(spin);
+    Stat a = stat(rt), b = stat(e2e), c = stat(gr), d = stat(spin), z = stat(zc);
     const double wire = 1514.0 * 8 * n;
     printf("%s{\"frames\": %u, \"kernel_us\": %.2f, \"kernel_mframes_per_s\": %.1f, \"kernel_gbit_per_s\": %.1f, "
            "\"resident_rt_us_median\": %.2f, \"resident_rt_us_p99\": %.2f, \"resident_spin_rt_us_median\": %.2f, "
            "\"resident_spin_rt_us_p99\": %.2f, \"e2e_rt_us_median\": %.2f, "
            "\"e2e_rt_us_p99\": %.2f, \"e2e_graph_rt_us_median\": %.2f, \"e2e_graph_rt_us_p99\": %.2f, "
-           "\"e2e_gbit_per_s\": %.1f, \"records_unexpected\": %u}",
+           "\"e2e_gbit_per_s\": %.1f, \"zero_copy_rt_us_median\": %.2f, \"zero_copy_rt_us_p99\": %.2f, "
+           "\"zero_copy_gbit_per_s\": %.1f, \"records_unexpected\": %u}",
            first ? "" : ", ", n, kern_us, n / kern_us, wire / kern_us / 1e3, a.med, a.p99, d.med, d.p99, b.med, b.p99, c.med, c.p99,
-           wire / b.med / 1e3, bad);
+           wire / b.med / 1e3, z.med, z.p99, wire / z.med / 1e3, bad);
     first = false;
     fflush(stdout);
   }
