@@ -8,7 +8,6 @@
 //   e2e_rt       : pinned host slots -> H2D -> pn_classify -> D2H records -> sync (median, p99)
 //   e2e_graph_rt : the same three operations captured once in a hipGraph, hipGraphLaunch + sync
 //   zero_copy_rt : the kernel reads the pinned host slots and writes records to pinned host memory
-//   poller_rt    : resident slots through the persistent poller (pn_poller_submit + pn_poller_wait)
 // Prints one JSON line.  Test/bench tool: links the product library only.
 #include <hip/hip_runtime.h>
 
@@ -87,10 +86,6 @@ int main(int argc, char** argv) {
   hipEvent_t ed;
   HIP_OK(hipEventCreateWithFlags(&ed, hipEventDisableTiming));
 
-  // persistent poller (latency mode): 64 resident one-wave workgroups spinning on a pinned doorbell
-  pn_poller* poller = nullptr;
-  PN_OK_(pn_poller_start(ctx, kStride, kOff, total, 64, 2000, &poller));
-
   printf("{\"tool\": \"bench/bench_latency\", \"workload\": \"C2 1514-B frames, 2048-B slots, frame_off 2\", "
          "\"resident_slots\": %u, \"rows\": [",
          total);
@@ -151,22 +146,6 @@ int main(int argc, char** argv) {
       HIP_OK(hipStreamSynchronize(s));
       if (k >= 5) zc.push_back(us_since(t0));
     }
-    // the same batch through the persistent poller: doorbell + spin on the done flags, no launch
-    std::vector<double> pl;
-    if (n <= 16384) {
-      for (int k = 0; k < iters + 5; ++k) {
-        auto t0 = Clock::now();
-        if (pn_poller_submit(poller, dev + (size_t)(k % groups) * n * kStride, n, res) != 0 ||
-            pn_poller_wait(poller, 1000000) != 0) {
-          fprintf(stderr, "poller: %s\n", pn_last_error(ctx));
-          pn_poller_stop(poller);
-          return 1;
-        }
-        if (k >= 5) pl.push_back(us_since(t0));
-      }
-    } else {
-      pl.push_back(-1.0);
-    }
     // the same, captured once as a graph (fixed host slots: the ring's next batch would be a node update)
     hipGraph_t graph;
     hipGraphExec_t exec;
@@ -189,22 +168,20 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < n; ++i)
       bad += !(res_host[i].payload_off == 54 && res_host[i].conn_id == 0 && (res_host[i].flags & 0x4));
 
-    Stat a = stat(rt), b = stat(e2e), c = stat(gr), d = stat(spin), z = stat(zc), q = stat(pl);
+    Stat a = stat(rt), b = stat(e2e), c = stat(gr), d = stat(spin), z = stat(zc);
     const double wire = 1514.0 * 8 * n;
     printf("%s{\"frames\": %u, \"kernel_us\": %.2f, \"kernel_mframes_per_s\": %.1f, \"kernel_gbit_per_s\": %.1f, "
            "\"resident_rt_us_median\": %.2f, \"resident_rt_us_p99\": %.2f, \"resident_spin_rt_us_median\": %.2f, "
            "\"resident_spin_rt_us_p99\": %.2f, \"e2e_rt_us_median\": %.2f, "
            "\"e2e_rt_us_p99\": %.2f, \"e2e_graph_rt_us_median\": %.2f, \"e2e_graph_rt_us_p99\": %.2f, "
            "\"e2e_gbit_per_s\": %.1f, \"zero_copy_rt_us_median\": %.2f, \"zero_copy_rt_us_p99\": %.2f, "
-           "\"zero_copy_gbit_per_s\": %.1f, \"poller_rt_us_median\": %.2f, \"poller_rt_us_p99\": %.2f, "
-           "\"records_unexpected\": %u}",
+           "\"zero_copy_gbit_per_s\": %.1f, \"records_unexpected\": %u}",
            first ? "" : ", ", n, kern_us, n / kern_us, wire / kern_us / 1e3, a.med, a.p99, d.med, d.p99, b.med, b.p99, c.med, c.p99,
-           wire / b.med / 1e3, z.med, z.p99, wire / z.med / 1e3, q.med, q.p99, bad);
+           wire / b.med / 1e3, z.med, z.p99, wire / z.med / 1e3, bad);
     first = false;
     fflush(stdout);
   }
   printf("]}\n");
-  PN_OK_(pn_poller_stop(poller));
   HIP_OK(hipStreamDestroy(s));
   HIP_OK(hipFree(dev));
   HIP_OK(hipFree(dev_e2e));

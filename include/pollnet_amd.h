@@ -219,29 +219,6 @@ int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_o
 /* Wait for the last stream used by this ctx. */
 int pn_sync(pn_ctx* ctx);
 
-/* ======================= persistent poller (latency mode) =======================
- * pollnet's own model is a thread that busy-polls (Core::pollNet, Core.h:494-552); the
- * poller moves that loop onto the GPU: a grid of `workgroups` one-wave workgroups stays
- * resident and spins on a doorbell in pinned host memory, so a batch costs no kernel
- * launch.  Records are exactly pn_classify's for the same frames (same frame pass).
- *   pn_poller_start : snapshot of this ctx's conn table + ring layout (as pn_classify);
- *                     idle_ms: the grid exits after that long without a batch (it always
- *                     drains) and is relaunched by the next submit.  pn_set_conn_table on
- *                     the ctx is refused while a poller runs; stop pollers before pn_close.
- *   pn_poller_submit: n (1..max_batch) frames resident in device (or pinned host) memory,
- *                     records to results_dev; returns at once.
- *   pn_poller_wait  : spin until the last submitted batch is done (0), or PN_EHIP after
- *                     timeout_us.
- *   pn_poller_alive : 1 while the grid is resident.
- *   pn_poller_stop  : signal, wait for the grid to exit, free. */
-typedef struct pn_poller pn_poller;
-int pn_poller_start(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, uint32_t workgroups,
-                    uint32_t idle_ms, pn_poller** out);
-int pn_poller_submit(pn_poller* p, const void* frames_dev, uint32_t n, void* results_dev);
-int pn_poller_wait(pn_poller* p, uint32_t timeout_us);
-int pn_poller_alive(const pn_poller* p);
-int pn_poller_stop(pn_poller* p);
-
 /* HBM streaming-read calibration kernel (used by bench/profiling only): reads
  * `bytes` (multiple of 16) from src and writes one u32 per workgroup to sink. */
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream);

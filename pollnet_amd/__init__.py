@@ -23,7 +23,6 @@ from .rx import (  # noqa: F401
     F,
     ConnTable,
     PollnetError,
-    Poller,
     RxContext,
     conn_hash_key,
     device_count,

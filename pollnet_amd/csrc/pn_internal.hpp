@@ -20,7 +20,6 @@ struct pn_ctx {
   void* tx_patch = nullptr;       // pn_tx_fill's per-frame patch records (8 B each)
   uint32_t tx_patch_n = 0;
   hipStream_t tx_stream = nullptr; // stream of the last pn_tx_fill (the scratch is reused)
-  int pollers = 0;                 // live pn_poller's on this ctx (they read tbl_dev)
   std::string err;
 };
 

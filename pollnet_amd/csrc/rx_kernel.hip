@@ -30,7 +30,6 @@
 // record writes with the frame reads.
 #include <hip/hip_runtime.h>
 
-#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -573,61 +572,6 @@ void launch(const KArgs& a, hipStream_t s) {
   if (coop_layout(a)) return launch_one<MIS, 1>(a, s);
   launch_one<MIS, 0>(a, s);
 }
-// ---- persistent poller (latency mode): pollnet's busy-poll loop moved onto the GPU ----
-// The host writes a batch descriptor into pinned host memory and bumps `seq` (the doorbell);
-// every workgroup spins on it, classifies its share of the batch with the same frame pass as
-// pn_classify, and stores `seq` into its own done flag.  No launch per batch.  Every wave
-// leaves the loop on `stop` or after idle_ticks without a new batch (wall clock), so the
-// grid always drains; the host relaunches an expired grid on the next batch.
-struct PollCtl {
-  uint32_t seq;  // doorbell: last batch submitted
-  uint32_t stop; // 1: leave now
-  uint32_t n;
-  uint32_t fpw;
-  uint64_t frames;
-  uint64_t out;
-};
-
-template <int MIS, int COOP>
-__global__ __launch_bounds__(kWave) void rx_poll_kernel(KArgs a, PollCtl* ctl, uint32_t* done, uint32_t last,
-                                                        uint64_t idle_ticks) {
-  const int lane = threadIdx.x;
-  uint64_t t_idle = wall_clock64();
-  for (;;) {
-    // relaxed polls (uncached reads of the pinned word, no cache invalidation per poll); one
-    // acquire fence per new batch
-    const uint32_t seq = __hip_atomic_load(&ctl->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (__hip_atomic_load(&ctl->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
-    if (seq == last) {
-      if (wall_clock64() - t_idle > idle_ticks) break;
-      __builtin_amdgcn_s_sleep(16);
-      continue;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    KArgs b = a;
-    b.n = __hip_atomic_load(&ctl->n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    b.fpw = __hip_atomic_load(&ctl->fpw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    b.frames = (const uint8_t*)__hip_atomic_load(&ctl->frames, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    b.out = (pn_result*)__hip_atomic_load(&ctl->out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t groups = (b.n + b.fpw - 1) / b.fpw;
-    for (uint32_t g = blockIdx.x; g < groups; g += gridDim.x)
-      classify_group<MIS, COOP, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux>(b, g * b.fpw, lane, nullptr);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, ""); // this wave's records before its flag
-    if (lane == 0) __hip_atomic_store(&done[blockIdx.x], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    last = seq;
-    t_idle = wall_clock64();
-  }
-}
-
-template <int MIS>
-void launch_poll(const KArgs& a, bool coop, uint32_t wgs, hipStream_t s, PollCtl* ctl, uint32_t* done, uint32_t last,
-                 uint64_t idle_ticks) {
-  if (coop)
-    hipLaunchKernelGGL((rx_poll_kernel<MIS, 1>), dim3(wgs), dim3(kWave), 0, s, a, ctl, done, last, idle_ticks);
-  else
-    hipLaunchKernelGGL((rx_poll_kernel<MIS, 0>), dim3(wgs), dim3(kWave), 0, s, a, ctl, done, last, idle_ticks);
-}
-
 } // namespace
 
 extern "C" {
@@ -676,7 +620,6 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   // a classify launched on this ctx may still be reading the table: let it finish
   // before the snapshot is replaced (the copy below is not ordered against that stream)
-  if (ctx->pollers) return set_err(ctx, PN_EINVAL, "pn_set_conn_table: stop this ctx's pollers first");
   if (ctx->tbl_dev) {
     e = hipStreamSynchronize(ctx->last_stream);
     if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(last classify)");
@@ -921,140 +864,6 @@ int pn_sync(pn_ctx* ctx) {
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->last_stream);
   if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize");
   return PN_OK;
-}
-
-struct pn_poller {
-  pn_ctx* ctx = nullptr;
-  KArgs a;                  // layout + table; n/frames/out/fpw come per batch through ctl
-  uint32_t mis = 0, wgs = 0, seq = 0, max_batch = 0;
-  bool coop = false;
-  uint64_t idle_ticks = 0;
-  hipStream_t stream = nullptr;
-  PollCtl* ctl = nullptr;   // pinned, coherent host memory (the doorbell)
-  uint32_t* done = nullptr; // pinned, coherent host memory: one flag per workgroup
-};
-
-static int poller_launch(pn_poller* p, uint32_t last) {
-  hipStream_t s = p->stream;
-  switch (p->mis) {
-    case 0: launch_poll<0>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    case 2: launch_poll<2>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    case 4: launch_poll<4>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    case 6: launch_poll<6>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    case 8: launch_poll<8>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    case 10: launch_poll<10>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    case 12: launch_poll<12>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-    default: launch_poll<14>(p->a, p->coop, p->wgs, s, p->ctl, p->done, last, p->idle_ticks); break;
-  }
-  hipError_t e = hipGetLastError();
-  return e == hipSuccess ? PN_OK : hip_err(p->ctx, e, "rx_poll launch");
-}
-
-int pn_poller_start(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, uint32_t workgroups,
-                    uint32_t idle_ms, pn_poller** out) {
-  if (!ctx || !out) return set_err(ctx, PN_EINVAL, "pn_poller_start: NULL argument");
-  if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, "pn_poller_start: no conn table (call pn_set_conn_table)");
-  if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || slot_stride < frame_off + 96 || max_batch == 0 ||
-      workgroups == 0 || workgroups > 1024 || idle_ms == 0 || idle_ms > 60000)
-    return set_err(ctx, PN_EINVAL, "pn_poller_start: bad layout, max_batch, workgroups (1..1024) or idle_ms (1..60000)");
-  hipError_t e = hipSetDevice(ctx->device);
-  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  int khz = 0;
-  e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device);
-  if (e != hipSuccess || khz <= 0) return hip_err(ctx, e == hipSuccess ? hipErrorInvalidValue : e, "wall clock rate");
-  pn_poller* p = new pn_poller();
-  p->ctx = ctx;
-  p->a.frames = nullptr;
-  p->a.out = nullptr;
-  p->a.tbl = ctx->tbl_dev;
-  p->a.mask = ctx->mask;
-  p->a.n_entries = ctx->n_entries;
-  p->a.max_conn = ctx->max_conn;
-  p->a.n = 0;
-  p->a.stride = slot_stride;
-  p->a.ipa_off = (frame_off + 14) & ~15u;
-  p->a.avail = slot_stride - frame_off;
-  p->a.offs = nullptr;
-  p->mis = (frame_off + 14) & 15;
-  p->coop = coop_layout(p->a);
-  p->wgs = workgroups;
-  p->max_batch = max_batch;
-  p->idle_ticks = (uint64_t)idle_ms * (uint64_t)khz;
-  if ((e = hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipHostMalloc((void**)&p->ctl, sizeof(PollCtl), hipHostMallocCoherent | hipHostMallocMapped)) != hipSuccess ||
-      (e = hipHostMalloc((void**)&p->done, sizeof(uint32_t) * workgroups, hipHostMallocCoherent | hipHostMallocMapped)) !=
-          hipSuccess) {
-    int rc = hip_err(ctx, e, "pn_poller_start: stream / pinned control block");
-    if (p->ctl) (void)hipHostFree(p->ctl);
-    if (p->stream) (void)hipStreamDestroy(p->stream);
-    delete p;
-    return rc;
-  }
-  memset(p->ctl, 0, sizeof(PollCtl));
-  memset(p->done, 0, sizeof(uint32_t) * workgroups);
-  int rc = poller_launch(p, 0);
-  if (rc) {
-    (void)hipHostFree(p->done);
-    (void)hipHostFree(p->ctl);
-    (void)hipStreamDestroy(p->stream);
-    delete p;
-    return rc;
-  }
-  ctx->pollers++;
-  *out = p;
-  return PN_OK;
-}
-
-int pn_poller_submit(pn_poller* p, const void* frames_dev, uint32_t n, void* results_dev) {
-  if (!p) return set_err(nullptr, PN_EINVAL, "pn_poller_submit: poller is NULL");
-  if (n == 0 || n > p->max_batch || !frames_dev || !results_dev || ((uintptr_t)frames_dev & 15) ||
-      ((uintptr_t)results_dev & 15))
-    return set_err(p->ctx, PN_EINVAL, "pn_poller_submit: n in 1..max_batch, 16-byte aligned buffers");
-  uint32_t fpw = 8; // every workgroup a group per round where the batch allows it
-  while (fpw < (uint32_t)kFramesPerWave && (n + fpw - 1) / fpw > p->wgs) fpw <<= 1;
-  const uint32_t seq = ++p->seq;
-  p->ctl->n = n;
-  p->ctl->fpw = fpw;
-  p->ctl->frames = (uint64_t)(uintptr_t)frames_dev;
-  p->ctl->out = (uint64_t)(uintptr_t)results_dev;
-  __atomic_store_n(&p->ctl->seq, seq, __ATOMIC_RELEASE);
-  if (hipStreamQuery(p->stream) == hipSuccess) return poller_launch(p, seq - 1); // grid expired while idle
-  return PN_OK;
-}
-
-int pn_poller_wait(pn_poller* p, uint32_t timeout_us) {
-  if (!p) return set_err(nullptr, PN_EINVAL, "pn_poller_wait: poller is NULL");
-  const uint32_t seq = p->seq;
-  const auto t0 = std::chrono::steady_clock::now();
-  for (uint64_t spins = 0;; ++spins) {
-    uint32_t b = 0;
-    while (b < p->wgs && __atomic_load_n(&p->done[b], __ATOMIC_ACQUIRE) == seq) ++b;
-    if (b == p->wgs) return PN_OK;
-    if ((spins & 1023) == 1023) {
-      // the grid may have expired between the doorbell and the submit's check: relaunch it
-      if (hipStreamQuery(p->stream) == hipSuccess) {
-        int rc = poller_launch(p, seq - 1);
-        if (rc) return rc;
-      }
-      const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
-      if ((uint64_t)us > timeout_us) return set_err(p->ctx, PN_EHIP, "pn_poller_wait: timed out");
-    }
-  }
-}
-
-int pn_poller_alive(const pn_poller* p) { return p && hipStreamQuery(p->stream) == hipErrorNotReady ? 1 : 0; }
-
-int pn_poller_stop(pn_poller* p) {
-  if (!p) return PN_OK;
-  __atomic_store_n(&p->ctl->stop, 1u, __ATOMIC_RELEASE);
-  hipError_t e = hipStreamSynchronize(p->stream);
-  int rc = e == hipSuccess ? PN_OK : hip_err(p->ctx, e, "pn_poller_stop: hipStreamSynchronize");
-  (void)hipStreamDestroy(p->stream);
-  (void)hipHostFree(p->done);
-  (void)hipHostFree(p->ctl);
-  p->ctx->pollers--;
-  delete p;
-  return rc;
 }
 
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream) {

@@ -117,11 +117,6 @@ _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 _pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
-_pn_poller_start = _sig("pn_poller_start", _i32, _vp, _u32, _u32, _u32, _u32, _u32, _c.POINTER(_vp))
-_pn_poller_submit = _sig("pn_poller_submit", _i32, _vp, _vp, _u32, _vp)
-_pn_poller_wait = _sig("pn_poller_wait", _i32, _vp, _u32)
-_pn_poller_alive = _sig("pn_poller_alive", _i32, _vp)
-_pn_poller_stop = _sig("pn_poller_stop", _i32, _vp)
 _pn_calib_slot_var = _sig("pn_calib_slot_read_var", _i32, _vp, _vp, _u32, _u32, _vp, _i32, _vp, _vp)
 _pn_idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
@@ -316,34 +311,6 @@ class RxContext:
 
     def calib_stream_read(self, src_dev, nbytes: int, sink_dev, stream=None):
         _check(_pn_calib(self._h, _ptr(src_dev), nbytes, _ptr(sink_dev), _stream_handle(stream)), self._h, "pn_calib")
-
-
-class Poller:
-    """Persistent GPU poller (pn_poller_*, include/pollnet_amd.h): pollnet's busy-poll loop
-    on the GPU; submit/wait per batch without a kernel launch."""
-
-    def __init__(self, ctx: "RxContext", slot_stride: int, frame_off: int, max_batch: int, workgroups: int = 64,
-                 idle_ms: int = 200):
-        h = _vp()
-        self._ctx = ctx
-        _check(_pn_poller_start(ctx._h, slot_stride, frame_off, max_batch, workgroups, idle_ms, _c.byref(h)), ctx._h,
-               "pn_poller_start")
-        self._h = h
-
-    def submit(self, frames_dev, n: int, results_dev):
-        _check(_pn_poller_submit(self._h, _ptr(frames_dev), n, _ptr(results_dev)), self._ctx._h, "pn_poller_submit")
-
-    def wait(self, timeout_us: int = 2_000_000):
-        _check(_pn_poller_wait(self._h, timeout_us), self._ctx._h, "pn_poller_wait")
-
-    def alive(self) -> bool:
-        return bool(_pn_poller_alive(self._h))
-
-    def stop(self):
-        if self._h:
-            rc = _pn_poller_stop(self._h)
-            self._h = None
-            _check(rc, self._ctx._h, "pn_poller_stop")
 
 
 @dataclass

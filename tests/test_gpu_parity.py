@@ -375,39 +375,3 @@ def test_calib_slot_read_var(torch_cuda, ctx):
         ctx.calib_slot_read_var(frames, n, 100, lens, sink, None, 16)
     with pytest.raises(pa.PollnetError, match="bad arguments"):
         ctx.calib_slot_read_var(frames, n, stride, lens, sink, None, 8)
-
-
-def test_persistent_poller_batches_and_expiry(torch_cuda, ctx):
-    """pn_poller_*: batches of several sizes through the resident grid give the oracle's records;
-    an idle grid exits by itself (it always drains) and the next submit relaunches it."""
-    import time
-
-    p = pa.rx.GenParams.for_config(5)
-    t = pa.gen_conn_table(p)
-    e, m = t.snapshot()
-    ctx.set_conn_entries(e, m, t.max_conn_cnt)
-    n_all = 5000
-    s = pa.gen_frames(p, n_all)
-    exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n_all, e, m, t.max_conn_cnt)
-    frames = torch_cuda.from_numpy(s.reshape(-1)).cuda()
-    res = torch_cuda.full(((n_all + 64) * 16,), 0xAB, dtype=torch_cuda.uint8, device="cuda")
-    poller = pa.Poller(ctx, STRIDE, FRAME_OFF, n_all, workgroups=64, idle_ms=50)
-    try:
-        with pytest.raises(pa.PollnetError, match="stop this ctx's pollers"):
-            ctx.set_conn_entries(e, m, t.max_conn_cnt)
-        for first, n in [(0, 64), (64, 1), (100, 513), (0, 5000), (4000, 1000)]:
-            res.fill_(0xAB)
-            torch_cuda.cuda.synchronize()
-            poller.submit(frames.data_ptr() + first * STRIDE, n, res)
-            poller.wait()
-            out = res.cpu().numpy()
-            assert (out[n * 16:] == 0xAB).all(), "poller wrote past n records"
-            assert_same(out[: n * 16].view(pa.RESULT_DTYPE), exp[first:first + n])
-        time.sleep(0.3)
-        assert not poller.alive(), "idle grid should have exited"
-        poller.submit(frames, 777, res)
-        poller.wait()
-        assert_same(res.cpu().numpy()[: 777 * 16].view(pa.RESULT_DTYPE), exp[:777])
-    finally:
-        poller.stop()
-    assert_same(gpu_classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, 64, e, m, t.max_conn_cnt), exp[:64])
