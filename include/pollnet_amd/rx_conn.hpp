@@ -21,6 +21,11 @@
 //   uint32_t onData(RxConn&, const uint8_t* data, uint32_t size)  -> bytes NOT consumed
 //   void     onFin(RxConn&, const uint8_t* data, uint32_t size)   (data still unconsumed)
 //   void     onReset(RxConn&)                                      (RST, or recv buffer full)
+//   void     onAckField(RxConn&, bool no_text)   optional: the point of step 5 where
+//            the reference processes the ACK field (TcpConn.h:536-665), after the ACK
+//            bit check and before the segment text; no_text = the segment occupies no
+//            sequence space (its duplicate-ACK test, TcpConn.h:622).  A full TCP
+//            endpoint (tcp_server.hpp) advances its send side here.
 // Delivered pointers are zero-copy into the caller's frame when the segment is the
 // next in-order one, else into recv_buf; valid only during the call (TcpConn.h:715).
 #pragma once
@@ -28,10 +33,20 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <type_traits>
+#include <utility>
 
 #include "../pollnet_amd.h"
 
 namespace pollnet_amd {
+
+namespace detail {
+template <class H, class C, class = void>
+struct has_on_ack_field : std::false_type {};
+template <class H, class C>
+struct has_on_ack_field<H, C, decltype(void(std::declval<H&>().onAckField(std::declval<C&>(), false)))>
+    : std::true_type {};
+} // namespace detail
 
 // What the TX side owes after a segment.
 struct RxAck {
@@ -121,6 +136,7 @@ class RxConn {
     }
     // 5. without ACK the segment goes no further (the ACK field itself is the TX side's)
     if (!(rec.flags & PN_F_ACK)) return out;
+    if constexpr (detail::has_on_ack_field<Handler, RxConn>::value) h.onAckField(*this, loc == loc_end);
 
     // 7. segment text
     const int32_t behind = (int32_t)(loc - nxt);

@@ -118,6 +118,7 @@ class SocketEthBatcher {
 
   const char* getLastError() const { return last_error_; }
   bool isClosed() const { return fd_ < 0; }
+  int fd() const { return fd_; }
   void close(const char* reason) {
     if (fd_ >= 0) {
       saveError(reason);

@@ -1,0 +1,39 @@
+"""GpuTcpServer (include/pollnet_amd/tcp_server.hpp): pollnet's EfviTcpServer surface
+(EfviTcp.h:177-309) over the GPU RX/TX paths, driven by the reference example's own
+handler (example/tcpserver.cc:61-90, compiled unchanged; tests/cpp/test_tcp_server.cpp).
+
+CPU: the sequential twin (oracle classification against the live table) alone — the
+server logic: handshakes, echo through writeNonblock, RSTs to unknown flows and after
+close, every stream echoed intact, every TX frame's checksums valid.
+GPU: the same traffic through pn_classify / pn_tx_fill at several frames-per-poll; the
+handler log and every TX frame must equal the twin's."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "test_tcp_server")
+
+
+def _run(*args):
+    if not os.path.exists(BIN):
+        if not os.path.isdir("/root/reference"):
+            pytest.skip("tests/cpp/test_tcp_server not built (its handler text comes from /root/reference)")
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tcp_server"], check=True, capture_output=True)
+    return subprocess.run([BIN, *args], capture_output=True, text=True, timeout=300)
+
+
+@pytest.mark.parametrize("per_poll", [1, 64, 512, 5000])
+def test_server_twin_example_handler(per_poll):
+    p = _run("twin", str(per_poll))
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "200/200 echoes intact, 0 bad checksums" in p.stdout, p.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_poll", [1, 37, 512, 8192])
+def test_gpu_server_matches_twin(per_poll):
+    p = _run("gpu", str(per_poll))
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "gpu: handler log identical, TX frames identical" in p.stdout, p.stdout
