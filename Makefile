@@ -22,12 +22,13 @@ RINGTEST = tests/cpp/test_rx_ring
 STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
 SERVERTEST = tests/cpp/test_tcp_server
+PEERTEST = tests/cpp/test_tcp_server_peer
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST)
+all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
-$(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_server.hpp \
+$(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp include/pollnet_amd/rx_ring.hpp $(HDRS) $(LIB) $(ORACLE) \
   oracle/_ref/tcpserver_handler.inc
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
@@ -35,6 +36,12 @@ $(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp include/pol
 
 oracle/_ref/tcpserver_handler.inc:
 	$(MAKE) ref
+
+# GpuTcpServer against reactive in-memory TCP peers (loss, timers, windows), GPU vs twin
+$(PEERTEST): tests/cpp/test_tcp_server_peer.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
+  include/pollnet_amd/tcp_server.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # TcpStream reassembly restated vs the reference's own TcpStream (4 instantiations)
 $(STREAMTEST): tests/cpp/test_tcp_stream.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_stream.hpp $(HDRS) $(LIB) $(ORACLE)
@@ -87,6 +94,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST)
+	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
 
 .PHONY: all ref clean

@@ -37,3 +37,29 @@ def test_gpu_server_matches_twin(per_poll):
     p = _run("gpu", str(per_poll))
     assert p.returncode == 0, p.stdout + p.stderr
     assert "gpu: handler log identical, TX frames identical" in p.stdout, p.stdout
+
+
+PEER = os.path.join(ROOT, "tests", "cpp", "test_tcp_server_peer")
+
+
+def _peer(mode):
+    if not os.path.exists(PEER):
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tcp_server_peer"], check=True, capture_output=True)
+    return subprocess.run([PEER, mode], capture_output=True, text=True, timeout=300)
+
+
+def test_server_twin_reactive_peers():
+    """120 reactive in-memory TCP clients with 3 % loss each way and a 1-ms-per-poll
+    clock: handshake / SYN-ACK and RTO retransmission, delayed ACKs, window-limited
+    sends, receive timeouts, admission refusal, server FINs — echoes intact, idle flows
+    timed out, nothing left open (sequential twin alone, no GPU)."""
+    p = _peer("twin")
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "PASS" in p.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_server_reactive_peers_match_twin():
+    p = _peer("gpu")
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "gpu: handler log identical, TX frames identical" in p.stdout, p.stdout
