@@ -8,7 +8,15 @@ CFLAGS_ORACLE = -O3 -march=x86-64-v3 -fPIC -Wall -std=c11
 LIB = pollnet_amd/libpollnet_amd.so
 SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
 HDRS = include/pollnet_amd.h
-KHDRS = pollnet_amd/csrc/frame_pass.hpp pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp
+KHDRS = pollnet_amd/csrc/frame_pass.hpp pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp \
+  pollnet_amd/csrc/rx_classify.hpp pollnet_amd/csrc/tx_fill.hpp
+# measurement-only library (bench ceilings; A/B variants with TUNING=1): never loaded by the product
+TUNING_LIB = pollnet_amd/libpollnet_amd_tuning.so
+TUNING_SRCS = pollnet_amd/csrc/rx_tuning.hip pollnet_amd/csrc/tx_tuning.hip
+TUNING ?= 0
+ifeq ($(TUNING),1)
+TUNING_FLAGS = -DPN_TUNING_VARIANTS
+endif
 
 ORACLE = oracle/liboracle.so
 REFDIR ?= /root/reference
@@ -24,7 +32,7 @@ GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
 SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
 
-all: $(LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
+all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
@@ -87,6 +95,9 @@ $(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(L
 $(LIB): $(SRCS) $(HDRS) $(KHDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lpthread
 
+$(TUNING_LIB): $(TUNING_SRCS) $(HDRS) include/pollnet_amd_tuning.h $(KHDRS)
+	$(HIPCC) $(HIPFLAGS) $(TUNING_FLAGS) -shared -o $@ $(TUNING_SRCS)
+
 $(ORACLE): oracle/pn_oracle.c oracle/pn_tx_oracle.c oracle/pn_oracle.h $(HDRS)
 	gcc $(CFLAGS_ORACLE) -shared -o $@ oracle/pn_oracle.c oracle/pn_tx_oracle.c -lpthread
 
@@ -94,6 +105,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
+	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
 
 .PHONY: all ref clean

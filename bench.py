@@ -197,6 +197,8 @@ def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, lens=None, reps=1
     with and without its 16-B/frame record writes.  With `lens` (u32 per slot: slot start
     to the frame's pad byte), the same pattern over each frame's own lines, in the RX
     kernel's workgroup order and occupancy: the ceiling for mixed-size rings (C3/C5)."""
+    from pollnet_amd import tuning as tn  # measurement-only library, never the product path
+
     sink = torch.zeros(4096, dtype=torch.int32, device=frames.device)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
@@ -209,18 +211,18 @@ def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, lens=None, reps=1
         torch.cuda.synchronize()
         return ev[0].elapsed_time(ev[1]) / reps * 1e-3
 
-    ts = t(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, stream))
+    ts = t(lambda: tn.calib_stream_read(ctx, frames, frames.numel(), sink, stream))
     out = {"stream_read_gbs": round(frames.numel() / ts / 1e9, 1),
-           "note": "calib kernels in pollnet_amd/csrc/rx_kernel.hip; no header work, no arithmetic"}
+           "note": "calib kernels in pollnet_amd/csrc/rx_tuning.hip (libpollnet_amd_tuning.so); no header work, no arithmetic"}
     if slot_pattern:
-        t0 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, sink, stream, 0))
-        t16 = t(lambda: ctx.calib_slot_read(frames, n, STRIDE, 1536, res, stream, 16))
+        t0 = t(lambda: tn.calib_slot_read(ctx, frames, n, STRIDE, 1536, sink, stream, 0))
+        t16 = t(lambda: tn.calib_slot_read(ctx, frames, n, STRIDE, 1536, res, stream, 16))
         out["slot_pattern_read_gbs"] = round(n * 1536 / t0 / 1e9, 1)
         out["slot_pattern_read_plus_16B_records_ms"] = round(t16 * 1e3, 5)
     if lens is not None:
         lens_dev = torch.from_numpy(lens).to(frames.device)
-        tv0 = t(lambda: ctx.calib_slot_read_var(frames, n, STRIDE, lens_dev, sink, stream, 0))
-        tv16 = t(lambda: ctx.calib_slot_read_var(frames, n, STRIDE, lens_dev, res, stream, 16))
+        tv0 = t(lambda: tn.calib_slot_read_var(ctx, frames, n, STRIDE, lens_dev, sink, stream, 0))
+        tv16 = t(lambda: tn.calib_slot_read_var(ctx, frames, n, STRIDE, lens_dev, res, stream, 16))
         out["frame_lines_read_ms"] = round(tv0 * 1e3, 5)
         out["frame_lines_read_plus_16B_records_ms"] = round(tv16 * 1e3, 5)
     return out

@@ -219,22 +219,6 @@ int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_o
 /* Wait for the last stream used by this ctx. */
 int pn_sync(pn_ctx* ctx);
 
-/* HBM streaming-read calibration kernel (used by bench/profiling only): reads
- * `bytes` (multiple of 16) from src and writes one u32 per workgroup to sink. */
-int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream);
-/* Ceiling for a slot layout: the first `bytes` (<= 2048) of each of n_slots slots,
- * read with the RX kernel's own load pattern and no arithmetic; store_bytes = 16 / 8
- * also writes that many bytes per slot to sink_dev (n_slots x 16 B) like the RX
- * kernel's records, 0 writes nothing; 16 | G << 8 (G = 1, 4, 16) writes the 16-B records of
- * G consecutive 64-slot groups in one burst per workgroup (write-grouping probe). */
-int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
-                       int store_bytes, void* sink_dev, void* stream);
-/* Ceiling for variable-length frames: slot i's first lens_dev[i] bytes (u32 per slot, device
- * memory; clamped to min(stride, 2048)), same load pattern, workgroup order and occupancy as
- * the RX kernel, no arithmetic; store_bytes 16 also writes a 16-B record per slot, 0 none. */
-int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
-                           int store_bytes, void* sink_dev, void* stream);
-
 /* ======================= synthetic frame generator =======================
  * Deterministic (seed, frame index) generator for the BASELINE configs; writes
  * slots into host memory with bytes after each frame zero-filled.  Multi-threaded.

@@ -166,9 +166,18 @@ class GpuRx {
 
   // Chunked pipeline shared by pollBatch / pollIndexed: chunk k+1 is launched before
   // chunk k is dispatched; eth_of(i) = frame i's Ethernet header in host memory.
+  // An error leaves no chunk in flight: the stream is drained before returning, so the
+  // next call may reuse the pinned buffers at once.
   template <class Launch, class EthOf, class RecvHandler, class TwHandler>
   const char* run(uint32_t n, const ConnTable& table, Launch&& launch_k, EthOf&& eth_of, RecvHandler& recv_handler,
                   TwHandler& tw_handler) {
+    const char* e = run_chunks(n, table, launch_k, eth_of, recv_handler, tw_handler);
+    if (e) (void)hipStreamSynchronize(stream_);
+    return e;
+  }
+  template <class Launch, class EthOf, class RecvHandler, class TwHandler>
+  const char* run_chunks(uint32_t n, const ConnTable& table, Launch& launch_k, EthOf& eth_of, RecvHandler& recv_handler,
+                         TwHandler& tw_handler) {
     if (n == 0) return nullptr;
     const uint32_t chunks = (n + cap_ - 1) / cap_;
     if (const char* e = launch_k(0)) return e;

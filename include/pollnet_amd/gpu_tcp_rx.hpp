@@ -21,6 +21,9 @@
 //   void onAckOwed(Conn&, const RxAck&);
 //   void onNewSegment(uint64_t key, const uint8_t* eth, const pn_result& rec);
 //   void onTimeWaitSegment(uint64_t key, uint32_t tw_id, const uint8_t* eth, const pn_result& rec);
+// (GpuTcpServer, tcp_server.hpp, builds pollnet's own surface on the same records and
+// decides the TIME_WAIT and unknown-flow branches itself; this class leaves them to the
+// caller's control plane.)
 //
 // Table changes made during a poll (accept()/remove()/enterTW() from a callback) are
 // seen by the records after them, as in the reference's sequential loop: once the
@@ -64,6 +67,9 @@ class GpuTcpRx {
     if ((e = rx_.init(device, slot_stride, frame_off, max_batch, mode))) return e;
     free_.clear();
     for (uint32_t i = Conf::MaxConnCnt; i-- > 0;) free_.push_back(i);
+    free_tw_.clear();
+    for (uint32_t i = Conf::MaxTimeWaitConnCnt; i-- > 0;) free_tw_.push_back(i);
+    tw_keys_.assign(Conf::MaxTimeWaitConnCnt, PN_EMPTY_KEY);
     dirty_ = true;
     return nullptr;
   }
@@ -94,18 +100,40 @@ class GpuTcpRx {
       dirty_ = true;
     }
   }
-  // The connection enters TIME_WAIT under tw_id (Core::enterTW, Core.h:627-647).
-  int enterTW(Conn& c, uint32_t tw_id) {
+  // The connection enters TIME_WAIT (Core::enterTW, Core.h:607-638): its entry is relabelled
+  // MaxConnCnt + tw_id with a TIME_WAIT id taken here.  Returns the tw_id; when all
+  // MaxTimeWaitConnCnt ids are taken the entry is deleted instead, as the reference does
+  // (Core.h:608-611), and PN_EFULL is returned.  PN_ENOENT: the connection holds no entry.
+  int enterTW(Conn& c) {
     if (!c.live) return PN_ENOENT;
-    const int rc = table_.enterTW(c.key, tw_id);
-    if (rc == PN_OK) {
-      c.live = false;
-      free_.push_back(c.id);
-      --conn_cnt_;
-      dirty_ = true;
+    if (free_tw_.empty()) {
+      remove(c);
+      return PN_EFULL;
     }
-    return rc;
+    const uint32_t tw_id = free_tw_.back();
+    const int rc = table_.enterTW(c.key, tw_id);
+    if (rc != PN_OK) return rc;
+    free_tw_.pop_back();
+    tw_keys_[tw_id] = c.key;
+    c.live = false;
+    free_.push_back(c.id);
+    --conn_cnt_;
+    dirty_ = true;
+    return (int)tw_id;
   }
+  // A TIME_WAIT entry ends (Core::delConnEntry on an in-sequence RST, Core.h:513-517, or
+  // when the TIME_WAIT timer fires, Core.h:740-744): the key is free for a new SYN.  The
+  // snapshot is marked stale, so later records of the same poll are re-resolved.
+  int removeTW(uint32_t tw_id) {
+    if (tw_id >= Conf::MaxTimeWaitConnCnt || tw_keys_[tw_id] == PN_EMPTY_KEY) return PN_ENOENT;
+    const int rc = table_.del(tw_keys_[tw_id]);
+    if (rc != PN_OK) return rc;
+    tw_keys_[tw_id] = PN_EMPTY_KEY;
+    free_tw_.push_back(tw_id);
+    dirty_ = true;
+    return PN_OK;
+  }
+  uint32_t getTimeWaitCnt() const { return Conf::MaxTimeWaitConnCnt - (uint32_t)free_tw_.size(); }
 
   uint32_t getConnCnt() const { return conn_cnt_; } // EfviTcp.h:256
   template <class F>
@@ -113,7 +141,7 @@ class GpuTcpRx {
     for (Conn& c : conns_)
       if (c.live) f(c);
   }
-  ConnTable& table() { return table_; }
+  const ConnTable& table() const { return table_; } // changes go through accept/remove/enterTW/removeTW
   GpuRx& rx() { return rx_; }
 
   // Classify n ring slots (host memory) on the GPU and dispatch them in ring order.
@@ -153,6 +181,9 @@ class GpuTcpRx {
     GpuTcpRx* self;
     Handler& h;
     void operator()(uint64_t key, const pn_result& rec, const uint8_t* eth) {
+      // a frame cut at its slot (or outside the indexed call's class) has no trustworthy
+      // payload extent: never delivered, whatever drop_bad_ says
+      if (rec.flags & (PN_F_TRUNC | PN_F_BADOFF)) return;
       if (self->drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
       pn_result r = rec;
       if (self->dirty_) { // the table changed earlier in this poll: resolve on the host, fix the record
@@ -197,7 +228,8 @@ class GpuTcpRx {
   GpuRx rx_;
   ConnTable table_;
   std::vector<Conn> conns_;
-  std::vector<uint32_t> free_;
+  std::vector<uint32_t> free_, free_tw_;
+  std::vector<uint64_t> tw_keys_; // key of each TIME_WAIT id in use (PN_EMPTY_KEY: free)
   uint32_t conn_cnt_ = 0;
   bool dirty_ = true;
   bool drop_bad_ = false;

@@ -1,0 +1,45 @@
+/*
+ * pollnet_amd_tuning.h — measurement-only entry points (libpollnet_amd_tuning.so).
+ *
+ * NOT part of the product ABI (include/pollnet_amd.h) and never loaded by the product
+ * path: same-run bandwidth ceilings that bench.py reports beside the production kernel,
+ * and (built with `make TUNING=1` only) the A/B variants of the RX and TX kernels that
+ * scripts/variants.py / scripts/tx_variants.py time.  Contexts come from pn_open().
+ */
+#ifndef POLLNET_AMD_TUNING_H
+#define POLLNET_AMD_TUNING_H
+
+#include "pollnet_amd.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* HBM streaming-read calibration kernel (used by bench/profiling only): reads
+ * `bytes` (multiple of 16) from src and writes one u32 per workgroup to sink. */
+int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream);
+/* Ceiling for a slot layout: the first `bytes` (<= 2048) of each of n_slots slots,
+ * read with the RX kernel's own load pattern and no arithmetic; store_bytes = 16 / 8
+ * also writes that many bytes per slot to sink_dev (n_slots x 16 B) like the RX
+ * kernel's records, 0 writes nothing; 16 | G << 8 (G = 1, 4, 16) writes the 16-B records of
+ * G consecutive 64-slot groups in one burst per workgroup (write-grouping probe). */
+int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
+                       int store_bytes, void* sink_dev, void* stream);
+/* Ceiling for variable-length frames: slot i's first lens_dev[i] bytes (u32 per slot, device
+ * memory; clamped to min(stride, 2048)), same load pattern, workgroup order and occupancy as
+ * the RX kernel, no arithmetic; store_bytes 16 also writes a 16-B record per slot, 0 none. */
+int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
+                           int store_bytes, void* sink_dev, void* stream);
+
+/* ---- A/B variants (make TUNING=1; ids documented at their definitions) ---- */
+int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                        void* results_dev, void* stream, int variant);
+int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
+                                uint32_t avail, void* results_dev, void* stream, int variant);
+int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                       const uint16_t* lens, int variant, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLLNET_AMD_TUNING_H */

@@ -1,0 +1,442 @@
+// rx_classify.hpp — the RX classify kernel (device code + launch helpers), shared by the
+// product library (rx_kernel.hip: the production instantiations behind pn_classify /
+// pn_classify_indexed) and the tuning library (rx_tuning.hip: A/B variants, ceilings).
+// Included by exactly one translation unit per library; everything is internal linkage.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/pollnet_amd.h"
+#include "device_common.hpp"
+#include "frame_pass.hpp"
+#include "pn_internal.hpp"
+
+// The MI355X (gfx950) receive-path per-frame transform: Ethernet/IPv4/TCP header
+// parse, IP + TCP one's-complement verification, conn-table probe and
+// payload off/len for a batch of RX-ring slots resident in HBM.
+//
+// Reference path (per frame, scalar): efvitcp/Core.h:503-526 (pointers, key,
+// findConnEntry, TIME_WAIT test), Core.h:448-472 (checksum, debug build),
+// Core.h:89-138 (CSum), TcpConn.h:469-473 (payload arithmetic).
+//
+// Execution model (one wavefront = 64 frames, 64-thread workgroups, no
+// inter-wave communication):
+//  phase 1  lane f owns frame f: gets a 112-B header window (either 8 lanes per
+//           slot load its first 128-B line coalesced into a swizzled LDS tile, or
+//           each lane loads its own window when the layout is not line-aligned),
+//           decodes fields at compile-time offsets (kernel specialised on
+//           (frame_off+14)%16), computes the 20-byte IP sum, the sum of the
+//           frame's words inside the window, connHashKey and the ordered probe
+//           of the (L2-resident) conn table.
+//  phase 2  the wave streams the rest of each frame's summed region
+//           [ip, ip+20+tcp_len(+pad)) from the window end on, with
+//           1 KiB buffer_load_dwordx4 instructions (64 lanes x 16 B), summing
+//           u16 halves with v_dot2_u32_u16 (exact integer sums, no folding),
+//           8 frames per batch, reduced across lanes with permlane32/16 swaps
+//           and DPP (one value per lane per batch) and parked on the frame's lane.
+//  phase 3  lane f subtracts the IP-header words, adds the pseudo-header and
+//           folds exactly like CSum::fold; one coalesced 16-B record per lane.
+// HBM bytes per frame = the frame itself (+16 B result): the kernel is bound by
+// HBM bandwidth (no MFMA: there is no contraction).  It runs within ~1 % of a
+// no-arithmetic kernel with the same reads and record writes;
+// the remaining gap to pure streaming is the DRAM cost of interleaving the
+// record writes with the frame reads.
+namespace {
+
+using namespace pn_dev;
+using pn_internal::g_err;
+using pn_internal::hip_err;
+using pn_internal::set_err;
+
+struct KArgs {
+  const uint8_t* frames;
+  pn_result* out;
+  const pn_conn_entry* tbl;
+  uint64_t mask;
+  uint32_t n_entries;
+  uint32_t max_conn;
+  uint32_t n;
+  uint32_t stride;
+  uint32_t ipa_off; // (frame_off + 14) & ~15: 16-B aligned start of the header window
+  uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
+  const uint64_t* offs; // indexed layout: frame i's Ethernet header at frames + offs[i] (nullptr: strided)
+  uint32_t fpw = kFramesPerWave; // frames per wave (8..64): small batches spread over more waves (latency)
+};
+
+// Per-frame state the header lane keeps from phase 1 to phase 3.
+struct FrameState {
+  uint32_t flags, ihl, tot_len, src_ip, dst_ip, seq_raw, doff, tflags, s_ip20, s_opt, tcp_len, conn_id;
+  uint32_t t_all; // exact u16-word sum of [ip, ip+20+tcp_len(+pad)) accumulated so far
+  int end_rel;    // summed extent relative to the window start (even), | 1 when tcp_len is odd; 0 = nothing to stream
+  uint32_t pad;   // odd tcp_len: the byte after the segment (kPadUnknown until phase 2 captured it)
+  bool trunc;
+};
+
+// ---- phase 1: decode one frame from its header window (lane f <-> frame f) ----
+template <int MIS, int ABL>
+__device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t ether_type, bool live, uint32_t s0,
+                                                   const KArgs& a) {
+  static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
+  FrameState st;
+  // IpHeader (Core.h:57-69), fields relative to ip = window + MIS
+  const uint32_t ver_ihl = h.template b8<MIS + 0>();
+  st.ihl = ver_ihl & 0xf;
+  st.tot_len = bswap16(h.template u16<MIS + 2>());
+  const uint32_t proto = h.template b8<MIS + 9>();
+  st.src_ip = h.template u32<MIS + 12>();
+  st.dst_ip = h.template u32<MIS + 16>();
+  // TcpHeader at ip + 20 (IHL assumed 5: Core.h:507)
+  const uint32_t src_port = h.template u16<MIS + 20>();
+  st.seq_raw = h.template u32<MIS + 24>();
+  st.doff = h.template b8<MIS + 32>() >> 4;
+  st.tflags = h.template b8<MIS + 33>();
+
+  uint32_t flags = (st.tflags & 0x1f) << 4; // fin,syn,rst,psh,ack -> PN_F_FIN..PN_F_ACK
+  if (ether_type != 0x0008 || (ver_ihl >> 4) != 4 || proto != 6) flags |= PN_F_NOT_TCP;
+  if (st.ihl != 5) flags |= PN_F_IHL_NE_5;
+
+  // CSum.add<20>(ip).fold() (Core.h:451-453)
+  st.s_ip20 = h.template sum16<MIS, MIS + 20>();
+  if (csum_fold(st.s_ip20) == 0) flags |= PN_F_IP_OK;
+  // RFC option words [20, 4*IHL)
+  st.s_opt = 0;
+  if (st.ihl > 5) st.s_opt = h.template sum16_upto<MIS + 20, MIS + 60>(MIS + 4 * st.ihl);
+
+  // uint16_t tcp_len = ntohs(tot_len) - 20 ; CSum::add(tcp, tcp_len) reads ceil(tcp_len/2) words
+  st.tcp_len = (st.tot_len - 20) & 0xffff;
+  const uint32_t seg_even = (st.tcp_len + 1) & ~1u;
+  st.trunc = 34 + seg_even > a.avail;
+  if (st.trunc) flags |= PN_F_TRUNC;
+  // summed region relative to the window: [MIS, MIS + 20 + seg_even); bit 0 flags an odd
+  // tcp_len, whose last summed byte (end - 1) is the byte after the segment
+  st.end_rel = (live && !st.trunc) ? (int)((MIS + 20 + seg_even) | (st.tcp_len & 1)) : 0;
+  st.pad = kPadUnknown;
+
+  // the part of the region in the window below the stream start, summed from registers
+  st.t_all = window_part<MIS>(h, st.end_rel & ~1, s0);
+
+  // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
+  st.conn_id = PN_MISS;
+  if constexpr (!(ABL & kAblNoProbe)) {
+    const uint32_t ip_h = __builtin_bswap32(st.src_ip);
+    const uint32_t port_h = bswap16(src_port);
+    const uint64_t key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
+    uint32_t e = (uint32_t)(key & a.mask);
+    uint64_t k = PN_EMPTY_KEY;
+    uint32_t cid = 0;
+    if (live && e < a.n_entries) { // the home slot: almost every lookup ends here
+      const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
+      k = ((uint64_t)ent.y << 32) | ent.x;
+      cid = ent.z;
+    }
+    if constexpr (ABL & kCoopProbe) {
+      // Lanes whose run continues past the home slot are served one at a time by the whole
+      // wave (all 64 lanes reach here): 64 consecutive entries per round trip, the first with
+      // key >= the lane's key (or the array end) found by a ballot -- the entry the scalar
+      // walk stops at.
+      const uint32_t lane = threadIdx.x;
+      bool srch = live && e < a.n_entries && k < key;
+      if (__ballot(srch) != 0) {
+        // short runs (the common case past the home slot): every searching lane fetches its
+        // next kAhead entries at once -- one round trip for all of them, in parallel
+        constexpr int kAhead = 2;
+        u32x4 nx[kAhead];
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j) {
+          nx[j] = u32x4{0u, 0u, 0u, 0u};
+          if (srch && e + 1 + j < a.n_entries) nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + e + 1 + j);
+        }
+        uint32_t step = 0, cid2 = 0;
+        uint64_t k2 = 0;
+#pragma unroll
+        for (int j = kAhead - 1; j >= 0; --j) { // the first entry (in order) that stops the walk
+          const uint64_t kk = ((uint64_t)nx[j].y << 32) | nx[j].x;
+          if (e + 1 + j >= a.n_entries || kk >= key) {
+            step = j + 1;
+            k2 = kk;
+            cid2 = nx[j].z;
+          }
+        }
+        if (srch) {
+          if (step != 0) {
+            e += step;
+            k = k2;
+            cid = cid2;
+            srch = false;
+          } else {
+            e += kAhead; // every fetched key < key: the run goes on
+          }
+        }
+      }
+      uint64_t need = __ballot(srch);
+      while (need != 0) { // wave-uniform
+        const uint32_t L = (uint32_t)__builtin_ctzll(need);
+        need &= need - 1;
+        const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L); // readlane returns int
+        for (uint32_t base = __builtin_amdgcn_readlane(e, L) + 1;; base += kWave) {
+          const uint32_t idx = base + lane;
+          u32x4 ent = {0u, 0u, 0u, 0u};
+          if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
+          const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
+          const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
+          if (stop != 0) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(stop);
+            const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
+            const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
+            if (lane == L) {
+              e = base + first;
+              k = ((uint64_t)khi << 32) | klo;
+              cid = c;
+            }
+            break;
+          }
+        }
+      }
+    } else {
+      while (live && e < a.n_entries && k < key) {
+        if (++e >= a.n_entries) break;
+        const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
+        k = ((uint64_t)ent.y << 32) | ent.x;
+        cid = ent.z;
+      }
+    }
+    if (live && e < a.n_entries && k == key) {
+      st.conn_id = cid;
+      flags |= PN_F_HIT;
+      if (cid >= a.max_conn) flags |= PN_F_TW;
+    }
+  }
+  st.flags = flags;
+  return st;
+}
+
+// ---- phase 3: fold and write the record on the frame's lane ----
+template <int MIS, int ABL, int SAUX>
+__device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f, const uint8_t* win, bool bad_off,
+                                       u32x4* lds_rec) {
+  uint32_t flags = st.flags;
+  uint32_t tcp_fold = 0xffff;
+  if (!st.trunc) {
+    const uint32_t s_seg = st.t_all - st.s_ip20; // exact: both are exact word sums
+    const uint32_t s_addr = (st.src_ip >> 16) + (st.src_ip & 0xffff) + (st.dst_ip >> 16) + (st.dst_ip & 0xffff);
+    // sum.add(ntohs(0x6)) ; sum.add(htons(tcp_len))  (Core.h:462-464)
+    tcp_fold = csum_fold(s_addr + 0x0600 + bswap16(st.tcp_len) + s_seg);
+    if (tcp_fold == 0) flags |= PN_F_TCP_OK;
+    const uint32_t hl = 4 * st.ihl;
+    if (st.ihl >= 5 && hl <= st.tot_len) {
+      if (csum_fold(st.s_ip20 + st.s_opt) == 0) flags |= PN_F_RFC_IP_OK;
+      uint32_t pad = 0;
+      if (st.tot_len & 1) { // the byte the reference sums past the segment (high half of the last word)
+        uint32_t b = st.pad;
+        if (b == kPadUnknown) b = (win + MIS)[st.tot_len]; // in-window / jumbo
+        pad = b << 8;
+      }
+      const uint32_t rfc = s_addr + 0x0600 + bswap16(st.tot_len - hl) + (s_seg - st.s_opt - pad);
+      if (csum_fold(rfc) == 0) flags |= PN_F_RFC_TCP_OK;
+    }
+  }
+  // TcpConn::onPack (TcpConn.h:469-473)
+  const int data_off = 34 + 4 * (int)st.doff;
+  const int data_end = 14 + (int)min(st.tot_len, 1500u);
+  u32x4 rec;
+  rec.x = st.conn_id;
+  rec.y = __builtin_bswap32(st.seq_raw) + ((st.tflags >> 1) & 1);
+  rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
+  rec.w = flags | (tcp_fold << 16);
+  if (bad_off) rec = u32x4{PN_MISS, 0, 0, PN_F_BADOFF}; // outside the launch's alignment class: not parsed
+  if (lds_rec) { // grouped launches write the workgroup's records in one burst at its end
+    *lds_rec = rec;
+  } else if constexpr (ABL & kAblNoStore) {
+    if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
+  } else if constexpr (ABL & kAblStore8) { // timing only: half the record bytes
+    reinterpret_cast<uint2*>(a.out)[f] = uint2{rec.x ^ rec.y, rec.z ^ rec.w};
+  } else if constexpr (ABL & kAblGlobalStore) { // the record through a plain global store (SAUX ignored)
+    *reinterpret_cast<u32x4*>(a.out + f) = rec;
+  } else {
+    // one coalesced 1-KiB store per wave; the descriptor covers this wave's 64 records
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc((const uint8_t*)(a.out + (f & ~63u)), 64 * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(rec, rs, (f & 63u) * 16, 0, SAUX);
+  }
+}
+
+// ---- the kernel: one 64-frame group per 64-thread workgroup ----
+// COOP = 1: 8 lanes per slot load its 128-B window block (the 16-B chunk before the
+// window + the window; the slot's first line in the default layout) into an
+// XOR-swizzled LDS tile that the header lanes read back (load_window_strided).
+// COOP = 0: each lane loads its own 112-B window (frame_off = 0).
+// IDX = 1: indexed layout (frame i at frames + offs[i], any place, same (offs+14)%16
+// class); per-frame stream descriptors; with COOP, waves whose frames all have their
+// block 16-B aligned inside the ring load blocks cooperatively, other waves per-lane
+// bounds-checked windows.
+// 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
+// default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
+template <int MIS, int COOP, int ABL, int LAUX, int SAUX, int IDX, int LWIN>
+__device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wave_base, const int lane, u32x4* lds_recs) {
+  if (wave_base >= a.n) return;
+  const uint32_t f = wave_base + lane;
+  const uint32_t n_here = min(a.fpw, a.n - wave_base);
+  const bool live = (uint32_t)lane < n_here;
+  const uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
+  // one wave-uniform descriptor over the wave's slots; lanes past n read zeros
+  const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
+
+  Window h;
+  uint32_t ether_type;
+  const uint8_t* win = nullptr; // this lane's window start (ip - MIS)
+  bool bad_off = false;
+  if constexpr (IDX) {
+    ether_type = 0;
+#pragma unroll
+    for (int q = 0; q < 4 * kWinChunks; ++q) h.d[q] = 0;
+    const uint64_t o = live ? a.offs[f] : 0;
+    bad_off = live && ((o + 14) & 15) != (uint64_t)MIS;
+    win = a.frames + o + 14 - MIS;
+    bool coop_done = false;
+    if constexpr (COOP) {
+      // Cooperative window: when every frame of the wave has its 128-B window block (the
+      // 16-B chunk before the window, and the window) 16-B aligned inside [base, eth + avail),
+      // 8 lanes per frame load the block coalesced into the LDS tile, as the strided kernel
+      // does (one request per line; the second line of a straddling block only when the
+      // header fields reach it); otherwise the wave falls back to per-lane windows.
+      const bool use = live && !bad_off;
+      const bool elig = !use || ((((uintptr_t)win & 15u) == 0) && o + 14 >= (uint64_t)(MIS + 16) &&
+                                 (uint32_t)(14 - MIS + kWinBytes) <= a.avail);
+      if (__all(elig)) {
+        __shared__ uint64_t line_addr[kFramesPerWave];
+        line_addr[lane] = use ? (uint64_t)(win - 16) : 0ull;
+        __syncthreads();
+        u32x4* tile = coop_tile();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+          const uint64_t la = line_addr[r];
+          u32x4 v = {0u, 0u, 0u, 0u};
+          if (la && block_part_needed<MIS>((uint32_t)la, part)) {
+            if constexpr (LWIN == 0) v = reinterpret_cast<const u32x4*>(la)[part]; // default policy (tuning)
+            else v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
+          }
+          tile[r * 8 + (part ^ (r & 7))] = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < kWinChunks; ++c) {
+          const u32x4 v = tile[lane * 8 + ((1 + c) ^ (lane & 7))];
+          h.d[4 * c + 0] = v.x;
+          h.d[4 * c + 1] = v.y;
+          h.d[4 * c + 2] = v.z;
+          h.d[4 * c + 3] = v.w;
+        }
+        if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+        else ether_type = tile[lane * 8 + (0 ^ (lane & 7))].w >> 16;
+        coop_done = true;
+      }
+    }
+    if (live && !coop_done) {
+      if (!bad_off) {
+        // window chunk c spans eth + (14 - MIS) + 16c .. +16: load it only inside avail
+#pragma unroll
+        for (int c = 0; c < kWinChunks; ++c) {
+          if ((uint32_t)(14 - MIS + 16 * c + 16) <= a.avail) {
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(win) + c);
+            h.d[4 * c + 0] = v.x;
+            h.d[4 * c + 1] = v.y;
+            h.d[4 * c + 2] = v.z;
+            h.d[4 * c + 3] = v.w;
+          }
+        }
+        if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
+        else ether_type = *reinterpret_cast<const uint32_t*>(win - 4) >> 16; // eth + 10 - MIS >= eth
+      }
+    }
+  } else {
+    ether_type = load_window_strided<MIS, COOP, LWIN>(rs, lane, a.stride, a.ipa_off, (uint32_t)(uintptr_t)wave_slot, h);
+  }
+  if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
+  FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, stream_start((uint64_t)win), a);
+  stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
+  if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
+}
+
+// GRP = 1: one 64-frame group per workgroup, records stored as each group finishes.
+// GRP > 1 (tuning variants): GRP consecutive groups per workgroup, their records kept in
+// LDS and written in one GRP-KiB burst at the end (scripts/write_grouping.py probe).
+// GOPT (tuning): bit 0 = GRP groups per workgroup but records stored per group (no LDS);
+// bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 5;
+// GOPT >> 4 = KiB of LDS padding, which caps workgroups per CU.  Production pads 2 KiB:
+// with the 8-KiB window tile that is 10 KiB per workgroup, 16 per CU = 4 waves/SIMD where
+// registers would allow 5 -- C2 -1.2 %, C3 -2.5 %, C5 -0.3 % (3 waves: C3 +9 %, C5 +13 %;
+// profiles/r01_experiments/occupancy_c{2,3,5}.json).
+// Bit 3: XCD-aware order.  Workgroup b is dispatched to XCD b % 8; mapping it to group
+// (b % 8) * ceil(G / 8) + b / 8 gives every XCD one contiguous eighth of the batch (its own
+// L2 and memory-side traffic stays in one region): C2 -1.2 %, C3 -4.2 %, C5 -3.4 %
+// (profiles/r01_experiments/xcd_order_c{2,3,5}.json; records identical).
+constexpr int kXcdOrder = 8;
+constexpr int kProdGopt = (2 << 4) | kXcdOrder;
+template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
+          int GRP = 1, int GOPT = kProdGopt>
+__global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
+  const int lane = threadIdx.x;
+  if constexpr ((GOPT >> 4) > 0) {
+    __shared__ uint32_t pad_lds[(GOPT >> 4) * 256];
+    pad_lds[lane] = lane;
+    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
+  }
+  if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
+    // contiguous eighth of the batch instead of every eighth group
+    classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, xcd_group(blockIdx.x, gridDim.x) * a.fpw, lane, nullptr);
+  } else if constexpr (GRP == 1 || (GOPT & 1)) {
+#pragma nounroll
+    for (int g = 0; g < GRP; ++g)
+      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, (blockIdx.x * GRP + g) * a.fpw, lane, nullptr);
+  } else {
+    __shared__ u32x4 recs[GRP * kFramesPerWave];
+    const uint32_t first = blockIdx.x * GRP * kFramesPerWave;
+#pragma nounroll
+    for (int g = 0; g < GRP; ++g) // not unrolled: two groups' live ranges overlapping would halve occupancy
+      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, first + g * kFramesPerWave, lane, recs + g * kFramesPerWave);
+    __syncthreads();
+    if (first >= a.n) return;
+    const uint32_t cnt = min((uint32_t)(GRP * kFramesPerWave), a.n - first);
+    const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.out + first), cnt * 16); // stores past n dropped
+#pragma unroll
+    for (int g = 0; g < GRP; ++g)
+      __builtin_amdgcn_raw_buffer_store_b128(recs[g * kFramesPerWave + lane], ro, (g * kFramesPerWave + lane) * 16, 0, SAUX);
+  }
+}
+} // namespace
+
+namespace {
+// Whether the cooperative header-window load applies: a 16-B chunk precedes the
+// window inside the slot (frame_off >= 2) and blocks are 16-B aligned.  One request
+// per block line: a single line for the default frame_off = 2 layout and ef_vi's
+// 10 + prefix for prefix <= 5, two otherwise.
+inline bool coop_layout(const KArgs& a) {
+  return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
+}
+
+// Indexed launches load the cooperative window blocks at the default cache policy: in a
+// packed capture a frame's last line is the next frame's window line, and a block loaded
+// with default policy is still in L2 when the previous frame's stream asks for it
+// (packed C2/C3/C5 -8..-10 %, permuted ef_vi event runs -2 %, in-order slot runs +1 %;
+// profiles/r01_experiments/indexed_window_policy_c{2,3,5}.json).
+constexpr int kIdxWin = 0;
+
+template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
+          int GRP = 1, int GOPT = kProdGopt>
+void launch_one(const KArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((rx_classify_kernel<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN, GRP, GOPT>),
+                     dim3((a.n + GRP * a.fpw - 1) / (GRP * a.fpw)), dim3(kWave), 0, s, a);
+}
+
+
+template <int MIS>
+void launch(const KArgs& a, hipStream_t s) {
+  if (coop_layout(a)) return launch_one<MIS, 1>(a, s);
+  launch_one<MIS, 0>(a, s);
+}
+} // namespace

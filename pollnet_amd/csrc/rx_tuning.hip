@@ -1,0 +1,310 @@
+// Tuning library (libpollnet_amd_tuning.so, include/pollnet_amd_tuning.h): the RX kernel's
+// A/B variants (scripts/variants.py, history in profiles/r01_experiments) and the
+// same-run bandwidth ceilings bench.py reports beside the production kernel.  Never
+// linked into or loaded by the product path; the variants are compiled only with
+// `make TUNING=1` (-DPN_TUNING_VARIANTS).
+#include "rx_classify.hpp"
+
+namespace {
+using pn_internal::g_err;
+using pn_internal::hip_err;
+using pn_internal::set_err;
+
+__global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src, uint64_t n16, uint32_t* sink) {
+  // the whole grid sweeps the buffer front to back, one 16-B coalesced load per lane per step
+  uint32_t acc = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256) {
+    const u32x4 v = src[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc; // keeps the loads live; practically never stores
+}
+
+// Read-only ceilings for the slot layout (no header work, no arithmetic): each wave
+// streams the first `bytes` of each of its 64 slots with the RX kernel's 1-KiB
+// buffer loads, 8 slots per batch.  STORE = 16 / 8: plus a per-slot record store
+// of that many bytes at the wave's end (sink holds n x 16 B), the RX kernel's
+// write pattern.
+template <int STORE>
+__global__ __launch_bounds__(kWave) void calib_slot_read_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                               uint32_t bytes, uint32_t* sink) {
+  const int lane = threadIdx.x;
+  const uint32_t wave_base = blockIdx.x * kFramesPerWave;
+  if (wave_base >= n) return;
+  const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+  const uint8_t* wb = base + (uint64_t)wave_base * stride;
+  uint32_t acc = 0;
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    u32x4 w0s[kBatch], w1s[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const uint32_t nb = (b0 + j < n_here) ? bytes : 0u;
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+  }
+  if constexpr (STORE == 16) {
+    if (lane < (int)n_here) {
+      u32x4 r = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+      *reinterpret_cast<u32x4*>(sink + 4 * (uint64_t)(wave_base + lane)) = r;
+    }
+  } else if constexpr (STORE == 8) {
+    if (lane < (int)n_here) *reinterpret_cast<uint64_t*>(sink + 2 * (uint64_t)(wave_base + lane)) = ((uint64_t)acc << 32) | acc;
+  } else {
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+  }
+}
+
+// Ceiling for variable-length frames (C3/C5 slot rings): slot i's first lens[i] bytes (the
+// frame's lines, from the slot start to the frame's pad byte), read with the RX kernel's load
+// pattern, workgroup order (each XCD a contiguous eighth) and LDS occupancy cap, no arithmetic;
+// STORE = 16 adds the 16-B records.  Out-of-range dwords of a line cost no extra traffic.
+template <int STORE>
+__global__ __launch_bounds__(kWave) void calib_slot_read_var_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                                   const uint32_t* lens, uint32_t* sink) {
+  __shared__ uint32_t pad_lds[512];
+  const int lane = threadIdx.x;
+  pad_lds[lane] = lane;
+  if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) n = 0; // never true: keeps the padding allocated
+  const uint32_t wave_base = xcd_group(blockIdx.x, gridDim.x) * kFramesPerWave;
+  if (wave_base >= n) return;
+  const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+  const uint8_t* wb = base + (uint64_t)wave_base * stride;
+  uint32_t acc = 0;
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    u32x4 w0s[kBatch], w1s[kBatch];
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) {
+      const uint32_t nb = (b0 + j < n_here) ? min(lens[wave_base + b0 + j], min(stride, 2048u)) : 0u;
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+  }
+  if constexpr (STORE == 16) {
+    if (lane < (int)n_here) {
+      u32x4 r = {acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+      *reinterpret_cast<u32x4*>(sink + 4 * (uint64_t)(wave_base + lane)) = r;
+    }
+  } else {
+    if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc;
+  }
+}
+
+// Write-grouping probe: the slot-read ceiling with each 64-thread workgroup owning G
+// consecutive 64-slot groups and writing their G x 64 16-B records (G KiB, contiguous) in
+// one burst at the end instead of 1 KiB after each group.
+// EACH = true: the same G-group loop, records written after each group (separates the
+// effect of fewer, longer workgroups from that of the write bursts).
+template <int G, bool EACH = false>
+__global__ __launch_bounds__(kWave) void calib_slot_read_grouped_kernel(const uint8_t* base, uint32_t n, uint32_t stride,
+                                                                       uint32_t bytes, uint32_t* sink) {
+  __shared__ u32x4 recs[EACH ? 1 : G * kFramesPerWave];
+  const int lane = threadIdx.x;
+  for (int g = 0; g < G; ++g) {
+    const uint32_t wave_base = (blockIdx.x * G + g) * kFramesPerWave;
+    uint32_t acc = 0;
+    if (wave_base < n) {
+      const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
+      const uint8_t* wb = base + (uint64_t)wave_base * stride;
+      for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+        u32x4 w0s[kBatch], w1s[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+          const uint32_t nb = (b0 + j < n_here) ? bytes : 0u;
+          const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
+          w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, kLoadAux);
+          w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, kLoadAux);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) acc ^= w0s[j].x ^ w0s[j].y ^ w0s[j].z ^ w0s[j].w ^ w1s[j].x ^ w1s[j].y ^ w1s[j].z ^ w1s[j].w;
+      }
+    }
+    if constexpr (EACH) {
+      if (wave_base + lane < n) {
+        const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(sink + 4 * (uint64_t)wave_base), 64 * 16);
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{acc, acc ^ 1u, acc ^ 2u, acc ^ 3u}, ro, lane * 16, 0, kStoreAux);
+      }
+    } else {
+      recs[g * kFramesPerWave + lane] = u32x4{acc, acc ^ 1u, acc ^ 2u, acc ^ 3u};
+    }
+  }
+  if constexpr (EACH) return;
+  __syncthreads();
+  const uint32_t first = blockIdx.x * G * kFramesPerWave;
+  const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(sink + 4 * (uint64_t)first),
+                                               16 * min((uint32_t)(G * kFramesPerWave), n - first));
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+    __builtin_amdgcn_raw_buffer_store_b128(recs[g * kFramesPerWave + lane], ro, (g * kFramesPerWave + lane) * 16, 0, kStoreAux);
+}
+
+} // namespace
+
+extern "C" {
+
+
+#ifdef PN_TUNING_VARIANTS
+// Tuning: the indexed kernel with the cooperative line window (variant 1) or without (0),
+// A/B-timed by scripts/bench_indexed.py; not part of the public header.
+int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
+                                uint32_t avail, void* results_dev, void* stream, int variant) {
+  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 3)
+    return set_err(ctx, PN_EINVAL, "indexed variant: bad args");
+  KArgs a;
+  a.frames = (const uint8_t*)base;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.n = n;
+  a.stride = 0;
+  a.ipa_off = 0;
+  a.avail = avail;
+  a.offs = offsets;
+  hipStream_t s = (hipStream_t)stream;
+  if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, kXcdOrder>(a, s); // window non-temporal
+  else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0, 1, 0>(a, s);  // production window, blockIdx order
+  else if (variant == 3) launch_one<0, 1, kProdAbl, 0, kStoreAux, 1, 0, 1, 0>(a, s);         // + stream at default policy
+  else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+
+int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                        void* results_dev, void* stream, int variant) {
+  if (!ctx || !ctx->tbl_dev || (frame_off + 14) % 16 != 0 || n == 0) return set_err(ctx, PN_EINVAL, "variant: bad args");
+  KArgs a;
+  a.frames = (const uint8_t*)frames_dev;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.offs = nullptr;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.avail = slot_stride - frame_off;
+  a.offs = nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  if ((variant & 1) && !coop_layout(a)) return set_err(ctx, PN_EINVAL, "variant: needs the cooperative layout");
+  // Tuning variants of the MIS = 0 (ip at slot+16) kernel, A/B-timed in one process by
+  // scripts/variants.py; not part of the public header.  History: profiles/r01_experiments.
+  switch (variant) {
+    case 0: launch_one<0, 0>(a, s); break;                         // per-lane window
+    case 1: launch_one<0, 1>(a, s); break;                         // cooperative window (production here)
+    case 2: launch_one<0, 0, kProdAbl, 0, 0>(a, s); break;                // per-lane, default cache policy
+    case 3: launch_one<0, 1, kProdAbl, 0, 0>(a, s); break;                // cooperative, default cache policy
+    case 4: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, 0>(a, s); break; // line-0 window default policy
+    case 5: launch_one<0, 1, kProdAbl, kLoadAux, 0>(a, s); break;         // default-policy record stores
+    case 6: launch_one<0, 1, kProdAbl, kLoadAux, 0, 0, 0>(a, s); break;   // both
+    case 7: launch_one<0, 1, kProdAbl, kLoadAux, 2>(a, s); break;         // nt record stores
+    case 8: launch_one<0, 1, kAblGlobalStore | kProdAbl>(a, s); break;        // plain global record store
+    case 9: launch_one<0, 1, 0>(a, s); break;                      // 16-B stream descriptors + per-dword tail masks
+    case 19: launch_one<0, 1, kAblStore8 | kProdAbl>(a, s); break;            // timing only: 8-B stores
+    case 22: launch_one<0, 1, kExactRange>(a, s); break;                         // scalar probe walk (before kCoopProbe)
+    case 23: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, 0>(a, s); break;  // 2 groups per WG, burst records
+    case 24: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 4, 0>(a, s); break;  // 4
+    case 25: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, 0>(a, s); break;  // 8
+    case 26: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 16, 0>(a, s); break; // 16
+    case 27: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, 1>(a, s); break;  // 8 groups, records per group
+    case 28: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2 << 4>(a, s); break;  // 1 group, +2 KiB LDS
+    case 29: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 6 << 4>(a, s); break;  // 1 group, +6 KiB LDS
+    case 30: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, (2 << 4) | 1>(a, s); break;  // 27 + 2 KiB
+    case 31: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2>(a, s); break;  // 1 group, 3-wave budget
+    case 32: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 4>(a, s); break;  // 1 group, 2-wave budget
+    case 33: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, 4>(a, s); break;  // 2 groups burst, 2-wave budget
+    case 34: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 0>(a, s); break;  // no LDS pad: 5 waves/SIMD
+    case 35: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, kProdGopt | 8>(a, s); break;  // XCD-contiguous (production)
+    case 36: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2 << 4>(a, s); break;  // blockIdx order
+    case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
+    case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
+    case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
+    case 18: launch_one<0, 1, kAblNoStore | kProdAbl>(a, s); break;
+    default: return set_err(ctx, PN_EINVAL, "variant: unknown");
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "variant launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+
+#endif // PN_TUNING_VARIANTS
+
+int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
+                       int store_bytes, void* sink_dev, void* stream) {
+  if (!ctx || !src_dev || !sink_dev || (stride & 15) || bytes > stride || bytes > 2048 || n_slots == 0)
+    return set_err(ctx, PN_EINVAL, "pn_calib_slot_read: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t waves = (n_slots + kFramesPerWave - 1) / kFramesPerWave;
+  const uint8_t* src = (const uint8_t*)src_dev;
+  uint32_t* sink = (uint32_t*)sink_dev;
+  switch (store_bytes) {
+    // 16 B records written per G groups (probe): store_bytes = 16 | G << 8
+    case 16 | (4 << 8): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<4>), dim3((waves + 3) / 4), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (16 << 8): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<16>), dim3((waves + 15) / 16), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (1 << 8): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<1>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (4 << 8) | (1 << 16): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<4, true>), dim3((waves + 3) / 4), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16 | (16 << 8) | (1 << 16): hipLaunchKernelGGL((calib_slot_read_grouped_kernel<16, true>), dim3((waves + 15) / 16), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 16: hipLaunchKernelGGL((calib_slot_read_kernel<16>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    case 8: hipLaunchKernelGGL((calib_slot_read_kernel<8>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink); break;
+    default: hipLaunchKernelGGL((calib_slot_read_kernel<0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, bytes, sink);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "calib slot launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+
+int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
+                           int store_bytes, void* sink_dev, void* stream) {
+  if (!ctx || !src_dev || !lens_dev || !sink_dev || (stride & 15) || n_slots == 0 ||
+      (store_bytes != 0 && store_bytes != 16))
+    return set_err(ctx, PN_EINVAL, "pn_calib_slot_read_var: bad arguments");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t waves = (n_slots + kFramesPerWave - 1) / kFramesPerWave;
+  const uint8_t* src = (const uint8_t*)src_dev;
+  const uint32_t* lens = (const uint32_t*)lens_dev;
+  uint32_t* sink = (uint32_t*)sink_dev;
+  if (store_bytes == 16)
+    hipLaunchKernelGGL((calib_slot_read_var_kernel<16>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, lens, sink);
+  else
+    hipLaunchKernelGGL((calib_slot_read_var_kernel<0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, lens, sink);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "calib slot var launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+
+int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream) {
+  if (!ctx || !src_dev || !sink_dev || (bytes & 15) || ((uintptr_t)src_dev & 15))
+    return set_err(ctx, PN_EINVAL, "pn_calib_stream_read: bad arguments");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  hipLaunchKernelGGL(calib_stream_read_kernel, dim3(2048), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src_dev,
+                     bytes / 16, (uint32_t*)sink_dev);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "calib launch");
+  ctx->last_stream = (hipStream_t)stream;
+  return PN_OK;
+}
+
+} // extern "C"

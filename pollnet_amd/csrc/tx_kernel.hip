@@ -1,274 +1,6 @@
-// MI355X (gfx950) TX checksum fill for a batch of outgoing frames.
-//
-// Reference: efvitcp never sums a frame in one pass; it carries one's-complement
-// state per connection and per send buffer and folds it when the frame leaves:
-//   TcpConn::reset / onEstablished cache the header sums (TcpConn.h:149-186, :422-428),
-//   sendPartial adds each appended piece with copyAndSum (TcpConn.h:238-240, :257-299),
-//   sendBuf adds seq/ack/window/timestamps (TcpConn.h:310-323),
-//   SendBuf::setOptDataLen writes tot_len and folds both sums (Core.h:157-163);
-//   resendUna patches the folded sum in place (TcpConn.h:771-785), sumRst builds
-//   RST / TIME_WAIT ACKs the same way (Core.h:385-398).  Efvi's UDP sender caches the
-//   IPv4 header sum once and folds it with each length (Efvi.h:405-411, 611-621).
-// Every one of those sums is congruent (mod 0xFFFF) to the plain RFC 1071 word sum of
-// the bytes that end up in the frame and is never 0, so CSum::fold of either gives the
-// same 16 bits: the kernel recomputes both checksums from the frame
-// bytes in one HBM pass and writes the values the reference's incremental path writes.
-// Efvi's cached fold is not CSum::fold: when the first end-around step of the cached
-// header sum carries, `cache += cache >> 16` keeps the carry bit and adds it again, so
-// the cache is one too large and the header checksum written with it does not verify
-// (DESIGN.md §12).  PN_TX_UDP_EFVI reproduces Efvi bit for bit, defect included;
-// PN_TX_UDP writes the same fields with CSum::fold (equal to Efvi everywhere else).
-//
-// Two launches per call:
-//  tx_fill_kernel   rx_kernel.hip's frame pass (frame_pass.hpp) — one wave per 64
-//                   slots, header window per lane, wave-wide 1-KiB streaming of each
-//                   frame's segment with exact dot2 word sums — then one 8-B patch
-//                   record per frame (the field values), written coalesced to ctx
-//                   scratch.  No write touches the frames here.
-//  tx_patch_kernel  one lane per frame writes its 2-byte fields into the frame.
-// Writing the fields in place from the first kernel costs 33-46 % of its time (DRAM
-// read/write interleaving over 1 Mi partially written lines); as a separate short
-// phase the same stores cost 22 % (profiles/r01_experiments/tx_variants_*.json).
-// HBM-bound: reads tot_len bytes (+ the Ethernet line head), writes 4-8 bytes.
-#include <hip/hip_runtime.h>
-
-#include <type_traits>
-
-#include "../../include/pollnet_amd.h"
-#include "device_common.hpp"
-#include "frame_pass.hpp"
-#include "pn_internal.hpp"
-
-namespace {
-
-using namespace pn_dev;
-using pn_internal::hip_err;
-using pn_internal::set_err;
-
-struct TArgs {
-  uint8_t* frames;
-  const uint16_t* lens; // setOptDataLen's len / update_udp_pkt's paylen per frame, or nullptr
-  uint32_t n;
-  uint32_t stride;
-  uint32_t ipa_off;  // (frame_off + 14) & ~15
-  uint32_t avail;    // stride - frame_off
-  uint32_t frame_off;
-  uint2* patch;      // n patch records (ctx scratch)
-  uint32_t fpw = kFramesPerWave; // frames per wave (8..64, frames_per_wave)
-};
-
-// Patch record: x = ip checksum | (tcp checksum or udp_len) << 16, y = tot_len word | flags << 16
-constexpr uint32_t kPatchOk = 1u << 16, kPatchLen = 2u << 16;
-
-__device__ __forceinline__ void st16(uint8_t* p, uint32_t v) { *reinterpret_cast<uint16_t*>(p) = (uint16_t)v; }
-
-// Where the field values go.  WB = -2 (production): the patch record.  Tuning variants
-// (scripts/tx_variants.py): WB = 0 2-byte stores straight into the frame; WB = 128 patch
-// the cooperative LDS tile and write back the slot's whole first line; WB = -1 nothing.
-constexpr int kWbPatch = -2;
-
-// MODE: PN_TX_TCP, PN_TX_UDP_EFVI or PN_TX_UDP.
-// PADK (tuning): KiB of LDS padding per workgroup (caps workgroups per CU, as the RX
-// kernel's 2-KiB pad does: 10 KiB = 4 waves/SIMD).
-template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false>
-__global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
-  const int lane = threadIdx.x;
-  const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * a.fpw;
-  if constexpr (PADK > 0) {
-    __shared__ uint32_t pad_lds[PADK * 256];
-    pad_lds[lane] = lane;
-    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
-  }
-  if (wave_base >= a.n) return;
-  const uint32_t f = wave_base + lane;
-  const uint32_t n_here = min(a.fpw, a.n - wave_base);
-  const bool live = (uint32_t)lane < n_here;
-  uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
-  const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
-
-  // LAUX0: the line-0 window loads keep the default policy (not nt), so the line the
-  // patch kernel later writes is still in the memory-side cache
-  Window h;
-  (void)load_window_strided<MIS, COOP, LAUX0>(rs, lane, a.stride, a.ipa_off, (uint32_t)(uintptr_t)wave_slot, h);
-  uint8_t* ip = wave_slot + (uint64_t)lane * a.stride + a.ipa_off + MIS;
-
-  // IpHeader (Core.h:57-69): tot_len at ip+2, checksum at ip+10
-  const uint32_t tot_word_old = h.template u16<MIS + 2>();
-  const uint32_t ip_chk_old = h.template u16<MIS + 10>();
-  uint32_t tot = bswap16(tot_word_old);
-  constexpr bool UDP = MODE != PN_TX_TCP;
-  constexpr uint32_t kHdr = UDP ? 28 : 40; // ip + udp / ip + tcp without options
-  const bool has_len = a.lens != nullptr;
-  uint32_t len = 0;
-  if (has_len && live) {
-    len = a.lens[f];
-    tot = (kHdr + len) & 0xffff; // htons(40 + len) (Core.h:158), htons(28 + paylen) (Efvi.h:615)
-  }
-  const bool ok = live && tot >= kHdr && 14 + tot <= a.avail;
-  const uint32_t tot_word = bswap16(tot);
-  const uint32_t s_ip_stored = h.template sum16<MIS, MIS + 20>(); // the 20 bytes as they are in memory
-  // the header's words with checksum 0 and the new tot_len (exact: both removed words are terms of s_ip_stored)
-  const uint32_t s_ip = s_ip_stored - ip_chk_old - tot_word_old + tot_word;
-
-  uint32_t ip_chk, l4; // l4: tcp checksum (TCP) or udp_len word (UDP)
-  if constexpr (UDP) {
-    if constexpr (MODE == PN_TX_UDP_EFVI) {
-      // Efvi: ipsum_cache over the header with tot_len = check = 0 (Efvi.h:405-411), then
-      // ipsum = cache + iplen; ipsum += ipsum >> 16; check = ~ipsum & 0xffff (Efvi.h:615-617)
-      uint32_t cache = s_ip - tot_word;
-      cache = (cache >> 16) + (cache & 0xffff);
-      cache += cache >> 16;
-      uint32_t ipsum = cache + tot_word;
-      ipsum += ipsum >> 16;
-      ip_chk = ~ipsum & 0xffff;
-    } else {
-      ip_chk = csum_fold(s_ip);
-    }
-    l4 = bswap16((8 + len) & 0xffff); // udp_len = htons(8 + paylen) (Efvi.h:618)
-  } else {
-    // summed extent [ip, ip + tot) rounded up to a whole word; bit 0 flags an odd tot_len,
-    // whose last word holds the byte after the segment (zero-padded in the sum: copyAndSum
-    // adds a trailing odd byte as the low byte of a word, TcpConn.h:291-295)
-    const uint32_t even_end = MIS + ((tot + 1) & ~1u);
-    const int end_rel = ok ? (int)(even_end | (tot & 1)) : 0;
-    uint32_t t_all = window_part<MIS>(h, end_rel & ~1, stream_start((uint64_t)(ip - MIS)));
-    uint32_t pad = kPadUnknown;
-    stream_phase<kExactRange, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
-    if (ok && (tot & 1) && pad == kPadUnknown) pad = ip[tot]; // pad byte inside the window
-    const uint32_t tcp_chk_old = h.template u16<MIS + 36>(); // TcpHeader.checksum at tcp+16 (Core.h:84)
-    const uint32_t s_seg = t_all - s_ip_stored - tcp_chk_old - ((tot & 1) ? (pad << 8) : 0u);
-    const uint32_t src_ip = h.template u32<MIS + 12>(), dst_ip = h.template u32<MIS + 16>();
-    const uint32_t s_addr = (src_ip >> 16) + (src_ip & 0xffff) + (dst_ip >> 16) + (dst_ip & 0xffff);
-    // pseudo-header: src, dst, ntohs(6), htons(20 + len) (TcpConn.h:165-167, Core.h:160)
-    l4 = csum_fold(s_addr + 0x0600 + bswap16(tot - 20) + s_seg);
-    ip_chk = csum_fold(s_ip);
-  }
-
-  if constexpr (WB == kWbPatch) {
-    if (live) {
-      const uint2 rec = {ip_chk | (l4 << 16), tot_word | (ok ? kPatchOk : 0u) | (has_len ? kPatchLen : 0u)};
-      a.patch[f] = rec; // one coalesced 512-B store per wave
-    }
-  } else if constexpr (WB == -3) { // timing only: a 16-B record per frame (RX's record size), plain store
-    if (live) reinterpret_cast<u32x4*>(a.patch)[f] = u32x4{ip_chk, l4, tot_word, f};
-  } else if constexpr (WB == -4) { // timing only: the 16-B record through RX's buffer store (sc1)
-    if (live) {
-      const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.patch + 2 * (f & ~63u)), 64 * 16);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4{ip_chk, l4, tot_word, f}, ro, (f & 63u) * 16, 0, kStoreAux);
-    }
-  } else {
-    constexpr int L4 = UDP ? 24 : 36;
-    constexpr bool kTile = COOP && WB > 0;
-    auto put = [&](auto o_tag, uint32_t v) {
-      constexpr int O = decltype(o_tag)::value;
-      if constexpr (WB < 0) {
-        if (v == 0xbeefu) st16(ip + O, v); // rarely (writes the right value): keeps the sums live
-      } else if constexpr (kTile) {
-        constexpr int L = 16 + MIS + O; // line offset of the field
-        uint16_t* row = reinterpret_cast<uint16_t*>(coop_tile() + lane * 8 + ((L >> 4) ^ (lane & 7)));
-        row[(L & 15) >> 1] = (uint16_t)v;
-      } else {
-        st16(ip + O, v);
-      }
-    };
-    if (ok) {
-      if (has_len) put(std::integral_constant<int, 2>{}, tot_word);
-      put(std::integral_constant<int, 10>{}, ip_chk);
-      if (!UDP || has_len) put(std::integral_constant<int, L4>{}, l4);
-    }
-    if constexpr (kTile) { // write the patched lines back, 8 lanes per 128-B line
-      __syncthreads();
-      u32x4* tile = coop_tile();
-      const uint32_t line0 = coop_block(a.ipa_off);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-        __builtin_amdgcn_raw_buffer_store_b128(tile[r * 8 + (part ^ (r & 7))], rs, r * a.stride + line0 + 16 * part, 0,
-                                               SAUX);
-      }
-    }
-  }
-}
-
-// Phase 2: one lane per frame writes the fields its patch record carries.
-template <int MODE>
-__global__ __launch_bounds__(256) void tx_patch_kernel(TArgs a) {
-  const uint32_t f = blockIdx.x * 256 + threadIdx.x;
-  if (f >= a.n) return;
-  const uint2 rec = a.patch[f];
-  if (!(rec.y & kPatchOk)) return;
-  uint8_t* ip = a.frames + (uint64_t)f * a.stride + a.frame_off + 14;
-  if (rec.y & kPatchLen) st16(ip + 2, rec.y);
-  st16(ip + 10, rec.x);
-  if constexpr (MODE == PN_TX_TCP) st16(ip + 36, rec.x >> 16);
-  else if (rec.y & kPatchLen) st16(ip + 24, rec.x >> 16);
-}
-
-bool coop_layout(const TArgs& a) {
-  return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
-}
-
-template <int MIS, int MODE>
-void launch(const TArgs& a, hipStream_t s) {
-  const dim3 grid((a.n + a.fpw - 1) / a.fpw), block(kWave);
-  // XCD-contiguous group order, as the RX kernel: -1.7 % (profiles/r01_experiments/tx_xcd_order_off{2,14}.json)
-  if (coop_layout(a)) {
-    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
-    return;
-  }
-  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
-}
-
-template <int MODE>
-void launch_mode(const TArgs& a, uint32_t mis, hipStream_t s) {
-  switch (mis) {
-    case 0: launch<0, MODE>(a, s); break;
-    case 2: launch<2, MODE>(a, s); break;
-    case 4: launch<4, MODE>(a, s); break;
-    case 6: launch<6, MODE>(a, s); break;
-    case 8: launch<8, MODE>(a, s); break;
-    case 10: launch<10, MODE>(a, s); break;
-    case 12: launch<12, MODE>(a, s); break;
-    default: launch<14, MODE>(a, s); break;
-  }
-  hipLaunchKernelGGL((tx_patch_kernel<MODE>), dim3((a.n + 255) / 256), dim3(256), 0, s, a);
-}
-
-int check_args(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, const uint16_t* lens) {
-  if (!frames) return set_err(ctx, PN_EINVAL, "pn_tx_fill: NULL frames");
-  if (((uintptr_t)frames & 15) || ((uintptr_t)lens & 1))
-    return set_err(ctx, PN_EINVAL, "pn_tx_fill: frames must be 16-byte, lens 2-byte aligned");
-  if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || slot_stride < frame_off + 96)
-    return set_err(ctx, PN_EINVAL, "pn_tx_fill: slot_stride/frame_off violate the layout contract");
-  return PN_OK;
-}
-
-// ctx-owned patch scratch, grown on demand.  A call on a different stream than the last
-// TX call first waits for that one (the scratch is reused).
-int ensure_patch(pn_ctx* ctx, uint32_t n, hipStream_t s) {
-  hipError_t e;
-  if (ctx->tx_patch && ctx->tx_stream != s) {
-    e = hipStreamSynchronize(ctx->tx_stream);
-    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(last tx_fill)");
-  }
-  if (n > ctx->tx_patch_n) {
-    if (ctx->tx_patch) {
-      e = hipStreamSynchronize(ctx->tx_stream);
-      if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(last tx_fill)");
-      (void)hipFree(ctx->tx_patch);
-      ctx->tx_patch = nullptr;
-      ctx->tx_patch_n = 0;
-    }
-    const uint32_t cap = n < (1u << 16) ? (1u << 16) : n;
-    e = hipMalloc(&ctx->tx_patch, (size_t)cap * sizeof(uint2));
-    if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(tx patch scratch)");
-    ctx->tx_patch_n = cap;
-  }
-  ctx->tx_stream = s;
-  return PN_OK;
-}
-
-} // namespace
+// TX checksum fill: the product entry point pn_tx_fill.  Kernels and
+// their design notes are in tx_fill.hpp; tuning variants in tx_tuning.hip (tuning library).
+#include "tx_fill.hpp"
 
 extern "C" int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                           const uint16_t* lens, uint32_t mode, void* stream) {
@@ -298,72 +30,6 @@ extern "C" int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint3
   else launch_mode<PN_TX_UDP>(a, mis, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "tx_fill launch");
-  ctx->last_stream = s;
-  return PN_OK;
-}
-
-// Tuning variants (TCP mode, cooperative layouts, no lens), A/B-timed by
-// scripts/tx_variants.py; not part of the public header.  History:
-// profiles/r01_experiments/tx_variants_*.json.
-extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
-                                  const uint16_t* lens, int variant, void* stream) {
-  if (!ctx || !frames || n == 0 || lens || (frame_off != 2 && frame_off != 14))
-    return set_err(ctx, PN_EINVAL, "tx variant: bad args");
-  TArgs a;
-  a.frames = (uint8_t*)frames;
-  a.lens = nullptr;
-  a.n = n;
-  a.stride = slot_stride;
-  a.ipa_off = (frame_off + 14) & ~15u;
-  a.avail = slot_stride - frame_off;
-  a.frame_off = frame_off;
-  // block write-back variants: the block is the slot's first line (every part loaded) inside the slot
-  if (!coop_layout(a) || a.stride < a.ipa_off + kWinBytes || (a.stride % 128) || (((uintptr_t)a.frames + a.ipa_off) & 127u) != 16)
-    return set_err(ctx, PN_EINVAL, "tx variant: needs the cooperative layout");
-  hipStream_t s = (hipStream_t)stream;
-  int rc = ensure_patch(ctx, variant >= 15 ? 2 * n : n, s); // 16-B record variants need 2 patch slots per frame
-  if (rc) return rc;
-  a.patch = (uint2*)ctx->tx_patch;
-  const dim3 grid((n + kFramesPerWave - 1) / kFramesPerWave), block(kWave), pgrid((n + 255) / 256), pblock(256);
-  auto go = [&](auto mis_tag) {
-    constexpr int M = decltype(mis_tag)::value;
-    constexpr int T = PN_TX_TCP;
-    switch (variant) {
-      case 0: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, kLoadAux>), grid, block, 0, s, a); return 0;     // in place, u16
-      case 2: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, kLoadAux>), grid, block, 0, s, a); return 0;  // in place, line wb
-      case 9: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -1, 0, kLoadAux>), grid, block, 0, s, a); return 0;    // no writes
-      case 10: // two-phase, line-0 window nt
-        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, kLoadAux>), grid, block, 0, s, a);
-        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
-        return 0;
-      case 11: // two-phase, blockIdx order (production before the XCD order)
-        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a);
-        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
-        return 0;
-      case 20: // two-phase, fill kernel at 4 waves/SIMD (2-KiB LDS pad)
-        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 2>), grid, block, 0, s, a);
-        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
-        return 0;
-      case 21: // two-phase, fill kernel in XCD-contiguous order
-        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
-        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
-        return 0;
-      case 13: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a); return 0; // phase 1 only
-      case 14: hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a); return 0;    // phase 2 only
-      case 15: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -3>), grid, block, 0, s, a); return 0;  // phase 1, 16-B records
-      case 16: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -4>), grid, block, 0, s, a); return 0;  // phase 1, RX-style store
-      // in place with the line-0 window at the default policy: the line is still in L2 when its
-      // fields are written, so the 2-byte stores (or the patched line) merge there
-      case 17: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, 0>), grid, block, 0, s, a); return 0;
-      case 18: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 0, 0>), grid, block, 0, s, a); return 0;
-      case 19: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, 0>), grid, block, 0, s, a); return 0;
-      default: return -1;
-    }
-  };
-  rc = frame_off == 2 ? go(std::integral_constant<int, 0>{}) : go(std::integral_constant<int, 12>{});
-  if (rc) return set_err(ctx, PN_EINVAL, "tx variant: unknown");
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return hip_err(ctx, e, "tx variant launch");
   ctx->last_stream = s;
   return PN_OK;
 }

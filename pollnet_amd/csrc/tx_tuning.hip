@@ -1,0 +1,72 @@
+// Tuning library: A/B variants of the TX fill (scripts/tx_variants.py), compiled only with
+// `make TUNING=1`.  Never part of the product library.
+#include "tx_fill.hpp"
+
+#ifdef PN_TUNING_VARIANTS
+
+// Tuning variants (TCP mode, cooperative layouts, no lens), A/B-timed by
+// scripts/tx_variants.py; not part of the public header.  History:
+// profiles/r01_experiments/tx_variants_*.json.
+extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                                  const uint16_t* lens, int variant, void* stream) {
+  if (!ctx || !frames || n == 0 || lens || (frame_off != 2 && frame_off != 14))
+    return set_err(ctx, PN_EINVAL, "tx variant: bad args");
+  TArgs a;
+  a.frames = (uint8_t*)frames;
+  a.lens = nullptr;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.avail = slot_stride - frame_off;
+  a.frame_off = frame_off;
+  // block write-back variants: the block is the slot's first line (every part loaded) inside the slot
+  if (!coop_layout(a) || a.stride < a.ipa_off + kWinBytes || (a.stride % 128) || (((uintptr_t)a.frames + a.ipa_off) & 127u) != 16)
+    return set_err(ctx, PN_EINVAL, "tx variant: needs the cooperative layout");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_patch(ctx, variant >= 15 ? 2 * n : n, s); // 16-B record variants need 2 patch slots per frame
+  if (rc) return rc;
+  a.patch = (uint2*)ctx->tx_patch;
+  const dim3 grid((n + kFramesPerWave - 1) / kFramesPerWave), block(kWave), pgrid((n + 255) / 256), pblock(256);
+  auto go = [&](auto mis_tag) {
+    constexpr int M = decltype(mis_tag)::value;
+    constexpr int T = PN_TX_TCP;
+    switch (variant) {
+      case 0: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, kLoadAux>), grid, block, 0, s, a); return 0;     // in place, u16
+      case 2: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, kLoadAux>), grid, block, 0, s, a); return 0;  // in place, line wb
+      case 9: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -1, 0, kLoadAux>), grid, block, 0, s, a); return 0;    // no writes
+      case 10: // two-phase, line-0 window nt
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, kLoadAux>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
+        return 0;
+      case 11: // two-phase, blockIdx order (production before the XCD order)
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
+        return 0;
+      case 20: // two-phase, fill kernel at 4 waves/SIMD (2-KiB LDS pad)
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 2>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
+        return 0;
+      case 21: // two-phase, fill kernel in XCD-contiguous order
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
+        return 0;
+      case 13: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a); return 0; // phase 1 only
+      case 14: hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a); return 0;    // phase 2 only
+      case 15: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -3>), grid, block, 0, s, a); return 0;  // phase 1, 16-B records
+      case 16: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -4>), grid, block, 0, s, a); return 0;  // phase 1, RX-style store
+      // in place with the line-0 window at the default policy: the line is still in L2 when its
+      // fields are written, so the 2-byte stores (or the patched line) merge there
+      case 17: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, 0>), grid, block, 0, s, a); return 0;
+      case 18: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 0, 0>), grid, block, 0, s, a); return 0;
+      case 19: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, 0>), grid, block, 0, s, a); return 0;
+      default: return -1;
+    }
+  };
+  rc = frame_off == 2 ? go(std::integral_constant<int, 0>{}) : go(std::integral_constant<int, 12>{});
+  if (rc) return set_err(ctx, PN_EINVAL, "tx variant: unknown");
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "tx variant launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+#endif // PN_TUNING_VARIANTS

@@ -112,14 +112,8 @@ _pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
 _pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_classify_indexed = _sig("pn_classify_indexed", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_tx_fill = _sig("pn_tx_fill", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp)
-_pn_tx_variant = _sig("pn_tx_fill_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _i32, _vp)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
-_pn_calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
-_pn_calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
-_pn_calib_slot_var = _sig("pn_calib_slot_read_var", _i32, _vp, _vp, _u32, _u32, _vp, _i32, _vp, _vp)
-_pn_idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
-_pn_variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
 _pn_gen_conn_table = _sig("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)
 _pn_wire_bytes = _sig("pn_wire_bytes", _u64, _vp, _u32, _u32, _u32)
@@ -275,11 +269,6 @@ class RxContext:
         _check(_pn_tx_fill(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), mode,
                            _stream_handle(stream)), self._h, "pn_tx_fill")
 
-    def tx_fill_variant(self, frames_dev, slot_stride, frame_off, n, lens, variant, stream=None):
-        """Tuning-only TX fill shapes (scripts/tx_variants.py); not part of the C header."""
-        _check(_pn_tx_variant(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), variant,
-                              _stream_handle(stream)), self._h, "pn_tx_fill_variant")
-
     def match_streams(self, frames, slot_stride: int, frame_off: int, n: int, filters: np.ndarray, stream_ids,
                       stream=None):
         """pn_match_streams: stream_ids[i] (u32, device or pinned memory) = the first filter
@@ -288,29 +277,8 @@ class RxContext:
         _check(_pn_match_streams(self._h, _ptr(frames), slot_stride, frame_off, n, flt.ctypes.data, len(flt),
                                  _ptr(stream_ids), _stream_handle(stream)), self._h, "pn_match_streams")
 
-    def classify_indexed_variant(self, base, offsets, eth_mod16, n, avail, results, stream, variant):
-        """Tuning-only indexed kernel shapes (scripts/bench_indexed.py); not part of the C header."""
-        _check(_pn_idx_variant(self._h, _ptr(base), _ptr(offsets), eth_mod16, n, avail, _ptr(results),
-                               _stream_handle(stream), variant), self._h, "pn_classify_indexed_variant")
-
-    def calib_slot_read(self, src_dev, n_slots, stride, nbytes, sink_dev, stream=None, store_bytes=0):
-        _check(_pn_calib_slot(self._h, _ptr(src_dev), n_slots, stride, nbytes, store_bytes, _ptr(sink_dev),
-                              _stream_handle(stream)), self._h, "pn_calib_slot_read")
-
-    def calib_slot_read_var(self, src_dev, n_slots, stride, lens_dev, sink_dev, stream=None, store_bytes=0):
-        _check(_pn_calib_slot_var(self._h, _ptr(src_dev), n_slots, stride, _ptr(lens_dev), store_bytes,
-                                  _ptr(sink_dev), _stream_handle(stream)), self._h, "pn_calib_slot_read_var")
-
-    def classify_variant(self, frames_dev, slot_stride, frame_off, n, results_dev, stream, variant):
-        """Tuning-only kernel shapes (scripts/variants.py); not part of the C header."""
-        _check(_pn_variant(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(results_dev),
-                           _stream_handle(stream), variant), self._h, "pn_classify_variant")
-
     def sync(self):
         _check(_pn_sync(self._h), self._h, "pn_sync")
-
-    def calib_stream_read(self, src_dev, nbytes: int, sink_dev, stream=None):
-        _check(_pn_calib(self._h, _ptr(src_dev), nbytes, _ptr(sink_dev), _stream_handle(stream)), self._h, "pn_calib")
 
 
 @dataclass

@@ -24,6 +24,7 @@ def main():
     import torch
 
     import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
 
     n, stride, off = a.frames, 2048, 2
     p = pa.rx.GenParams.for_config(a.config)
@@ -57,16 +58,16 @@ def main():
     poffs = torch.from_numpy(starts.astype(np.uint64).view(np.int64)).cuda()
     runs = {
         "indexed_packed": lambda: ctx.classify_indexed(packed_dev, poffs, off, n, stride - off, out, st),
-        "indexed_packed_all_default": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 3),
-        "indexed_packed_blockidx_order": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 2),
-        "indexed_permuted_blockidx_order": lambda: ctx.classify_indexed_variant(frames, perm, off, n, stride - off, out, st, 2),
+        "indexed_packed_all_default": lambda: tn.classify_indexed_variant(ctx, packed_dev, poffs, off, n, stride - off, out, st, 3),
+        "indexed_packed_blockidx_order": lambda: tn.classify_indexed_variant(ctx, packed_dev, poffs, off, n, stride - off, out, st, 2),
+        "indexed_permuted_blockidx_order": lambda: tn.classify_indexed_variant(ctx, frames, perm, off, n, stride - off, out, st, 2),
         "strided": lambda: ctx.classify(frames, stride, off, n, out, st),
         "indexed_in_order": lambda: ctx.classify_indexed(frames, ident, off, n, stride - off, out, st),
         "indexed_permuted": lambda: ctx.classify_indexed(frames, perm, off, n, stride - off, out, st),
-        "indexed_in_order_perlane": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 0),
-        "indexed_in_order_coop_win_nt": lambda: ctx.classify_indexed_variant(frames, ident, off, n, stride - off, out, st, 1),
-        "indexed_permuted_coop_win_nt": lambda: ctx.classify_indexed_variant(frames, perm, off, n, stride - off, out, st, 1),
-        "indexed_packed_win_nt": lambda: ctx.classify_indexed_variant(packed_dev, poffs, off, n, stride - off, out, st, 1),
+        "indexed_in_order_perlane": lambda: tn.classify_indexed_variant(ctx, frames, ident, off, n, stride - off, out, st, 0),
+        "indexed_in_order_coop_win_nt": lambda: tn.classify_indexed_variant(ctx, frames, ident, off, n, stride - off, out, st, 1),
+        "indexed_permuted_coop_win_nt": lambda: tn.classify_indexed_variant(ctx, frames, perm, off, n, stride - off, out, st, 1),
+        "indexed_packed_win_nt": lambda: tn.classify_indexed_variant(ctx, packed_dev, poffs, off, n, stride - off, out, st, 1),
     }
     for name, f in runs.items():  # parity first
         f()

@@ -18,6 +18,7 @@ def main():
     import torch
 
     import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
     from streams_np import match_streams_np
 
     n, off = 1 << 20, 2
@@ -56,7 +57,7 @@ def main():
             for _ in range(5):
                 ev[0].record(st)
                 for r in range(20):
-                    ctx.calib_slot_read(dev[r % 4], n, 2048, nb, sink, st, 0)
+                    tn.calib_slot_read(ctx, dev[r % 4], n, 2048, nb, sink, st, 0)
                 ev[1].record(st)
                 torch.cuda.synchronize()
                 cs.append(ev[0].elapsed_time(ev[1]) / 20)

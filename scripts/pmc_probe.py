@@ -24,6 +24,7 @@ def main():
     import torch
 
     import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
 
     p = pa.rx.GenParams.for_config(a.config)
     s = pa.gen_frames(p, a.frames)
@@ -35,11 +36,11 @@ def main():
     sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
     for _ in range(a.reps):
-        ctx.calib_stream_read(frames, frames.numel(), sink, st)
+        tn.calib_stream_read(ctx, frames, frames.numel(), sink, st)
         if a.variant < 0:
             ctx.classify(frames, 2048, 2, a.frames, res, st)
         else:
-            ctx.classify_variant(frames, 2048, 2, a.frames, res, st, a.variant)
+            tn.classify_variant(ctx, frames, 2048, 2, a.frames, res, st, a.variant)
     torch.cuda.synchronize()
     print(f"calib_bytes={frames.numel()} wire_bytes={pa.wire_bytes(s, 2048, 2, a.frames)} frames={a.frames}")
 

@@ -31,6 +31,7 @@ def main():
     import torch
 
     import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
 
     n, off = a.frames, a.frame_off
     p = pa.rx.GenParams.for_config(2)
@@ -51,8 +52,8 @@ def main():
     for var in vs:
         work.copy_(base)
         if var == 14:
-            ctx.tx_fill_variant(work, 2048, off, n, None, 13, st)  # phase 2 needs phase 1's records
-        ctx.tx_fill_variant(work, 2048, off, n, arg(var), var, st)
+            tn.tx_fill_variant(ctx, work, 2048, off, n, None, 13, st)  # phase 2 needs phase 1's records
+        tn.tx_fill_variant(ctx, work, 2048, off, n, arg(var), var, st)
         torch.cuda.synchronize()
         if var not in TIMING_ONLY or var == 14:
             assert torch.equal(work, ref), f"variant {var} differs from production"
@@ -76,10 +77,10 @@ def main():
         times["prod"].append(timed(lambda: ctx.tx_fill(work, 2048, off, n, None, pa.PN_TX_TCP, st)))
         times["rx_classify"].append(timed(lambda: ctx.classify(work, 2048, off, n, res, st)))
         if off == 2:
-            times["slotread_1536"].append(timed(lambda: ctx.calib_slot_read(work, n, 2048, 1536, sink, st, 0)))
-            times["slotread_1536_store16"].append(timed(lambda: ctx.calib_slot_read(work, n, 2048, 1536, res, st, 16)))
+            times["slotread_1536"].append(timed(lambda: tn.calib_slot_read(ctx, work, n, 2048, 1536, sink, st, 0)))
+            times["slotread_1536_store16"].append(timed(lambda: tn.calib_slot_read(ctx, work, n, 2048, 1536, res, st, 16)))
         for var in vs:
-            times[var].append(timed(lambda: ctx.tx_fill_variant(work, 2048, off, n, arg(var), var, st)))
+            times[var].append(timed(lambda: tn.tx_fill_variant(ctx, work, 2048, off, n, arg(var), var, st)))
     algo = 1504 * n
     out = {"frames": n, "frame_off": off, "algo_bytes_per_frame": 1504}
     for k, ts in times.items():

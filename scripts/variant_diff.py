@@ -5,6 +5,7 @@ import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import pollnet_amd as pa
+from pollnet_amd import tuning as tn
 cfg, v, n = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
 p = pa.rx.GenParams.for_config(cfg)
 s = pa.gen_frames(p, n)
@@ -16,7 +17,7 @@ ref = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
 res = torch.zeros_like(ref)
 st = torch.cuda.current_stream()
 ctx.classify(fr, 2048, 2, n, ref, st)
-ctx.classify_variant(fr, 2048, 2, n, res, st, v)
+tn.classify_variant(ctx, fr, 2048, 2, n, res, st, v)
 torch.cuda.synchronize()
 a = ref.cpu().numpy().view(np.uint32).reshape(-1, 4)
 b = res.cpu().numpy().view(np.uint32).reshape(-1, 4)

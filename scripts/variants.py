@@ -34,6 +34,7 @@ def main():
     import torch
 
     import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
 
     p = pa.rx.GenParams.for_config(a.config)
     s = pa.gen_frames(p, a.frames, 2048, a.frame_off)
@@ -68,7 +69,7 @@ def main():
     vs = [int(x) for x in a.variants.split(",")]
     for v in vs:
         res.zero_()
-        ctx.classify_variant(frames, 2048, a.frame_off, a.frames, res, st, v)
+        tn.classify_variant(ctx, frames, 2048, a.frame_off, a.frames, res, st, v)
         torch.cuda.synchronize()
         if v not in TIMING_ONLY:
             assert torch.equal(res, ref), f"variant {v} differs from production"
@@ -92,17 +93,17 @@ def main():
         return ev[0].elapsed_time(ev[1]) / a.reps
 
     for _ in range(a.rounds):
-        times["calib"].append(timed(lambda: ctx.calib_stream_read(frames, frames.numel(), sink, st)))
+        times["calib"].append(timed(lambda: tn.calib_stream_read(ctx, frames, frames.numel(), sink, st)))
         for b, wpg in SLOT_MODES:
             tgt = res if wpg else sink
-            times[f"slotread_{b}_store{wpg}"].append(timed(lambda: ctx.calib_slot_read(frames, a.frames, 2048, b, tgt, st, wpg)))
+            times[f"slotread_{b}_store{wpg}"].append(timed(lambda: tn.calib_slot_read(ctx, frames, a.frames, 2048, b, tgt, st, wpg)))
         times["prod"].append(timed(lambda: ctx.classify(frames, 2048, a.frame_off, a.frames, res, st)))
         r0 = a.reps
         a.reps = 50
         times["prod_b2b50"].append(timed(lambda: ctx.classify(frames, 2048, a.frame_off, a.frames, res, st)))
         a.reps = r0
         for v in vs:
-            times[v].append(timed(lambda: ctx.classify_variant(frames, 2048, a.frame_off, a.frames, res, st, v)))
+            times[v].append(timed(lambda: tn.classify_variant(ctx, frames, 2048, a.frame_off, a.frames, res, st, v)))
     algo = wire + 16 * a.frames
     out = {"config": a.config, "frames": a.frames,
            "calib_stream_read_tbps": round(frames.numel() / (statistics.median(times["calib"]) * 1e-3) / 1e12, 3)}

@@ -16,6 +16,7 @@ def main():
     import torch
 
     import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
 
     n = 1 << 20
     p = pa.rx.GenParams.for_config(2)
@@ -32,10 +33,10 @@ def main():
     for _ in range(12):
         for k, m in modes.items():
             for b in batches[:2]:
-                ctx.calib_slot_read(b, n, 2048, 1536, sink, st, m)
+                tn.calib_slot_read(ctx, b, n, 2048, 1536, sink, st, m)
             ev[0].record(st)
             for r in range(8):
-                ctx.calib_slot_read(batches[r % 4], n, 2048, 1536, sink, st, m)
+                tn.calib_slot_read(ctx, batches[r % 4], n, 2048, 1536, sink, st, m)
             ev[1].record(st)
             torch.cuda.synchronize()
             times[k].append(ev[0].elapsed_time(ev[1]) / 8)

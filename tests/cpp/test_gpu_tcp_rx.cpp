@@ -88,6 +88,7 @@ struct Handler {
   }
   void onTimeWaitSegment(uint64_t key, uint32_t tw_id, const uint8_t*, const pn_result& r) {
     log.push_back({5, key, tw_id, r.flags, rec_hash(r)});
+    if (r.flags & PN_F_RST) srv->removeTW(tw_id); // in-sequence RST ends TIME_WAIT (Core.h:513-517)
   }
 };
 
@@ -127,11 +128,27 @@ struct Twin {
       free_.push_back(c.id);
     }
   }
-  int enterTW(Conn& c, uint32_t tw_id) {
+  std::vector<uint32_t> free_tw = [] {
+    std::vector<uint32_t> v;
+    for (uint32_t i = Conf::MaxTimeWaitConnCnt; i-- > 0;) v.push_back(i);
+    return v;
+  }();
+  std::vector<uint64_t> tw_keys = std::vector<uint64_t>(Conf::MaxTimeWaitConnCnt, PN_EMPTY_KEY);
+  int removeTW(uint32_t tw_id) {
+    if (table.del(tw_keys[tw_id]) != PN_OK) return PN_ENOENT;
+    tw_keys[tw_id] = PN_EMPTY_KEY;
+    free_tw.push_back(tw_id);
+    return PN_OK;
+  }
+  int enterTW(Conn& c) {
+    const uint32_t tw_id = free_tw.back();
     const int rc = table.enterTW(c.key, tw_id);
     if (rc == PN_OK) {
+      free_tw.pop_back();
+      tw_keys[tw_id] = c.key;
       c.live = false;
       free_.push_back(c.id);
+      return (int)tw_id;
     }
     return rc;
   }
@@ -240,13 +257,15 @@ int main(int argc, char** argv) {
       }
       per[f].push_back(mk((uint32_t)F.stream.size(), (uint32_t)F.stream.size(), ACK | FIN));
       per[f].push_back(mk((uint32_t)F.stream.size() + 1, (uint32_t)F.stream.size() + 1, ACK)); // after close: unknown
-    } else { // TIME_WAIT flows (n_tw) and unknown flows: a few ACK-only segments each
+    } else { // TIME_WAIT flows (n_tw) and unknown flows: a few ACK-only segments each; every
+      // other TIME_WAIT flow ends it with an RST and reconnects with a SYN (delete-then-SYN)
+      const bool reconnect = f < n_flows + n_tw && f % 2 == 0;
       for (int k = 0; k < 3; k++) {
         Seg s;
         s.src_ip = F.ip;
         s.src_port = F.port;
         s.seq = F.isn + k;
-        s.flags = ACK;
+        s.flags = reconnect && k == 1 ? RST : reconnect && k == 2 ? SYN : ACK;
         per[f].push_back(s);
       }
     }
@@ -291,7 +310,7 @@ int main(int argc, char** argv) {
     for (uint32_t t = 0; t < n_tw; t++) { // pre-existing TIME_WAIT entries
       const Flow& F = flows[n_flows + t];
       auto* c = srv.accept(pn_conn_hash_key(htonl(F.ip), htons(F.port)), F.isn);
-      if (!c || srv.enterTW(*c, t) != PN_OK) return false;
+      if (!c || srv.enterTW(*c) != (int)t) return false;
     }
     const uint32_t step = span ? n : batch;
     for (uint32_t b = 0; b < n; b += step) {
@@ -353,6 +372,8 @@ int main(int argc, char** argv) {
     std::printf("FAIL: %u/%u flows delivered their stream\n", streams_ok, n_flows);
     fail++;
   }
+  uint32_t n_reconnect = 0; // TIME_WAIT flows with an even flow index: RST then SYN
+  for (uint32_t f = n_flows; f < n_flows + n_tw; f++) n_reconnect += f % 2 == 0;
   size_t cnt[6] = {};
   for (auto& e : glog) cnt[e.type]++;
   std::printf("%s%s: ", indexed ? "indexed zero-copy" : zero_copy ? "zero-copy" : "copy",
@@ -361,12 +382,14 @@ int main(int argc, char** argv) {
               "%u/%u streams (%u B) intact; conns left %u\n",
               n, batch, glog.size(), cnt[1], cnt[2], cnt[3], cnt[4], cnt[5], streams_ok, n_flows, bytes,
               gpu->getConnCnt());
-  if (gpu->getConnCnt() != 0) {
-    std::printf("FAIL: connections left open\n");
+  std::printf("TIME_WAIT: %u ended by RST and reconnected by SYN, %u left\n", n_reconnect, gpu->getTimeWaitCnt());
+  if (gpu->getConnCnt() != n_reconnect || gpu->getTimeWaitCnt() != n_tw - n_reconnect) {
+    std::printf("FAIL: expected %u reconnected flows open and %u TIME_WAIT entries, have %u / %u\n", n_reconnect,
+                n_tw - n_reconnect, gpu->getConnCnt(), gpu->getTimeWaitCnt());
     fail++;
   }
-  if (cnt[2] != n_flows || cnt[5] != 3 * n_tw) {
-    std::printf("FAIL: expected %u disconnects and %u time-wait segments\n", n_flows, 3 * n_tw);
+  if (cnt[2] != n_flows || cnt[5] != 3 * n_tw - n_reconnect) {
+    std::printf("FAIL: expected %u disconnects and %u time-wait segments\n", n_flows, 3 * n_tw - n_reconnect);
     fail++;
   }
   std::printf("%s\n", fail ? "FAIL" : "PASS");

@@ -3,6 +3,7 @@ host-side (no GPU) behaviour of the boundary."""
 import ctypes
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -12,10 +13,15 @@ import pollnet_amd as pa
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
-    src = open(os.path.join(ROOT, "include", "pollnet_amd.h")).read()
+def declared_functions(header="pollnet_amd.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(pn_[a-z0-9_]+)\s*\(", src)))
+
+
+def exported_functions(lib_path):
+    out = subprocess.run(["nm", "-D", "--defined-only", lib_path], capture_output=True, text=True, check=True).stdout
+    return sorted({ln.split()[-1] for ln in out.splitlines() if " T " in ln and ln.split()[-1].startswith("pn_")})
 
 
 def test_header_declares_and_library_exports_all():
@@ -24,6 +30,23 @@ def test_header_declares_and_library_exports_all():
     lib = ctypes.CDLL(pa.LIB_PATH)
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_product_exports_exactly_the_header():
+    """The product library exports the C-ABI of include/pollnet_amd.h and nothing else:
+    tuning variants and bandwidth ceilings live in libpollnet_amd_tuning.so."""
+    assert exported_functions(pa.LIB_PATH) == declared_functions()
+
+
+def test_tuning_library_is_separate():
+    from pollnet_amd import tuning
+
+    tuned = set(exported_functions(tuning.LIB_PATH))
+    declared = set(declared_functions("pollnet_amd_tuning.h"))
+    assert {"pn_calib_stream_read", "pn_calib_slot_read", "pn_calib_slot_read_var"} <= tuned <= declared
+    assert not tuned & set(declared_functions())
+    src = open(os.path.join(ROOT, "pollnet_amd", "rx.py")).read() + open(os.path.join(ROOT, "pollnet_amd", "__init__.py")).read()
+    assert "tuning" not in src  # the product package never loads the tuning library
 
 
 def test_result_layout():

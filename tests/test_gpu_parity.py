@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import pollnet_amd as pa
+from pollnet_amd import tuning as tn
 from oracle import pyoracle as orc
 
 from frames import FRAME_OFF, STRIDE, make_frame, to_slots
@@ -365,13 +366,13 @@ def test_calib_slot_read_var(torch_cuda, ctx):
     frames = torch_cuda.randint(0, 256, (n * stride,), dtype=torch_cuda.uint8, device="cuda")
     lens = torch_cuda.randint(64, 1600, (n,), dtype=torch_cuda.int32, device="cuda")
     sink = torch_cuda.full(((n + 64) * 16,), 0xAB, dtype=torch_cuda.uint8, device="cuda")
-    ctx.calib_slot_read_var(frames, n, stride, lens, sink, torch_cuda.cuda.current_stream(), 16)
+    tn.calib_slot_read_var(ctx, frames, n, stride, lens, sink, torch_cuda.cuda.current_stream(), 16)
     torch_cuda.cuda.synchronize()
     out = sink.cpu().numpy()
     assert (out[n * 16:] == 0xAB).all()
     recs = out[: n * 16].view("<u4").reshape(n, 4)
     assert (recs[:, 1] == recs[:, 0] ^ 1).all() and (recs[:, 3] == recs[:, 0] ^ 3).all()
     with pytest.raises(pa.PollnetError, match="bad arguments"):
-        ctx.calib_slot_read_var(frames, n, 100, lens, sink, None, 16)
+        tn.calib_slot_read_var(ctx, frames, n, 100, lens, sink, None, 16)
     with pytest.raises(pa.PollnetError, match="bad arguments"):
-        ctx.calib_slot_read_var(frames, n, stride, lens, sink, None, 8)
+        tn.calib_slot_read_var(ctx, frames, n, stride, lens, sink, None, 8)
