@@ -195,17 +195,72 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
 }
 
 // Phase 2: one lane per frame writes the fields its patch record carries.
-template <int MODE>
+// PV (tuning, scripts/tx_variants.py): 0 plain 2-byte stores (production); 1 the same with
+// the nt policy.  (Global stores: a per-lane buffer descriptor would be waterfalled.)
+template <int MODE, int PV = 0>
 __global__ __launch_bounds__(256) void tx_patch_kernel(TArgs a) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
   if (f >= a.n) return;
   const uint2 rec = a.patch[f];
   if (!(rec.y & kPatchOk)) return;
   uint8_t* ip = a.frames + (uint64_t)f * a.stride + a.frame_off + 14;
-  if (rec.y & kPatchLen) st16(ip + 2, rec.y);
-  st16(ip + 10, rec.x);
-  if constexpr (MODE == PN_TX_TCP) st16(ip + 36, rec.x >> 16);
-  else if (rec.y & kPatchLen) st16(ip + 24, rec.x >> 16);
+  if constexpr (PV == 0) {
+    if (rec.y & kPatchLen) st16(ip + 2, rec.y);
+    st16(ip + 10, rec.x);
+    if constexpr (MODE == PN_TX_TCP) st16(ip + 36, rec.x >> 16);
+    else if (rec.y & kPatchLen) st16(ip + 24, rec.x >> 16);
+  } else { // nt 2-byte stores (PV == 1)
+    if (rec.y & kPatchLen) __builtin_nontemporal_store((uint16_t)rec.y, reinterpret_cast<uint16_t*>(ip + 2));
+    __builtin_nontemporal_store((uint16_t)rec.x, reinterpret_cast<uint16_t*>(ip + 10));
+    if constexpr (MODE == PN_TX_TCP) __builtin_nontemporal_store((uint16_t)(rec.x >> 16), reinterpret_cast<uint16_t*>(ip + 36));
+    else if (rec.y & kPatchLen) __builtin_nontemporal_store((uint16_t)(rec.x >> 16), reinterpret_cast<uint16_t*>(ip + 24));
+  }
+}
+
+// Timing-only probe (tuning): each frame's first B bytes of the 64-B-aligned region holding
+// ip+10 written in full (B/16 lanes per frame, 16 B each), no read, garbage values.
+template <int B>
+__global__ __launch_bounds__(256) void tx_probe_fullwrite_kernel(TArgs a) {
+  constexpr int L = B / 16;
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t f = t / L, part = t % L;
+  if (f >= a.n) return;
+  const uint64_t ip = (uint64_t)(a.frames + (uint64_t)f * a.stride + a.frame_off + 14);
+  const uint64_t q = ((ip + 10) & ~(uint64_t)(B - 1)) + 16 * part;
+  *reinterpret_cast<u32x4*>(q) = u32x4{f, part, 0u, 0u};
+}
+
+// Phase 2, whole-sector form (tuning): 8 lanes per frame rewrite each 64-B sector that holds
+// a field (the sector read back, the fields patched in registers, 16 B per lane), so the
+// memory sees full-sector writes instead of 2-byte masked ones.  Valid only where those
+// sectors lie inside the frame's own slot and nothing else writes them meanwhile.
+// SAUX: store policy (0 plain, 2 nt).
+template <int SAUX>
+__global__ __launch_bounds__(256) void tx_patch_sector_kernel(TArgs a) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t f = t >> 3, part = t & 7;
+  if (f >= a.n) return;
+  const uint2 rec = a.patch[f];
+  if (!(rec.y & kPatchOk)) return;
+  uint8_t* slot = a.frames + (uint64_t)f * a.stride;
+  const uint64_t ip = (uint64_t)(slot + a.frame_off + 14);
+  const uint64_t sa = (ip + 10) & ~63ull, sb = (ip + 36) & ~63ull; // sectors of the two checksum fields
+  const uint64_t sec = part < 4 ? sa : sb;
+  if (part >= 4 && sb == sa) return;
+  const uint64_t q = sec + 16 * (part & 3);
+  u32x4 v = *reinterpret_cast<const u32x4*>(q);
+  auto patch16 = [&](uint64_t at, uint32_t val) { // a 2-byte field at address `at`, if inside this quad
+    if (at >= q && at < q + 16) {
+      const uint32_t o = (uint32_t)(at - q), w = o >> 2, sh = (o & 2) * 8;
+      uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+      d[w] = (d[w] & ~(0xffffu << sh)) | ((val & 0xffffu) << sh);
+    }
+  };
+  if (rec.y & kPatchLen) patch16(ip + 2, rec.y);
+  patch16(ip + 10, rec.x);
+  patch16(ip + 36, rec.x >> 16);
+  if constexpr (SAUX == 2) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(q));
+  else *reinterpret_cast<u32x4*>(q) = v;
 }
 
 inline bool coop_layout(const TArgs& a) {

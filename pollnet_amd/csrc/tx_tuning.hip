@@ -50,6 +50,16 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a);
         return 0;
+      // phase-2 store forms after the production phase 1 (line-0 window default policy, XCD order)
+      case 30: case 32: case 33:
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
+        if (variant == 30) hipLaunchKernelGGL((tx_patch_kernel<T, 1>), pgrid, pblock, 0, s, a);      // 2-byte nt
+        else if (variant == 32) hipLaunchKernelGGL((tx_patch_sector_kernel<0>), dim3((8 * n + 255) / 256), pblock, 0, s, a);
+        else if (variant == 33) hipLaunchKernelGGL((tx_patch_sector_kernel<2>), dim3((8 * n + 255) / 256), pblock, 0, s, a);
+        else return -1;
+        return 0;
+      case 35: hipLaunchKernelGGL((tx_probe_fullwrite_kernel<64>), dim3((4 * n + 255) / 256), pblock, 0, s, a); return 0;
+      case 36: hipLaunchKernelGGL((tx_probe_fullwrite_kernel<128>), dim3((8 * n + 255) / 256), pblock, 0, s, a); return 0;
       case 13: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T>), grid, block, 0, s, a); return 0; // phase 1 only
       case 14: hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, a); return 0;    // phase 2 only
       case 15: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, -3>), grid, block, 0, s, a); return 0;  // phase 1, 16-B records
