@@ -85,3 +85,66 @@ def test_shard_ranges():
     assert spans[0][0] == 0 and spans[-1][1] == 10 and all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
     with pytest.raises(ValueError):
         shard_range(4, 4, 10)
+
+
+def _gpu_worker(rank, world, port, n_per_rank, out_dir):
+    """One rank on the box's GPU: its contiguous C4 shard through pn_classify (the C-ABI)."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import torch
+
+    import pollnet_amd as pa
+    from pollnet_amd.shard import shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(rank % torch.cuda.device_count())
+    p = pa.rx.GenParams.for_config(4)
+    lo, hi = shard_range(rank, world, n_per_rank)
+    slots = pa.gen_frames(p, hi - lo, first_index=lo, threads=4)
+    ctx = pa.RxContext(torch.cuda.current_device())
+    ctx.set_conn_table(pa.gen_conn_table(p))
+    frames = torch.from_numpy(slots.reshape(-1)).cuda()
+    res = torch.empty((hi - lo) * 16, dtype=torch.uint8, device="cuda")
+    dist.barrier()
+    ctx.classify(frames, 2048, 2, hi - lo, res, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    dist.barrier()
+    np.save(os.path.join(out_dir, f"gpu_rank{rank}.npy"), res.cpu().numpy())
+    ctx.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_two_rank_shards_equal_c4_digest(tmp_path, golden_dir):
+    """Two gloo ranks share the box's GPU, each classifying its contiguous half of the C4
+    shard (2 Mi frames) through pn_classify; the concatenated records hash to the committed
+    single-process C4 digest (made by the oracle)."""
+    import json
+
+    with open(os.path.join(golden_dir, "full_digests.json")) as f:
+        ref = json.load(f)["c4"]
+    world = 2
+    mp.spawn(_gpu_worker, args=(world, _free_port(), ref["n"] // world, str(tmp_path)), nprocs=world, join=True)
+    got = np.concatenate([np.load(tmp_path / f"gpu_rank{r}.npy") for r in range(world)])
+    assert hashlib.sha256(got.tobytes()).hexdigest() == ref["records_sha256"]
+
+
+@pytest.mark.gpu
+def test_bench_spawns_ranks_itself():
+    """`bench.py --gpus 2` without torchrun starts its 2 ranks (spawn) and reports n_gpus 2;
+    on a 1-GPU box the ranks share the device (a rehearsal of the N>1 flow)."""
+    import json
+    import subprocess
+    import sys
+
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--frames", "65536", "--batches", "2", "--no-cpu-baseline", "--no-e2e", "--no-secondary"],
+                       capture_output=True, text=True, timeout=240, env={k: v for k, v in os.environ.items()
+                                                                        if k not in ("WORLD_SIZE", "RANK")})
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
+    assert line["config"]["global_frames"] == 2 * 65536
