@@ -98,6 +98,15 @@ typedef struct pn_conn_table pn_conn_table;
 uint64_t pn_conn_hash_key(uint32_t ip_be, uint16_t port_be);
 
 int pn_table_create(uint32_t max_conn_cnt, uint32_t max_tw_cnt, pn_conn_table** out);
+/* The same with flags:
+ *   PN_TABLE_REFERENCE_LITERAL  run Core::tryExpandConnTbl's in-place rehash (Core.h:650-682)
+ *   exactly, without the product's repair: under the histories where that rehash strands keys
+ *   (its debug build exits there, Core.h:665-669) the table, and so every pn_classify record,
+ *   is what the reference's would be, lost connections included.  Default (0): the defect is
+ *   detected and the table rebuilt canonically (pn_table_repairs counts it). */
+#define PN_TABLE_REFERENCE_LITERAL 1u
+int pn_table_create_ex(uint32_t max_conn_cnt, uint32_t max_tw_cnt, uint32_t flags, pn_conn_table** out);
+uint32_t pn_table_flags(const pn_conn_table* t);
 void pn_table_destroy(pn_conn_table* t);
 /* findConnEntry (Core.h:558-562): index of the entry the probe stops at; *hit = key matched. */
 int pn_table_find(const pn_conn_table* t, uint64_t key, uint32_t* entry_idx, int* hit, uint32_t* conn_id);

@@ -35,10 +35,13 @@ class ConnTable {
   ConnTable& operator=(const ConnTable&) = delete;
   ~ConnTable() { pn_table_destroy(t_); }
 
-  const char* init(uint32_t max_conn_cnt, uint32_t max_tw_cnt) {
+  // reference_literal: PN_TABLE_REFERENCE_LITERAL (the reference's rehash kept as is, defect included)
+  const char* init(uint32_t max_conn_cnt, uint32_t max_tw_cnt, bool reference_literal = false) {
     pn_table_destroy(t_);
     t_ = nullptr;
-    return pn_table_create(max_conn_cnt, max_tw_cnt, &t_) ? "pn_table_create failed" : nullptr;
+    return pn_table_create_ex(max_conn_cnt, max_tw_cnt, reference_literal ? PN_TABLE_REFERENCE_LITERAL : 0u, &t_)
+               ? "pn_table_create failed"
+               : nullptr;
   }
   static uint64_t key(uint32_t ip_be, uint16_t port_be) { return pn_conn_hash_key(ip_be, port_be); } // Core.h:167
   bool find(uint64_t key, uint32_t* entry_idx, uint32_t* conn_id) const {                              // Core.h:558

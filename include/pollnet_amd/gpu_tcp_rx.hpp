@@ -60,9 +60,10 @@ class GpuTcpRx {
 
   // device / ring layout / chunk / mode as GpuRx::init; the table holds MaxConnCnt
   // connections and MaxTimeWaitConnCnt TIME_WAIT entries (Core.h:780-781).
+  // reference_literal: the conn table keeps the reference's rehash as is (PN_TABLE_REFERENCE_LITERAL).
   const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch,
-                   GpuRx::Mode mode = GpuRx::Mode::Copy) {
-    const char* e = table_.init(Conf::MaxConnCnt, Conf::MaxTimeWaitConnCnt);
+                   GpuRx::Mode mode = GpuRx::Mode::Copy, bool reference_literal = false) {
+    const char* e = table_.init(Conf::MaxConnCnt, Conf::MaxTimeWaitConnCnt, reference_literal);
     if (e) return e;
     if ((e = rx_.init(device, slot_stride, frame_off, max_batch, mode))) return e;
     free_.clear();

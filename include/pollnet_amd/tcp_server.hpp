@@ -90,6 +90,7 @@ PN_CONF_OPT(RxBatch, uint32_t, 512)         // frames per poll (RecvBufCnt = 512
 PN_CONF_OPT(TxBatch, uint32_t, 1024)        // frames per pn_tx_fill launch
 PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
 PN_CONF_OPT(Device, int, 0)
+PN_CONF_OPT(ReferenceLiteralTable, bool, false) // PN_TABLE_REFERENCE_LITERAL: the reference's rehash, defect kept
 #undef PN_CONF_OPT
 
 #define PN_HANDLER_OPT(name, call)                                                                   \
@@ -515,7 +516,7 @@ class GpuTcpServer {
     }
     std::memcpy(local_mac_, link_.localMac(), 6);
     port_be_ = htons(server_port);
-    if ((err_ = table_.init(kMaxConn, kMaxConn))) return false;
+    if ((err_ = table_.init(kMaxConn, kMaxConn, srv_detail::opt_ReferenceLiteralTable<Conf>::value))) return false;
     if ((err_ = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch))) return false;
     free_conns_.clear();
     for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i

@@ -25,8 +25,10 @@ struct ConnTable {
   uint64_t mask = 0;
   uint32_t max_conn = 0, max_tw = 0, size = 0;
   uint32_t repairs = 0;
+  bool literal = false; // PN_TABLE_REFERENCE_LITERAL: keep tryExpandConnTbl's result as it is
 
-  bool init(uint32_t mc, uint32_t mtw) {
+  bool init(uint32_t mc, uint32_t mtw, bool lit) {
+    literal = lit;
     max_conn = mc;
     max_tw = mtw;
     uint64_t max_tbl = 1ull << (1 + msb_count(mc + mtw));
@@ -69,7 +71,9 @@ struct ConnTable {
     // conn_id and becomes unreachable.  We run the reference's rehash verbatim and,
     // only if that condition fires, rebuild the table from a snapshot instead
     // (ordered hashing has one canonical layout per key set, which is what the
-    // reference produces whenever its rehash is well-defined).
+    // reference produces whenever its rehash is well-defined).  In reference-literal
+    // mode the table keeps exactly what the reference's rehash leaves, stranded keys
+    // included, so that records match the reference bit for bit under such histories.
     std::vector<pn_conn_entry> saved;
     saved.reserve(size);
     for (const auto& x : tbl)
@@ -93,7 +97,7 @@ struct ConnTable {
     };
     rehash(0, size - end_cnt);
     rehash(mask + 1, end_cnt);
-    if (broken) {
+    if (broken && !literal) {
       ++repairs;
       for (auto& x : tbl) x = pn_conn_entry{PN_EMPTY_KEY, 0, 0};
       for (const auto& x : saved) insert_sorted(x.key, x.conn_id);
@@ -145,10 +149,14 @@ uint64_t pn_conn_hash_key(uint32_t ip_be, uint16_t port_be) {
 }
 
 int pn_table_create(uint32_t max_conn_cnt, uint32_t max_tw_cnt, pn_conn_table** out) {
-  if (!out || max_conn_cnt == 0) return PN_EINVAL;
+  return pn_table_create_ex(max_conn_cnt, max_tw_cnt, 0, out);
+}
+
+int pn_table_create_ex(uint32_t max_conn_cnt, uint32_t max_tw_cnt, uint32_t flags, pn_conn_table** out) {
+  if (!out || max_conn_cnt == 0 || (flags & ~PN_TABLE_REFERENCE_LITERAL)) return PN_EINVAL;
   auto* t = new (std::nothrow) pn_conn_table();
   if (!t) return PN_ENOMEM;
-  if (!t->t.init(max_conn_cnt, max_tw_cnt)) {
+  if (!t->t.init(max_conn_cnt, max_tw_cnt, flags & PN_TABLE_REFERENCE_LITERAL)) {
     delete t;
     return PN_EINVAL;
   }
@@ -196,5 +204,6 @@ const pn_conn_entry* pn_table_entries(const pn_conn_table* t, uint32_t* n_entrie
 uint32_t pn_table_max_conn_cnt(const pn_conn_table* t) { return t ? t->t.max_conn : 0; }
 uint32_t pn_table_size(const pn_conn_table* t) { return t ? t->t.size : 0; }
 uint32_t pn_table_repairs(const pn_conn_table* t) { return t ? t->t.repairs : 0; }
+uint32_t pn_table_flags(const pn_conn_table* t) { return t && t->t.literal ? PN_TABLE_REFERENCE_LITERAL : 0u; }
 
 } // extern "C"

@@ -95,6 +95,8 @@ def _sig(name, res, *args):
 
 _pn_conn_hash_key = _sig("pn_conn_hash_key", _u64, _u32, _u16)
 _pn_table_create = _sig("pn_table_create", _i32, _u32, _u32, _c.POINTER(_vp))
+_pn_table_create_ex = _sig("pn_table_create_ex", _i32, _u32, _u32, _u32, _c.POINTER(_vp))
+_pn_table_flags = _sig("pn_table_flags", _u32, _vp)
 _pn_table_destroy = _sig("pn_table_destroy", None, _vp)
 _pn_table_find = _sig("pn_table_find", _i32, _vp, _u64, _c.POINTER(_u32), _c.POINTER(_i32), _c.POINTER(_u32))
 _pn_table_add = _sig("pn_table_add", _i32, _vp, _u64, _u32)
@@ -136,13 +138,20 @@ def device_count() -> int:
     return n.value
 
 
-class ConnTable:
-    """Core's ordered linear-probe conn table (Core.h:178-182, 235-236, 558-682)."""
+PN_TABLE_REFERENCE_LITERAL = 1
 
-    def __init__(self, max_conn_cnt: int, max_tw_cnt: int):
+
+class ConnTable:
+    """Core's ordered linear-probe conn table (Core.h:178-182, 235-236, 558-682).
+    reference_literal=True keeps tryExpandConnTbl's rehash exactly (Core.h:650-682), the
+    key-stranding defect included; the default repairs it (``repairs`` counts)."""
+
+    def __init__(self, max_conn_cnt: int, max_tw_cnt: int, reference_literal: bool = False):
         h = _vp()
-        _check(_pn_table_create(max_conn_cnt, max_tw_cnt, _c.byref(h)), None, "pn_table_create")
+        flags = PN_TABLE_REFERENCE_LITERAL if reference_literal else 0
+        _check(_pn_table_create_ex(max_conn_cnt, max_tw_cnt, flags, _c.byref(h)), None, "pn_table_create_ex")
         self._h = h
+        self.reference_literal = bool(_pn_table_flags(h) & PN_TABLE_REFERENCE_LITERAL)
 
     def __del__(self):
         if getattr(self, "_h", None):

@@ -376,3 +376,34 @@ def test_calib_slot_read_var(torch_cuda, ctx):
         tn.calib_slot_read_var(ctx, frames, n, 100, lens, sink, None, 16)
     with pytest.raises(pa.PollnetError, match="bad arguments"):
         tn.calib_slot_read_var(ctx, frames, n, stride, lens, sink, None, 8)
+
+
+def test_reference_literal_table_records(torch_cuda, ctx):
+    """PN_TABLE_REFERENCE_LITERAL on the rehash-defect history (tests/test_oracle.py): frames
+    from every live flow — the stranded ones included — classified on the GPU against the
+    literal table equal the oracle's records against the oracle's own table, bit for bit;
+    the stranded flows come back as misses, as they would from the reference."""
+    import socket
+    import struct
+
+    from test_oracle import _apply, _random_history
+
+    ops, live = _random_history(7, 400, 0.5)
+    ot, lt = orc.Table(256, 256), pa.ConnTable(256, 256, reference_literal=True)
+    for op, k, c in ops:
+        _apply(ot, op, k, c)
+        _apply(lt, op, k, c)
+    frames = []
+    for k in list(live) + [(0x0A0B0C0D << 15) | 0x1234]:  # + one unknown flow
+        ip = (k >> 15) & 0xFFFFFFFF
+        port = (k & 0x7FFF) | ((k >> 32) & 0x8000)  # connHashKey inverted (Core.h:167-172)
+        frames.append(make_frame(src=socket.inet_ntoa(struct.pack("!I", ip)), sport=port, payload=b"x" * (k % 97)))
+    slots = to_slots(frames)
+    n = len(frames)
+    e, m = lt.snapshot()
+    got = gpu_classify(torch_cuda, ctx, slots, STRIDE, FRAME_OFF, n, e, m, lt.max_conn_cnt)
+    oe = ot.entries()
+    exp = orc.classify_batch(slots, STRIDE, FRAME_OFF, n, oe, ot.mask, 256)
+    assert_same(got, exp)
+    lost = [i for i, k in enumerate(live) if oe[ot.find(k)]["key"] != k]
+    assert lost and all(got["conn_id"][i] == pa.PN_MISS for i in lost)

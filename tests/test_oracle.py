@@ -155,6 +155,26 @@ def test_reference_rehash_defect_and_product_repair():
         assert hit and c == cid
 
 
+def test_reference_literal_table_equals_oracle_through_the_defect():
+    """PN_TABLE_REFERENCE_LITERAL: the product table runs tryExpandConnTbl's rehash exactly
+    (Core.h:650-682), so on the defect history it equals the literal oracle byte for byte at
+    every step (mask, every key, every occupied conn_id) and strands the same keys."""
+    ops, live = _random_history(7, 400, 0.5)
+    ot, lt = orc.Table(256, 256), pa.ConnTable(256, 256, reference_literal=True)
+    assert lt.reference_literal
+    for op, k, c in ops:
+        _apply(ot, op, k, c)
+        _apply(lt, op, k, c)
+        le, lm = lt.snapshot()
+        oe = ot.entries()
+        assert lm == ot.mask and np.array_equal(le["key"], oe["key"])
+        occ = le["key"] != pa.PN_EMPTY_KEY
+        assert np.array_equal(le["conn_id"][occ], oe["conn_id"][occ])
+    assert lt.repairs == 0
+    lost = [k for k in live if not lt.find(k)[1]]
+    assert lost and lost == [k for k in live if oe[ot.find(k)]["key"] != k]
+
+
 def test_product_table_is_canonical_under_clustered_history():
     """Ordered hashing has one layout per key set; the product keeps it through
     adds, backward-shift deletes, expansions and repairs (clustered keys)."""
