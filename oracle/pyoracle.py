@@ -198,3 +198,77 @@ def tx_fill_batch(slots: np.ndarray, stride: int, frame_off: int, n: int, lens=N
 
 def tx_copy_and_sum_batch(slots: np.ndarray, out: np.ndarray, stride: int, frame_off: int, n: int, threads: int = 1):
     _tx_cas(slots.ctypes.data, out.ctypes.data, stride, frame_off, n, threads)
+
+
+# ---------------- the reference itself: efvitcp/Core.h's hot-path code (oracle/_ref/libref_core.so) ----------------
+REF_CORE_SO = os.path.join(HERE, "_ref", "libref_core.so")
+_rc = None
+
+
+def ref_core():
+    """ctypes handle of libref_core.so (oracle/ref_core.cc: Core.h's CSum, headers, connHashKey,
+    conn-table member functions and Core::checksum compiled verbatim), or None if not built."""
+    global _rc
+    if _rc is None and os.path.exists(REF_CORE_SO):
+        lib = C.CDLL(REF_CORE_SO)
+        for name, res, args in (
+            ("ref_csum_fold", C.c_uint16, [_u32]),
+            ("ref_csum_words", C.c_uint16, [_vp, _u32]),
+            ("ref_conn_hash_key", _u64, [_u32, C.c_uint16]),
+            ("ref_header_fields", None, [_vp, _vp]),
+            ("ref_checksum", _i32, [_vp]),
+            ("ref_table_new", _vp, []),
+            ("ref_table_free", None, [_vp]),
+            ("ref_table_add", _i32, [_vp, _u64, _u32]),
+            ("ref_table_del", _i32, [_vp, _u64]),
+            ("ref_table_set_conn_id", _i32, [_vp, _u64, _u32]),
+            ("ref_table_find", _u32, [_vp, _u64]),
+            ("ref_table_entries", _u32, [_vp, _vp, _vp, _vp]),
+            ("ref_table_debug_exits", _i32, [_vp]),
+            ("ref_table_total_size", _u32, []),
+        ):
+            f = getattr(lib, name)
+            f.restype, f.argtypes = res, args
+        _rc = lib
+    return _rc
+
+
+class RefCoreTable:
+    """Core<Conf>'s conn table run by the reference's own member functions (MaxConnCnt =
+    MaxTimeWaitConnCnt = 256), driven as TcpServer / enterTW drive it."""
+
+    def __init__(self):
+        self.lib = ref_core()
+        self.h = self.lib.ref_table_new()
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.ref_table_free(self.h)
+            self.h = None
+
+    def add(self, key, cid):
+        return int(self.lib.ref_table_add(self.h, key, cid))
+
+    def delete(self, key):
+        return int(self.lib.ref_table_del(self.h, key))
+
+    def set_conn_id(self, key, cid):
+        return int(self.lib.ref_table_set_conn_id(self.h, key, cid))
+
+    def find(self, key):
+        return int(self.lib.ref_table_find(self.h, key))
+
+    def entries(self):
+        n = int(self.lib.ref_table_total_size())
+        keys = np.zeros(n, np.uint64)
+        cids = np.zeros(n, np.uint32)
+        mask = C.c_uint64()
+        got = self.lib.ref_table_entries(self.h, keys.ctypes.data, cids.ctypes.data, C.byref(mask))
+        assert got == n
+        out = np.zeros(n, ENTRY_DTYPE)
+        out["key"], out["conn_id"] = keys, cids
+        return out, int(mask.value)
+
+    @property
+    def debug_exits(self):
+        return int(self.lib.ref_table_debug_exits(self.h))

@@ -3,7 +3,7 @@
 # efvitcp/Core.h needs <etherfabric/*.h> (ef_vi, not installed) and stand-ins for those
 # headers are not allowed, so it is not built.
 REFDIR ?= /root/reference
-all: _ref/libref_tcpstream.so _ref/ref_socket_c1 _ref/tcpserver_handler.inc
+all: _ref/libref_tcpstream.so _ref/ref_socket_c1 _ref/tcpserver_handler.inc _ref/libref_core.so
 
 _ref/libref_tcpstream.so: ref_tcpstream.cc $(REFDIR)/TcpStream.h
 	mkdir -p _ref
@@ -24,3 +24,27 @@ _ref/tcpserver_handler.inc: $(REFDIR)/example/tcpserver.cc
 	mkdir -p _ref
 	sed -n '61,90p' $< > $@
 	grep -q 'onTcpData' $@ && grep -q '} handler;' $@
+
+# The reference's own Core.h code for the hot path (CSum, headers, connHashKey, the conn
+# table's member functions, Core::checksum), extracted verbatim by line range and compiled
+# inside the harness class of ref_core.cc.  Each range is checked to start and end where
+# expected, so a changed reference fails the build instead of compiling the wrong lines.
+CORE = $(REFDIR)/efvitcp/Core.h
+_ref/core_defs.inc: $(CORE)
+	mkdir -p _ref
+	sed -n '44p' $< | grep -q 'RecvMSS' && sed -n '138p' $< | grep -q '^};' && sed -n '167p' $< | grep -q 'connHashKey' && sed -n '182p' $< | grep -q '^};'
+	sed -n '44,138p;167,182p' $< > $@
+_ref/core_sizes.inc: $(CORE)
+	mkdir -p _ref
+	sed -n '235p' $< | grep -q MaxTableSize && sed -n '236p' $< | grep -q TotalTableSize
+	sed -n '235,236p' $< > $@
+_ref/core_table.inc: $(CORE)
+	mkdir -p _ref
+	sed -n '558p' $< | grep -q findConnEntry && sed -n '605p' $< | grep -q '^  }' && sed -n '640p' $< | grep -q EFVITCP_DEBUG && sed -n '650p' $< | grep -q tryExpandConnTbl && sed -n '682p' $< | grep -q '^  }'
+	sed -n '558,605p;640,648p;650,682p' $< > $@
+_ref/core_checksum.inc: $(CORE)
+	mkdir -p _ref
+	sed -n '448p' $< | grep -q EFVITCP_DEBUG && sed -n '449p' $< | grep -q 'void checksum' && sed -n '472p' $< | grep -q endif
+	sed -n '448,472p' $< > $@
+_ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc
+	g++ -O2 -std=c++17 -fPIC -shared -Wno-unused-result -o $@ ref_core.cc

@@ -1,0 +1,176 @@
+// Test-only harness: compiles the reference's OWN efvitcp/Core.h code for the hot path,
+// extracted verbatim from /root/reference at build time (oracle/ref.mk -> _ref/core_*.inc,
+// git-ignored; no reference text is kept in the repository):
+//   core_defs.inc     Core.h:44-138, 167-182  constants, EtherHeader/IpHeader/TcpHeader,
+//                                             CSum, connHashKey, getMSB, ConnHashEntry
+//   core_sizes.inc    Core.h:235-236          MaxTableSize, TotalTableSize
+//   core_table.inc    Core.h:558-605, 640-682 findConnEntry, getTblSize, addConnEntry,
+//                                             delConnEntry, printTbl, tryExpandConnTbl
+//   core_checksum.inc Core.h:448-472          Core::checksum (EFVITCP_DEBUG)
+// Those member functions are pasted, unchanged, into RefCore below, which supplies only
+// the data members they read (conn_tbl, tbl_mask, conn_cnt, conns, tw_cnt, tw_ids) and
+// takes the debug build's `cout` / `exit(1)` as members, so a failed check is recorded
+// and execution continues (the reference process would end there).  No ef_vi header is
+// needed or faked: none of these lines touches ef_vi.
+// Nothing here is shipped or used by the product path; tests/test_ref_core.py pins the
+// oracle (oracle/pn_oracle.c) and the product's conn table against it.
+#define EFVITCP_DEBUG
+#include <arpa/inet.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <utility>
+
+namespace efvitcp {
+using std::endl;
+#include "_ref/core_defs.inc"
+
+// The debug build's output and exit, captured.
+struct Capture {
+  std::ostringstream os;
+  template <class T>
+  Capture& operator<<(const T& v) {
+    os << v;
+    return *this;
+  }
+  Capture& operator<<(std::ostream& (*m)(std::ostream&)) {
+    os << m;
+    return *this;
+  }
+};
+
+template <uint32_t MaxConn, uint32_t MaxTW>
+struct RefCore {
+  struct Conf {
+    static const uint32_t MaxConnCnt = MaxConn;
+    static const uint32_t MaxTimeWaitConnCnt = MaxTW;
+  };
+#include "_ref/core_sizes.inc"
+
+  Capture cout;
+  int exits = 0;
+  void exit(int) { ++exits; }
+
+  // the id stacks are sized for any mix of connection and TIME_WAIT ids up to the table's
+  // capacity (random test histories do not keep the reference's per-class limits)
+  uint32_t conn_cnt = 0;
+  uint32_t conns[MaxConn + MaxTW];
+  uint32_t tw_cnt = 0;
+  uint32_t tw_ids[MaxConn + MaxTW];
+  uint64_t tbl_mask = 0;
+  ConnHashEntry conn_tbl[TotalTableSize];
+
+  RefCore() { // Core::init's table part (Core.h:315-322)
+    for (uint32_t i = 0; i < MaxConn; i++) conns[i] = i;
+    for (uint32_t i = 0; i < MaxTW; i++) tw_ids[i] = i;
+    for (auto& e : conn_tbl) e.key = EmptyKey;
+    tbl_mask = std::min(MaxTableSize, 128u) - 1;
+  }
+
+#include "_ref/core_table.inc"
+#include "_ref/core_checksum.inc"
+};
+} // namespace efvitcp
+
+namespace {
+using Ref = efvitcp::RefCore<256, 256>; // the oracle tests' table sizing (tests/test_oracle.py)
+}
+
+extern "C" {
+
+uint16_t ref_csum_fold(uint32_t sum) { return efvitcp::CSum(sum).fold(); }
+
+// CSum over n host-order u16 words via add(uint16_t), then fold().
+uint16_t ref_csum_words(const uint16_t* w, uint32_t n) {
+  efvitcp::CSum s = 0;
+  for (uint32_t i = 0; i < n; i++) s.add(w[i]);
+  return s.fold();
+}
+
+uint64_t ref_conn_hash_key(uint32_t ip_be, uint16_t port_be) { return efvitcp::connHashKey(ip_be, port_be); }
+
+// Header fields as the reference's bitfield structs read them (IpHeader/TcpHeader, Core.h:57-87):
+// out[0] ip header_len, [1] ip_ver, [2] tot_len (host order), [3] protocol,
+// [4] data_offset, [5] fin, [6] syn, [7] rst, [8] psh, [9] ack, [10] seq (host order).
+void ref_header_fields(const uint8_t* eth, uint32_t* out) {
+  const auto* ip = reinterpret_cast<const efvitcp::IpHeader*>(eth + sizeof(efvitcp::EtherHeader));
+  const auto* tcp = reinterpret_cast<const efvitcp::TcpHeader*>(ip + 1);
+  out[0] = ip->header_len;
+  out[1] = ip->ip_ver;
+  out[2] = ntohs(ip->tot_len);
+  out[3] = ip->protocol;
+  out[4] = tcp->data_offset;
+  out[5] = tcp->fin;
+  out[6] = tcp->syn;
+  out[7] = tcp->rst;
+  out[8] = tcp->psh;
+  out[9] = tcp->ack;
+  out[10] = ntohl(tcp->seq_num);
+}
+
+// Core::checksum on one frame: bit 0 = the IP sum verified, bit 1 = the TCP sum verified
+// (each exit(1) of the debug build is recorded instead of ending the process).
+int ref_checksum(const uint8_t* eth) {
+  std::unique_ptr<Ref> c(new Ref());
+  c->checksum(reinterpret_cast<efvitcp::IpHeader*>(const_cast<uint8_t*>(eth) + sizeof(efvitcp::EtherHeader)));
+  const std::string log = c->cout.os.str();
+  const bool ip_bad = log.find("invalid ip sum") != std::string::npos;
+  const bool tcp_bad = log.find("invalid tcp sum") != std::string::npos;
+  return (ip_bad ? 0 : 1) | (tcp_bad ? 0 : 2);
+}
+
+// ---- the conn table, driven the way the reference's callers drive it ----
+void* ref_table_new() { return new Ref(); }
+void ref_table_free(void* t) { delete static_cast<Ref*>(t); }
+
+// TcpServer.h:88-90 / Core::enterTW's bookkeeping: a connection id takes a conn slot, an id
+// >= MaxConnCnt a TIME_WAIT slot; then findConnEntry + addConnEntry.  -1 if the key is present.
+int ref_table_add(void* tp, uint64_t key, uint32_t conn_id) {
+  Ref* t = static_cast<Ref*>(tp);
+  efvitcp::ConnHashEntry* e = t->findConnEntry(key);
+  if (e->key == key) return -1;
+  if (conn_id < 256) t->conn_cnt++;
+  else t->tw_cnt++;
+  t->addConnEntry(e, key, conn_id);
+  return 0;
+}
+int ref_table_del(void* tp, uint64_t key) {
+  Ref* t = static_cast<Ref*>(tp);
+  if (t->findConnEntry(key)->key != key) return -1;
+  t->delConnEntry(key);
+  return 0;
+}
+// relabel (Core::enterTW's entry->conn_id = MaxConnCnt + tw_id, Core.h:626), moving the count
+int ref_table_set_conn_id(void* tp, uint64_t key, uint32_t conn_id) {
+  Ref* t = static_cast<Ref*>(tp);
+  efvitcp::ConnHashEntry* e = t->findConnEntry(key);
+  if (e->key != key) return -1;
+  if (e->conn_id < 256 && conn_id >= 256) t->conn_cnt--, t->tw_cnt++;
+  if (e->conn_id >= 256 && conn_id < 256) t->tw_cnt--, t->conn_cnt++;
+  e->conn_id = conn_id;
+  return 0;
+}
+uint32_t ref_table_find(void* tp, uint64_t key) {
+  Ref* t = static_cast<Ref*>(tp);
+  return (uint32_t)(t->findConnEntry(key) - t->conn_tbl);
+}
+// entries as 16-B {key, conn_id, pad} records (the product's pn_conn_entry layout)
+uint32_t ref_table_entries(void* tp, uint64_t* keys, uint32_t* conn_ids, uint64_t* mask) {
+  Ref* t = static_cast<Ref*>(tp);
+  for (uint32_t i = 0; i < Ref::TotalTableSize; i++) {
+    keys[i] = t->conn_tbl[i].key;
+    conn_ids[i] = t->conn_tbl[i].conn_id;
+  }
+  *mask = t->tbl_mask;
+  return Ref::TotalTableSize;
+}
+uint32_t ref_table_total_size() { return Ref::TotalTableSize; }
+// how many times the debug build's rehash check fired (Core.h:665-669: it would have exited)
+int ref_table_debug_exits(void* tp) { return static_cast<Ref*>(tp)->exits; }
+
+} // extern "C"

@@ -407,3 +407,27 @@ def test_reference_literal_table_records(torch_cuda, ctx):
     assert_same(got, exp)
     lost = [i for i, k in enumerate(live) if oe[ot.find(k)]["key"] != k]
     assert lost and all(got["conn_id"][i] == pa.PN_MISS for i in lost)
+
+
+def test_gpu_verdicts_equal_reference_core_checksum(torch_cuda, ctx, golden_dir):
+    """GPU IP_OK / TCP_OK against the reference's own Core::checksum (Core.h:448-472, compiled
+    from /root/reference into oracle/_ref/libref_core.so) directly, on the committed edge
+    fixture: every frame whose summed bytes lie inside its slot."""
+    ref = orc.ref_core()
+    if ref is None:
+        pytest.skip("oracle/_ref/libref_core.so not built")
+    d = np.load(os.path.join(golden_dir, "edge_frames.npz"))
+    slots, stride, off = d["slots"], int(d["stride"]), int(d["frame_off"])
+    n = len(slots)
+    got = gpu_classify(torch_cuda, ctx, slots, stride, off, n, d["entries"], int(d["mask"]), int(d["max_conn"]))
+    checked = 0
+    for i in range(n):
+        eth = np.ascontiguousarray(slots[i, off:])
+        tot = (int(eth[16]) << 8) | int(eth[17])
+        if tot < 20 or 14 + tot + (tot & 1) > stride - off:
+            continue
+        v = ref.ref_checksum(eth.ctypes.data)
+        f = int(got["flags"][i])
+        assert bool(v & 1) == bool(f & pa.F.IP_OK) and bool(v & 2) == bool(f & pa.F.TCP_OK), i
+        checked += 1
+    assert checked > 1500

@@ -1,0 +1,164 @@
+"""The oracle and the product's conn table pinned against the reference's OWN code.
+
+oracle/_ref/libref_core.so is efvitcp/Core.h's hot-path code compiled verbatim from
+/root/reference (oracle/ref_core.cc, oracle/ref.mk): CSum (Core.h:89-138), the
+EtherHeader/IpHeader/TcpHeader bitfield layouts (:51-87), connHashKey (:167-172),
+Core::checksum (:448-472, the EFVITCP_DEBUG check, its exit(1) recorded instead of
+taken) and the conn table's member functions findConnEntry / addConnEntry /
+delConnEntry / tryExpandConnTbl (:558-605, 650-682).  Everything the RX records
+depend on apart from TcpConn::onPack's two lines of payload arithmetic
+(TcpConn.h:469-473, pinned by the reference's TcpStream.h in test_oracle.py) is
+therefore checked against the reference itself, on the committed edge fixtures,
+the BASELINE config slices and random inputs."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import pollnet_amd as pa  # noqa: E402
+from oracle import pyoracle as orc  # noqa: E402
+
+ref = orc.ref_core()
+pytestmark = pytest.mark.skipif(ref is None, reason="oracle/_ref/libref_core.so not built (needs /root/reference)")
+
+
+def test_csum_fold_and_word_sums_match_reference():
+    rng = np.random.default_rng(1)
+    sums = [0, 1, 0xFFFF, 0x10000, 0x1FFFE, 0x1FFFF, 0xFFFEFFFF, 0xFFFFFFFF] + list(
+        rng.integers(0, 1 << 32, 20000, dtype=np.uint64))
+    for s in sums:
+        assert orc._fold(orc._Csum(int(s))) == ref.ref_csum_fold(int(s)), hex(int(s))
+    for n in (0, 1, 2, 10, 750):  # up to a 1500-B segment's words
+        for _ in range(50):
+            w = rng.integers(0, 1 << 16, n, dtype=np.uint16)
+            c = orc._Csum(0)
+            for x in w:
+                orc._add16(orc.C.byref(c), int(x))
+            assert orc._fold(c) == ref.ref_csum_words(w.ctypes.data, n)
+
+
+def test_conn_hash_key_matches_reference():
+    rng = np.random.default_rng(2)
+    ips = [0, 0xFFFFFFFF, 0x0100000A, 0x0200000A] + list(rng.integers(0, 1 << 32, 20000, dtype=np.uint64))
+    ports = [0, 0xFFFF, 0x0080, 0x8000, 0x409C] + list(rng.integers(0, 1 << 16, 20000, dtype=np.uint64))
+    for ip, port in zip(ips, ports):
+        k = ref.ref_conn_hash_key(int(ip), int(port))
+        assert k == orc._key(int(ip), int(port)) == pa.conn_hash_key(int(ip), int(port))
+
+
+def _frames():
+    """(slots, stride, frame_off, n, entries, mask, max_conn) of every committed fixture."""
+    d = np.load(os.path.join(ROOT, "tests", "golden", "edge_frames.npz"))
+    out = [(d["slots"], int(d["stride"]), int(d["frame_off"]), len(d["slots"]), d["entries"], int(d["mask"]),
+            int(d["max_conn"]))]
+    for cfg in (2, 3, 5):
+        p = pa.rx.GenParams.for_config(cfg)
+        t = pa.gen_conn_table(p)
+        e, m = t.snapshot()
+        out.append((pa.gen_frames(p, 4096), 2048, 2, 4096, e, m, t.max_conn_cnt))
+    return out
+
+
+def test_header_fields_match_reference_bitfields():
+    """IpHeader.header_len / TcpHeader.data_offset / flag bits as the reference's structs read
+    them (Core.h:57-87) equal the oracle's record fields (IHL_NE_5, FIN..ACK, seq + syn)."""
+    out = np.zeros(11, np.uint32)
+    checked = 0
+    for slots, stride, off, n, e, m, mc in _frames():
+        rec = orc.classify_batch(np.ascontiguousarray(slots), stride, off, n, e, m, mc)
+        for i in range(n):
+            eth = slots[i, off:]
+            ref.ref_header_fields(np.ascontiguousarray(eth).ctypes.data, out.ctypes.data)
+            f = int(rec["flags"][i])
+            assert bool(f & pa.F.IHL_NE_5) == (out[0] != 5)
+            for bit, v in ((pa.F.FIN, out[5]), (pa.F.SYN, out[6]), (pa.F.RST, out[7]), (pa.F.PSH, out[8]),
+                           (pa.F.ACK, out[9])):
+                assert bool(f & bit) == bool(v)
+            assert int(rec["seq"][i]) == (int(out[10]) + int(out[6])) & 0xFFFFFFFF  # TcpConn.h:473
+            checked += 1
+    assert checked > 14000
+
+
+def test_checksum_verdicts_match_reference_core_checksum():
+    """Core::checksum (Core.h:448-472) — the reference's own verification, run on every fixture
+    frame whose summed bytes lie inside its slot — gives the oracle's REF-mode IP_OK / TCP_OK
+    verdicts bit for bit (IHL assumed 5, odd segments summed with the byte after them)."""
+    checked = bad = 0
+    for slots, stride, off, n, e, m, mc in _frames():
+        rec = orc.classify_batch(np.ascontiguousarray(slots), stride, off, n, e, m, mc)
+        for i in range(n):
+            eth = slots[i, off:]
+            tot = (int(eth[16]) << 8) | int(eth[17])
+            if tot < 20 or 14 + tot + (tot & 1) > stride - off:  # the reference would read outside the slot
+                assert rec["flags"][i] & pa.F.TRUNC or tot < 20
+                continue
+            v = ref.ref_checksum(np.ascontiguousarray(eth).ctypes.data)
+            f = int(rec["flags"][i])
+            assert bool(v & 1) == bool(f & pa.F.IP_OK), i
+            assert bool(v & 2) == bool(f & pa.F.TCP_OK), i
+            checked += 1
+            bad += (v != 3)
+    assert checked > 14000 and bad > 100  # both verdicts occur
+
+
+def _history(seed, n_steps, cluster_frac):
+    from test_oracle import _random_history
+
+    return _random_history(seed, n_steps, cluster_frac)
+
+
+@pytest.mark.parametrize("seed,steps,cluster", [(11, 3000, 0.0), (3, 3000, 0.5), (7, 400, 0.5)])
+def test_conn_table_matches_reference_member_functions(seed, steps, cluster):
+    """The same add / delete / relabel history through the reference's own findConnEntry /
+    addConnEntry / delConnEntry / tryExpandConnTbl, the C oracle and the product table in
+    reference-literal mode: identical masks, keys and occupied conn_ids at every step.  Where
+    the reference's rehash strands keys (seed 7), its own debug check fires (Core.h:665-669)
+    and the product's default mode repairs the layout."""
+    ops, live = _history(seed, steps, cluster)
+    rt, ot = orc.RefCoreTable(), orc.Table(256, 256)
+    lt, pt = pa.ConnTable(256, 256, reference_literal=True), pa.ConnTable(256, 256)
+    for op, k, c in ops:
+        if op == "add":
+            ro = ot.add(k, c)
+            if ro == -2:  # MaxConnCnt + MaxTimeWaitConnCnt entries: the reference's callers never add then
+                live.pop(k, None)
+                continue
+            assert rt.add(k, c) == ro
+            lt.add(k, c)
+            pt.add(k, c)
+        elif op == "del":
+            r = rt.delete(k)
+            assert r == ot.delete(k)
+            if r == 0:
+                lt.delete(k)
+            pt.delete(k)
+        else:
+            r = rt.set_conn_id(k, c)
+            if r == 0:
+                ot.set_conn_id(k, c)
+                lt.set_conn_id(k, c)
+            pt.set_conn_id(k, c)
+        re_, rm = rt.entries()
+        le, lm = lt.snapshot()
+        oe = ot.entries()
+        assert rm == lm == ot.mask
+        assert np.array_equal(re_["key"], le["key"]) and np.array_equal(re_["key"], oe["key"])
+        occ = re_["key"] != pa.PN_EMPTY_KEY
+        assert np.array_equal(re_["conn_id"][occ], le["conn_id"][occ])
+        assert np.array_equal(re_["conn_id"][occ], oe["conn_id"][occ])
+    stranded = [k for k in live if re_[rt.find(k)]["key"] != k]
+    # the product repairs exactly the expansions in which the reference's own debug check fires
+    assert (rt.debug_exits > 0) == (pt.repairs > 0)
+    if stranded:
+        assert rt.debug_exits > 0
+    if seed == 7:
+        assert stranded
+    if cluster == 0.0:
+        assert rt.debug_exits == 0
+    for k, cid in live.items():  # the product's default table finds every live key
+        _, hit, got = pt.find(k)
+        assert hit and got == cid
