@@ -9,16 +9,14 @@
  *   - the reference's OWN efvitcp/Core.h code for this path, compiled verbatim from
  *     /root/reference (oracle/ref_core.cc -> oracle/_ref/libref_core.so, line ranges
  *     extracted by oracle/ref.mk; no ef_vi header needed or faked): CSum, the header
- *     bitfield layouts, connHashKey, Core::checksum and the conn table's member
- *     functions — tests/test_ref_core.py checks this restatement against them on the
- *     committed fixtures, the config slices, random inputs and table histories;
+ *     bitfield layouts, connHashKey, Core::checksum, the conn table's member
+ *     functions and TcpConn::onPack's payload statements (TcpConn.h:469-473) —
+ *     tests/test_ref_core.py checks this restatement against them on the committed
+ *     fixtures, the config slices, random inputs and table histories;
  *   - the reference's own TcpStream.h compiled the same way (oracle/_ref/libref_tcpstream.so:
  *     ethertype/protocol filter, IHL=5 payload split);
  *   - RFC 1071 known answers (tests/golden/known_answers.json) and real kernel-generated
  *     IPv4 headers captured on loopback.
- * Only TcpConn::onPack's payload arithmetic (TcpConn.h:469-473, two lines inside a large
- * member function) is restated without being compiled; TcpStream.h's equivalent split
- * pins it except for the 1500 clamp.
  * Every function cites the reference line it restates.
  */
 #ifndef PN_ORACLE_H

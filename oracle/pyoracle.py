@@ -217,6 +217,8 @@ def ref_core():
             ("ref_conn_hash_key", _u64, [_u32, C.c_uint16]),
             ("ref_header_fields", None, [_vp, _vp]),
             ("ref_checksum", _i32, [_vp]),
+            ("ref_onpack_head", None, [_vp, _vp, _vp, _vp]),
+            ("ref_checksum_folds", _i32, [_vp, _vp, _vp]),
             ("ref_table_new", _vp, []),
             ("ref_table_free", None, [_vp]),
             ("ref_table_add", _i32, [_vp, _u64, _u32]),

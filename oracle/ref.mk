@@ -46,5 +46,10 @@ _ref/core_checksum.inc: $(CORE)
 	mkdir -p _ref
 	sed -n '448p' $< | grep -q EFVITCP_DEBUG && sed -n '449p' $< | grep -q 'void checksum' && sed -n '472p' $< | grep -q endif
 	sed -n '448,472p' $< > $@
-_ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc
+# TcpConn::onPack's first statements (TcpConn.h:469-473): payload start/end and seq + syn
+_ref/onpack_head.inc: $(REFDIR)/efvitcp/TcpConn.h
+	mkdir -p _ref
+	sed -n '468p' $< | grep -q 'void onPack' && sed -n '473p' $< | grep -q 'seq_num' && sed -n '474p' $< | grep -q got_ts
+	sed -n '469,473p' $< > $@
+_ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc _ref/onpack_head.inc
 	g++ -O2 -std=c++17 -fPIC -shared -Wno-unused-result -o $@ ref_core.cc

@@ -7,6 +7,7 @@
 //   core_table.inc    Core.h:558-605, 640-682 findConnEntry, getTblSize, addConnEntry,
 //                                             delConnEntry, printTbl, tryExpandConnTbl
 //   core_checksum.inc Core.h:448-472          Core::checksum (EFVITCP_DEBUG)
+//   onpack_head.inc   TcpConn.h:469-473       TcpConn::onPack's payload extent and seq
 // Those member functions are pasted, unchanged, into RefCore below, which supplies only
 // the data members they read (conn_tbl, tbl_mask, conn_cnt, conns, tw_cnt, tw_ids) and
 // takes the debug build's `cout` / `exit(1)` as members, so a failed check is recorded
@@ -122,6 +123,33 @@ int ref_checksum(const uint8_t* eth) {
   const bool ip_bad = log.find("invalid ip sum") != std::string::npos;
   const bool tcp_bad = log.find("invalid tcp sum") != std::string::npos;
   return (ip_bad ? 0 : 1) | (tcp_bad ? 0 : 2);
+}
+
+// The same, plus the folded sums the check printed ("invalid ip sum: N" / "invalid tcp sum: N";
+// 0 when it verified): the value pn_result.tcp_fold carries.
+int ref_checksum_folds(const uint8_t* eth, uint32_t* ip_fold, uint32_t* tcp_fold) {
+  std::unique_ptr<Ref> c(new Ref());
+  c->checksum(reinterpret_cast<efvitcp::IpHeader*>(const_cast<uint8_t*>(eth) + sizeof(efvitcp::EtherHeader)));
+  const std::string log = c->cout.os.str();
+  auto value = [&](const char* what) -> uint32_t {
+    const size_t p = log.find(what);
+    return p == std::string::npos ? 0u : (uint32_t)std::stoul(log.substr(p + std::strlen(what)));
+  };
+  *ip_fold = value("invalid ip sum: ");
+  *tcp_fold = value("invalid tcp sum: ");
+  return (*ip_fold ? 0 : 1) | (*tcp_fold ? 0 : 2);
+}
+
+// TcpConn::onPack's first statements (TcpConn.h:469-473) on one frame: payload offset from
+// the Ethernet header, payload length (data_end - data, signed), seq + syn.
+void ref_onpack_head(uint8_t* eth, uint32_t* payload_off, int32_t* payload_len, uint32_t* seq) {
+  using namespace efvitcp;
+  IpHeader* ip_hdr = reinterpret_cast<IpHeader*>(eth + sizeof(EtherHeader));
+#include "_ref/onpack_head.inc"
+  (void)opt;
+  *payload_off = (uint32_t)(data - eth);
+  *payload_len = (int32_t)(data_end - data);
+  *seq = seq_num;
 }
 
 // ---- the conn table, driven the way the reference's callers drive it ----

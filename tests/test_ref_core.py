@@ -4,12 +4,11 @@ oracle/_ref/libref_core.so is efvitcp/Core.h's hot-path code compiled verbatim f
 /root/reference (oracle/ref_core.cc, oracle/ref.mk): CSum (Core.h:89-138), the
 EtherHeader/IpHeader/TcpHeader bitfield layouts (:51-87), connHashKey (:167-172),
 Core::checksum (:448-472, the EFVITCP_DEBUG check, its exit(1) recorded instead of
-taken) and the conn table's member functions findConnEntry / addConnEntry /
-delConnEntry / tryExpandConnTbl (:558-605, 650-682).  Everything the RX records
-depend on apart from TcpConn::onPack's two lines of payload arithmetic
-(TcpConn.h:469-473, pinned by the reference's TcpStream.h in test_oracle.py) is
-therefore checked against the reference itself, on the committed edge fixtures,
-the BASELINE config slices and random inputs."""
+taken), the conn table's member functions findConnEntry / addConnEntry /
+delConnEntry / tryExpandConnTbl (:558-605, 650-682), and TcpConn::onPack's payload
+statements (TcpConn.h:469-473).  Every field of every RX record is therefore checked
+against the reference itself, on the committed edge fixtures, the BASELINE config
+slices, random inputs and table histories."""
 import os
 import sys
 
@@ -86,7 +85,11 @@ def test_header_fields_match_reference_bitfields():
 def test_checksum_verdicts_match_reference_core_checksum():
     """Core::checksum (Core.h:448-472) — the reference's own verification, run on every fixture
     frame whose summed bytes lie inside its slot — gives the oracle's REF-mode IP_OK / TCP_OK
-    verdicts bit for bit (IHL assumed 5, odd segments summed with the byte after them)."""
+    verdicts and the folded TCP sum (pn_result.tcp_fold, the value the debug build prints)
+    bit for bit (IHL assumed 5, odd segments summed with the byte after them)."""
+    import ctypes
+
+    ipf, tcpf = ctypes.c_uint32(), ctypes.c_uint32()
     checked = bad = 0
     for slots, stride, off, n, e, m, mc in _frames():
         rec = orc.classify_batch(np.ascontiguousarray(slots), stride, off, n, e, m, mc)
@@ -96,13 +99,34 @@ def test_checksum_verdicts_match_reference_core_checksum():
             if tot < 20 or 14 + tot + (tot & 1) > stride - off:  # the reference would read outside the slot
                 assert rec["flags"][i] & pa.F.TRUNC or tot < 20
                 continue
-            v = ref.ref_checksum(np.ascontiguousarray(eth).ctypes.data)
+            v = ref.ref_checksum_folds(np.ascontiguousarray(eth).ctypes.data, ctypes.byref(ipf), ctypes.byref(tcpf))
             f = int(rec["flags"][i])
             assert bool(v & 1) == bool(f & pa.F.IP_OK), i
             assert bool(v & 2) == bool(f & pa.F.TCP_OK), i
+            assert int(rec["tcp_fold"][i]) == tcpf.value, i  # the folded TCP sum itself
             checked += 1
             bad += (v != 3)
     assert checked > 14000 and bad > 100  # both verdicts occur
+
+
+def test_payload_extent_matches_reference_onpack():
+    """payload_off / payload_len / seq of every record equal what TcpConn::onPack's own first
+    statements compute (TcpConn.h:469-473: data = tcp + doff*4, data_end = ip +
+    min(tot_len, 1500), seq = ntohl(seq_num) + syn), compiled from the reference."""
+    import ctypes
+
+    off_, len_, seq_ = ctypes.c_uint32(), ctypes.c_int32(), ctypes.c_uint32()
+    checked = 0
+    for slots, stride, off, n, e, m, mc in _frames():
+        rec = orc.classify_batch(np.ascontiguousarray(slots), stride, off, n, e, m, mc)
+        for i in range(n):
+            eth = np.ascontiguousarray(slots[i, off:])
+            ref.ref_onpack_head(eth.ctypes.data, ctypes.byref(off_), ctypes.byref(len_), ctypes.byref(seq_))
+            assert int(rec["payload_off"][i]) == off_.value, i
+            assert int(rec["payload_len"][i]) == len_.value, i  # signed: < 0 on malformed frames
+            assert int(rec["seq"][i]) == seq_.value, i
+            checked += 1
+    assert checked > 14000
 
 
 def _history(seed, n_steps, cluster_frac):
