@@ -36,6 +36,8 @@
 //   4. every frame the poll produced (SYN-ACK, ACKs, data, RST, TIME_WAIT ACKs,
 //      retransmissions) gets its IP and TCP checksums from ONE pn_tx_fill launch over the
 //      pinned TX batch, then goes out through the link in generation order.
+// Conf::RxLatencyBudgetUs (default 0: every poll with frames classifies them) lets frames of
+// consecutive polls accumulate for up to that long before one launch takes them all.
 // Sends issued outside poll() (a writeNonblock from the user's own loop) are built at once
 // and leave with the next poll's TX batch.  The table snapshot on the device is refreshed
 // before each classify; records after a table change within the same batch are
@@ -87,6 +89,7 @@ PN_CONF_OPT(SendTimeoutSec, uint32_t, 0)
 PN_CONF_OPT(RecvTimeoutSec, uint32_t, 0)
 PN_CONF_OPT(ConnSendBufCnt, uint32_t, 1024) // EfviTcp.h:181
 PN_CONF_OPT(RxBatch, uint32_t, 512)         // frames per poll (RecvBufCnt = 512, EfviTcp.h:186)
+PN_CONF_OPT(RxLatencyBudgetUs, uint32_t, 0) // hold received frames up to this long for a fuller batch
 PN_CONF_OPT(TxBatch, uint32_t, 1024)        // frames per pn_tx_fill launch
 PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
 PN_CONF_OPT(Device, int, 0)
@@ -319,6 +322,7 @@ class GpuTcpServer {
   static constexpr uint32_t kTimeWaitTimeout = 60 * 1000; // Core.h:48
   static constexpr uint32_t kRxBatch = srv_detail::opt_RxBatch<Conf>::value;
   static constexpr uint32_t kTxBatch = srv_detail::opt_TxBatch<Conf>::value;
+  static constexpr uint32_t kRxBudgetUs = srv_detail::opt_RxLatencyBudgetUs<Conf>::value;
   static_assert(kSendBufCnt >= 4 && !(kSendBufCnt & (kSendBufCnt - 1)), "ConnSendBufCnt must be a power of 2");
   static_assert(Conf::RecvBufSize >= 2 * 1460, "RecvBufSize below two RMSS");
 
@@ -431,11 +435,21 @@ class GpuTcpServer {
   void poll(Handler& handler, int64_t ns = 0) {
     if (!ready_) return;
     H<Handler> h{handler};
+    const int64_t now = ns ? ns : getns();
     // 1. timers (Core::pollTime, Core.h:710-748)
-    wheel_.tick((uint32_t)((ns ? ns : getns()) >> 20), [&](TimerNode* n) { onTimer(h, n); });
-    // 2./3. RX batch: classify on the GPU, dispatch in ring order
-    const uint32_t n = link_.fill(be_.rxSlots(), Backend::kStride, Backend::kFrameOff, kRxBatch);
+    wheel_.tick((uint32_t)(now >> 20), [&](TimerNode* n) { onTimer(h, n); });
+    // 2./3. RX batch: classify on the GPU, dispatch in ring order.  With a latency budget the
+    // frames of several polls accumulate in the ring (timers and TX still run every poll) until
+    // the ring is full or the oldest has waited the budget: one launch per budget instead of
+    // one per poll.
+    const uint32_t got = link_.fill(be_.rxSlots() + (size_t)rx_pending_ * Backend::kStride, Backend::kStride,
+                                    Backend::kFrameOff, kRxBatch - rx_pending_);
+    if (got && rx_pending_ == 0) rx_first_ns_ = now;
+    rx_pending_ += got;
+    const bool due = rx_pending_ == kRxBatch || now - rx_first_ns_ >= (int64_t)kRxBudgetUs * 1000;
+    const uint32_t n = due ? rx_pending_ : 0;
     if (n) {
+      rx_pending_ = 0;
       if (dirty_ && Backend::kSnapshot) {
         if ((err_ = be_.syncTable(table_))) return;
       }
@@ -544,7 +558,7 @@ class GpuTcpServer {
       c.fin_sent_ = c.fin_received_ = true;
       tws_[i].timer.owner = kMaxConn + i;
     }
-    tx_n_ = 0;
+    tx_n_ = rx_pending_ = 0;
     dirty_ = true;
     ready_ = true;
     err_ = nullptr;
@@ -1045,7 +1059,8 @@ class GpuTcpServer {
   std::vector<Conn> conns_;
   std::vector<Tw> tws_;
   std::vector<uint32_t> free_conns_, free_tws_;
-  uint32_t conn_cnt_ = 0, tw_cnt_ = 0, tx_n_ = 0;
+  uint32_t conn_cnt_ = 0, tw_cnt_ = 0, tx_n_ = 0, rx_pending_ = 0;
+  int64_t rx_first_ns_ = 0;
   uint32_t local_ip_ = 0, rst_ack_ = 0;
   uint16_t port_be_ = 0;
   uint8_t local_mac_[6] = {};

@@ -45,6 +45,11 @@ struct PeerConf {
   };
 };
 
+// the same with received frames held up to 3 ms for a fuller GPU batch
+struct PeerConfBudget : PeerConf {
+  static const uint32_t RxLatencyBudgetUs = 3000;
+};
+
 static const int64_t kT0 = (int64_t)777777 << 20;
 
 enum Kind : uint8_t { kFinEnd, kRstEnd, kIdle, kServerFin };
@@ -291,9 +296,9 @@ struct PeerHandler {
   void onSendTimeout(Conn& c) { line("send timeout", c); }
 };
 
-template <class Backend>
+template <class Backend, class Conf = PeerConf>
 struct Run {
-  using Server = GpuTcpServer<PeerConf, PeerLink, Backend>;
+  using Server = GpuTcpServer<Conf, PeerLink, Backend>;
   std::unique_ptr<Server> srv = std::make_unique<Server>();
   std::string log;
   uint32_t polls = 0;
@@ -413,16 +418,16 @@ static int check(const char* tag, R& r) {
   return fail;
 }
 
-int main(int argc, char** argv) {
-  const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
-  const auto pop = population();
+template <class Conf>
+static int scenario(bool gpu, const std::vector<Client>& pop, const char* name) {
   int fail = 0;
-  Run<OracleBackend> twin;
-  if (!twin.go(pop)) return 3;
+  Run<OracleBackend, Conf> twin;
+  if (!twin.go(pop)) return 100;
+  std::printf("[%s]\n", name);
   fail += check("twin", twin);
   if (gpu) {
-    Run<GpuBackend> g;
-    if (!g.go(pop)) return 5;
+    Run<GpuBackend, Conf> g;
+    if (!g.go(pop)) return 100;
     fail += check("gpu", g);
     const auto &a = g.srv->link().out, &b = twin.srv->link().out;
     size_t same = 0;
@@ -434,6 +439,14 @@ int main(int argc, char** argv) {
     std::printf("gpu: handler log %s, TX frames %s (%zu)\n", g.log == twin.log ? "identical" : "DIFFERENT",
                 frames_eq ? "identical" : "DIFFERENT", a.size());
   }
+  return fail;
+}
+
+int main(int argc, char** argv) {
+  const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
+  const auto pop = population();
+  int fail = scenario<PeerConf>(gpu, pop, "classify every poll");
+  fail += scenario<PeerConfBudget>(gpu, pop, "3-ms RX latency budget");
   std::printf("%s\n", fail ? "FAIL" : "PASS");
   return fail ? 1 : 0;
 }
