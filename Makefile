@@ -31,12 +31,13 @@ STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
 SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
+CLISRVTEST = tests/cpp/test_tcp_client_server
 
-all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
+all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
-$(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp \
+$(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp include/pollnet_amd/rx_ring.hpp $(HDRS) $(LIB) $(ORACLE) \
   oracle/_ref/tcpserver_handler.inc
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
@@ -45,9 +46,20 @@ $(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/s
 oracle/_ref/tcpserver_handler.inc:
 	$(MAKE) ref
 
+# GpuTcpClient <-> GpuTcpServer running both reference example handlers over a lossy in-memory wire
+$(CLISRVTEST): tests/cpp/test_tcp_client_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
+  include/pollnet_amd/tcp_client.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp \
+  include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) \
+  oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
+	$(HIPCC) -O2 -std=c++17 -Wall -Wno-unused-function -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+oracle/_ref/tcpclient_handler.inc:
+	$(MAKE) ref
+
 # GpuTcpServer against reactive in-memory TCP peers (loss, timers, windows), GPU vs twin
 $(PEERTEST): tests/cpp/test_tcp_server_peer.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
-  include/pollnet_amd/tcp_server.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+  include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
@@ -105,6 +117,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST)
+	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 .PHONY: all ref clean

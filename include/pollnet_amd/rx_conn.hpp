@@ -82,6 +82,21 @@ class RxConn {
     last_ack_seq_ = recv_buf_seq_; // the SYN-ACK acknowledged the SYN
   }
 
+  // A fresh connection before any SYN was received (TcpConn::reset, TcpConn.h:150-153): stream
+  // offset 0, nothing owed, the ack field 0 — what a client's SYN carries.
+  void resetRecv() {
+    recv_buf_seq_ = 0;
+    n_segs_ = 1;
+    segs_[0] = {0, 0};
+    fin_received_ = fin_sent_ = false;
+    closed_ = false;
+    pending_ack_ = false;
+    has_ts_ = false;
+    last_ack_seq_ = 0;
+  }
+  // The last ACK sent (a client's SYN carried ack 0 before the SYN-ACK set recv_buf_seq).
+  void setLastAckSeq(uint32_t s) { last_ack_seq_ = s; }
+
   // TX side: an ACK carrying ackSeq() went out (TcpConn::updateLastAck, TcpConn.h:844-849).
   void ackSent() {
     pending_ack_ = false;

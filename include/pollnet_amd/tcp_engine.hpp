@@ -1,0 +1,1057 @@
+// tcp_engine.hpp — the TCP endpoint engine under GpuTcpServer / GpuTcpClient.
+//
+// pollnet's efvitcp endpoints (TcpServer.h, TcpClient.h over Core<Conf> and TcpConn<Conf>)
+// run per poll: one timer tick (Core::pollTime, Core.h:710-748), then Core::pollNet over
+// the RX events (Core.h:494-552) with the endpoint's recv handler, TcpConn::onPack for
+// segments of known connections (TcpConn.h:466-769), and every frame they send finalised
+// with its checksums (SendBuf::setOptDataLen, Core.h:157-163).  TcpEngine does the same
+// with the per-frame work on the GPU:
+//   - the link's pending frames land in a pinned ring; ONE pn_classify launch parses them,
+//     verifies both checksums and probes the conn table for the whole batch;
+//   - the records are walked in ring order on the host: the NIC filter, the checksum discard
+//     a NIC applies, TIME_WAIT (Core.h:510-524), then the endpoint's own branches for unknown
+//     flows and unestablished connections (Derived::onMiss / Derived::onHandshake: a server's
+//     SYN accept and SYN-RECEIVED, a client's SYN-SENT), then onPack — its receive half is
+//     RxConn (rx_conn.hpp), its ACK-field / send half is here;
+//   - every frame the poll built gets its IP and TCP checksums from ONE pn_tx_fill launch
+//     over the pinned TX batch and leaves through the link in generation order.
+// The table snapshot on the device is refreshed before each classify; records after a table
+// change within the same batch are re-resolved on the host (one ordered probe), so every
+// frame sees the table the reference's sequential loop would have shown it.
+//
+// Send side: the reference's segment ring (ConnSendBufCnt segments of up to SMSS bytes,
+// TcpConn.h:58-90, 232-256), window, RTO / fast retransmit and delayed ACK, restated for
+// pollnet's configuration (EfviTcp.h:21-36, 180-199: no window scaling, no timestamps, no
+// congestion window).  Time: now_ts = ns >> 20 (Core.h:46), from `ns` or CLOCK_REALTIME.
+#pragma once
+
+#include <arpa/inet.h>
+#include <net/if.h>
+#include <netinet/in.h>
+#include <sys/ioctl.h>
+#include <sys/socket.h>
+#include <cstdio>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <type_traits>
+#include <utility>
+#include <vector>
+
+#include "gpu_rx.hpp"
+#include "rx_conn.hpp"
+#include "rx_ring.hpp"
+
+namespace pollnet_amd {
+
+// ---------------------------------------------------------------------------
+// Optional Conf members / handler callbacks, detected by name.
+namespace srv_detail {
+#define PN_CONF_OPT(name, type, dflt)                                                               \
+  template <class C, class = void>                                                                  \
+  struct opt_##name {                                                                               \
+    static constexpr type value = dflt;                                                             \
+  };                                                                                                \
+  template <class C>                                                                                \
+  struct opt_##name<C, decltype(void(C::name))> {                                                   \
+    static constexpr type value = C::name;                                                          \
+  };
+PN_CONF_OPT(SendTimeoutSec, uint32_t, 0)
+PN_CONF_OPT(RecvTimeoutSec, uint32_t, 0)
+PN_CONF_OPT(ConnSendBufCnt, uint32_t, 1024) // EfviTcp.h:181
+PN_CONF_OPT(RxBatch, uint32_t, 512)         // frames per poll (RecvBufCnt = 512, EfviTcp.h:186)
+PN_CONF_OPT(RxLatencyBudgetUs, uint32_t, 0) // hold received frames up to this long for a fuller batch
+PN_CONF_OPT(TxBatch, uint32_t, 1024)        // frames per pn_tx_fill launch
+PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
+PN_CONF_OPT(Device, int, 0)
+PN_CONF_OPT(ReferenceLiteralTable, bool, false) // PN_TABLE_REFERENCE_LITERAL: the reference's rehash, defect kept
+PN_CONF_OPT(ConnRetrySec, uint32_t, 0)          // client: reconnect interval (EfviTcp.h:94-98), 0 = never
+#undef PN_CONF_OPT
+
+#define PN_HANDLER_OPT(name, call)                                                                   \
+  template <class H, class C, class = void>                                                          \
+  struct has_##name : std::false_type {};                                                            \
+  template <class H, class C>                                                                        \
+  struct has_##name<H, C, decltype(void(std::declval<H&>().call))> : std::true_type {};
+PN_HANDLER_OPT(onTcpConnected, onTcpConnected(std::declval<C&>()))
+PN_HANDLER_OPT(onTcpDisconnect, onTcpDisconnect(std::declval<C&>()))
+PN_HANDLER_OPT(onSendTimeout, onSendTimeout(std::declval<C&>()))
+PN_HANDLER_OPT(onRecvTimeout, onRecvTimeout(std::declval<C&>()))
+PN_HANDLER_OPT(allowNewConnection, allowNewConnection(uint32_t(0), uint16_t(0)))
+PN_HANDLER_OPT(onTcpConnectFailed, onTcpConnectFailed())
+#undef PN_HANDLER_OPT
+
+template <class C, class = void>
+struct user_data {
+  struct type {};
+};
+template <class C>
+struct user_data<C, std::void_t<typename C::UserData>> {
+  using type = typename C::UserData;
+};
+
+inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] << 8 | p[1]); }
+inline uint32_t rd32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+inline void wr16(uint8_t* p, uint16_t v) {
+  p[0] = (uint8_t)(v >> 8);
+  p[1] = (uint8_t)v;
+}
+inline void wr32(uint8_t* p, uint32_t v) {
+  wr16(p, (uint16_t)(v >> 16));
+  wr16(p + 2, (uint16_t)v);
+}
+} // namespace srv_detail
+
+// ---------------------------------------------------------------------------
+// Hashed timer wheel with efvitcp's semantics (Core.h:184-200, 684-748): 256 one-tick
+// slots plus 256 slots of 256 ticks, LIFO within a slot, advanced one tick per call.
+struct TimerNode {
+  TimerNode* prev = this;
+  TimerNode* next = this;
+  uint32_t owner = 0; // conn id (< MaxConnCnt) or MaxConnCnt + tw id
+  uint32_t kind = 0;  // 0 resend, 1 delayed ACK, 2 + user timer id; TIME_WAIT nodes: 0
+  uint32_t expire = 0;
+  TimerNode() = default;
+  TimerNode(const TimerNode&) : TimerNode() {} // nodes are never copied linked
+  TimerNode& operator=(const TimerNode&) { return *this; }
+  bool unlinked() const { return prev == this; }
+  void unlink() {
+    prev->next = next;
+    next->prev = prev;
+    prev = next = this;
+  }
+};
+
+class TimerWheel {
+ public:
+  static constexpr uint32_t kSlots = 256;
+  TimerWheel() = default;
+  TimerWheel(const TimerWheel&) = delete;
+  TimerWheel& operator=(const TimerWheel&) = delete;
+
+  uint32_t now() const { return now_; }
+  void reset(uint32_t now_ts) {
+    now_ = now_ts;
+    for (auto& s : near_) s.prev = s.next = &s;
+    for (auto& s : far_) s.prev = s.next = &s;
+  }
+  void add(uint32_t dur, TimerNode* n) {
+    TimerNode* slot;
+    if (dur <= kSlots) {
+      slot = &near_[(now_ + dur) % kSlots];
+    } else {
+      dur = std::min(dur, kSlots * (kSlots + 1) - 1 - (now_ % kSlots));
+      n->expire = now_ + dur;
+      slot = &far_[n->expire / kSlots % kSlots];
+    }
+    n->next = slot->next;
+    n->prev = slot;
+    slot->next->prev = n;
+    slot->next = n;
+  }
+  // One tick if ts moved (time never goes back); fire(node) for each expired node, unlinked.
+  template <class Fire>
+  void tick(uint32_t ts, Fire&& fire) {
+    if (ts == now_) return;
+    if (++now_ % kSlots == 0) { // cascade the far slot that comes due
+      TimerNode* slot = &far_[now_ / kSlots % kSlots];
+      for (TimerNode* n = slot->next; n != slot;) {
+        TimerNode* nx = n->next;
+        n->prev = n->next = n;
+        add(n->expire - now_, n);
+        n = nx;
+      }
+      slot->prev = slot->next = slot;
+    }
+    TimerNode* slot = &near_[now_ % kSlots];
+    if (slot->unlinked()) return;
+    TimerNode due; // detach the slot so timers re-armed while firing land in a later tick
+    due.next = slot->next;
+    due.prev = slot->prev;
+    slot->next->prev = &due;
+    slot->prev->next = &due;
+    slot->prev = slot->next = slot;
+    while (due.next != &due) {
+      TimerNode* n = due.next;
+      n->unlink();
+      fire(n);
+    }
+  }
+
+ private:
+  uint32_t now_ = 0;
+  TimerNode near_[kSlots], far_[kSlots];
+};
+
+// ---------------------------------------------------------------------------
+// Links: where received frames come from and where built frames go.
+//   const char* open(const char* interface)       (nullptr = ok)
+//   uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t frame_off, uint32_t cap)
+//   void send(const uint8_t* eth, uint32_t len)
+//   uint32_t localIp() (network order), const uint8_t* localMac()
+//   const char* resolveMac(uint32_t ip_be, uint8_t* mac)   (clients: the next hop's MAC)
+//
+// SocketLink: an AF_PACKET socket on `interface` (pollnet's SocketEthReceiver,
+// Socket.h:567-629, drained by recvmmsg into the pinned ring) that also transmits the
+// built frames.  Needs CAP_NET_RAW; the host stack must be kept off the server port
+// (e.g. a firewall drop), as with any user-space TCP stack on a shared interface.
+class SocketLink {
+ public:
+  const char* open(const char* interface) {
+    int fd = ::socket(AF_INET, SOCK_DGRAM, 0);
+    if (fd < 0) return "socket(AF_INET) failed";
+    ifreq ifr;
+    std::memset(&ifr, 0, sizeof ifr);
+    std::strncpy(ifr.ifr_name, interface, IFNAMSIZ - 1);
+    ifr.ifr_addr.sa_family = AF_INET;
+    int rc = ioctl(fd, SIOCGIFADDR, &ifr); // Core.h:258-264
+    if (rc == 0) local_ip_ = ((sockaddr_in*)&ifr.ifr_addr)->sin_addr.s_addr;
+    if (rc == 0 && (rc = ioctl(fd, SIOCGIFHWADDR, &ifr)) == 0) std::memcpy(mac_, ifr.ifr_hwaddr.sa_data, 6);
+    ::close(fd);
+    if (rc != 0) return "ioctl SIOCGIFADDR/SIOCGIFHWADDR failed";
+    if (!rx_.init(interface)) return rx_.getLastError();
+    return nullptr;
+  }
+  uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t frame_off, uint32_t cap) {
+    return rx_.fill(slots, stride, frame_off, cap);
+  }
+  void send(const uint8_t* eth, uint32_t len) { (void)::send(rx_.fd(), eth, len, MSG_DONTWAIT); }
+  uint32_t localIp() const { return local_ip_; }
+  const uint8_t* localMac() const { return mac_; }
+  // The MAC of the next hop toward ip (TcpClient::getDestMac, TcpClient.h:100-152): the gateway
+  // `ip route get` names (or ip itself when on-link), looked up in the kernel's ARP table.
+  const char* resolveMac(uint32_t ip_be, uint8_t* mac) {
+    char ip[INET_ADDRSTRLEN], cmd[96], line[512], hop[64] = "";
+    inet_ntop(AF_INET, &ip_be, ip, sizeof ip);
+    std::snprintf(cmd, sizeof cmd, "/usr/sbin/ip route get %s", ip);
+    FILE* p = popen(cmd, "r");
+    if (!p) return "ip route get failed";
+    while (!hop[0] && fgets(line, sizeof line, p)) {
+      const char* via = std::strstr(line, " via ");
+      if (std::sscanf(via ? via + 5 : line, "%63s", hop) != 1) hop[0] = 0;
+    }
+    pclose(p);
+    if (!hop[0]) return "no route to the server";
+    FILE* arp = std::fopen("/proc/net/arp", "r");
+    if (!arp) return "cannot open /proc/net/arp";
+    bool found = false;
+    char aip[64], hw[64];
+    while (!found && fgets(line, sizeof line, arp)) {
+      unsigned m[6];
+      if (std::sscanf(line, "%63s %*s %*s %63s", aip, hw) == 2 && std::strcmp(aip, hop) == 0 &&
+          std::sscanf(hw, "%x:%x:%x:%x:%x:%x", &m[0], &m[1], &m[2], &m[3], &m[4], &m[5]) == 6) {
+        for (int i = 0; i < 6; i++) mac[i] = (uint8_t)m[i];
+        found = true;
+      }
+    }
+    std::fclose(arp);
+    return found ? nullptr : "next hop not in the ARP table";
+  }
+
+ private:
+  SocketEthBatcher rx_;
+  uint32_t local_ip_ = 0;
+  uint8_t mac_[6] = {};
+};
+
+// ---------------------------------------------------------------------------
+// GpuBackend: the per-frame work on the GPU.  The RX ring and the TX batch are pinned
+// host memory read in place by the kernels (zero copy: only each frame's own lines
+// cross PCIe, GpuRx::Mode::ZeroCopy).
+class GpuBackend {
+ public:
+  static constexpr bool kSnapshot = true; // records are classified against a table snapshot
+  static constexpr uint32_t kStride = 2048, kFrameOff = 2;
+
+  GpuBackend() = default;
+  GpuBackend(const GpuBackend&) = delete;
+  GpuBackend& operator=(const GpuBackend&) = delete;
+  ~GpuBackend() {
+    if (rx_ring_) (void)hipHostFree(rx_ring_);
+    if (tx_ring_) (void)hipHostFree(tx_ring_);
+  }
+
+  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap) {
+    if (const char* e = rx_.init(device, kStride, kFrameOff, rx_cap, GpuRx::Mode::ZeroCopy)) return e;
+    if (hipHostMalloc((void**)&rx_ring_, (size_t)kStride * rx_cap, hipHostMallocDefault) != hipSuccess)
+      return "hipHostMalloc(rx ring) failed";
+    if (hipHostMalloc((void**)&tx_ring_, (size_t)kStride * tx_cap, hipHostMallocDefault) != hipSuccess)
+      return "hipHostMalloc(tx batch) failed";
+    std::memset(rx_ring_, 0, (size_t)kStride * rx_cap);
+    std::memset(tx_ring_, 0, (size_t)kStride * tx_cap);
+    return nullptr;
+  }
+  uint8_t* rxSlots() { return rx_ring_; }
+  uint8_t* txSlots() { return tx_ring_; }
+  const char* syncTable(const ConnTable& t) { return rx_.syncTable(t); }
+  // f(key, rec, eth) for the n frames of the RX ring, in ring order.
+  template <class F>
+  const char* classify(uint32_t n, const ConnTable& t, F&& f) {
+    return rx_.pollBatch(
+        rx_ring_, n, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
+        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
+  }
+  // IP + TCP checksums of the first n TX slots (PN_TX_TCP: SendBuf::setOptDataLen, Core.h:157-163).
+  const char* fillTx(uint32_t n) {
+    if (pn_tx_fill(rx_.ctx(), tx_ring_, kStride, kFrameOff, n, nullptr, PN_TX_TCP, rx_.stream()))
+      return pn_last_error(rx_.ctx());
+    if (hipStreamSynchronize(rx_.stream()) != hipSuccess) return "hipStreamSynchronize(tx_fill) failed";
+    return nullptr;
+  }
+
+ private:
+  GpuRx rx_;
+  uint8_t* rx_ring_ = nullptr;
+  uint8_t* tx_ring_ = nullptr;
+};
+
+
+// ---------------------------------------------------------------------------
+// TcpEngine<Conf, IConf, Link, Backend, Derived>: connections, timers, segments, frames.
+//   IConf   MaxConnCnt / MaxTimeWaitConnCnt / ConnRecvBufSize / TimestampOption (the efvitcp
+//           Conf the pollnet wrapper derives, EfviTcp.h:21-36, 180-199)
+//   Derived (CRTP) supplies the endpoint's branches:
+//     static constexpr bool kClient;
+//     bool accepts(const uint8_t* eth)                                   the NIC filter
+//     template <class HH> void onMiss(HH&, uint64_t key, const pn_result&, const uint8_t* eth)
+//     template <class HH> bool onHandshake(HH&, Conn&, const pn_result&, const uint8_t* eth)
+//                                   (an unestablished connection's segment; true: go on to onPack)
+template <class Conf, class IConfT, class Link, class Backend, class Derived>
+class TcpEngine {
+ public:
+  using IConf = IConfT;
+  static constexpr uint32_t kMaxConn = IConf::MaxConnCnt;
+  static constexpr uint32_t kMaxTw = IConf::MaxTimeWaitConnCnt;
+  static constexpr uint32_t kSendBufCnt = srv_detail::opt_ConnSendBufCnt<Conf>::value;
+  static constexpr uint32_t kSendMTU = 1024 - 28;      // SendBuf1K: SendBufSize - offsetof(ip_hdr), Core.h:232-234
+  static constexpr uint32_t kSegCap = kSendMTU - 40;   // largest SMSS (onSyn's clamp, TcpConn.h:357)
+  static constexpr uint32_t kSynRetries = 3, kTcpRetries = 10, kMinRtoMS = 100, kMaxRtoMS = 30 * 1000;
+  static constexpr uint32_t kDelayedAckMS = srv_detail::opt_DelayedAckMS<Conf>::value;
+  static constexpr uint32_t kTimeWaitTimeout = 60 * 1000; // Core.h:48
+  static constexpr uint32_t kRxBatch = srv_detail::opt_RxBatch<Conf>::value;
+  static constexpr uint32_t kTxBatch = srv_detail::opt_TxBatch<Conf>::value;
+  static constexpr uint32_t kRxBudgetUs = srv_detail::opt_RxLatencyBudgetUs<Conf>::value;
+  static constexpr uint32_t kSendTimeoutMs = srv_detail::opt_SendTimeoutSec<Conf>::value * 1000;
+  static constexpr uint32_t kRecvTimeoutMs = srv_detail::opt_RecvTimeoutSec<Conf>::value * 1000;
+  static_assert(kSendBufCnt >= 4 && !(kSendBufCnt & (kSendBufCnt - 1)), "ConnSendBufCnt must be a power of 2");
+  static_assert(Conf::RecvBufSize >= 2 * 1460, "RecvBufSize below two RMSS");
+
+  class Conn : public srv_detail::user_data<Conf>::type {
+   public:
+    const char* err_ = nullptr; // EfviTcp.h:54 / 197 (UserData::err_)
+
+    uint32_t getConnId() const { return id_; }
+    void getPeername(sockaddr_in& addr) const { // TcpConn.h:37-41
+      addr.sin_addr.s_addr = peer_ip_;
+      addr.sin_port = peer_port_;
+    }
+    bool isEstablished() const { return established_; }
+    bool isConnected() const { return established_; }
+    bool isClosed() const { return fin_received_ && !established_; } // TcpConn.h:45
+    const char* getLastError() const { return err_; }
+    void close(const char* reason) { // EfviTcp.h:61-64, 230-233
+      err_ = reason;
+      eng_->closeConn(*this);
+    }
+    // EfviTcpClient::Conn::writeSome (EfviTcp.h:66-70): send, and re-arm the send timeout.
+    int writeSome(const void* data, uint32_t size, bool more = false) {
+      const int ret = (int)send(data, size, more);
+      if (kSendTimeoutMs) setUserTimer(0, kSendTimeoutMs);
+      return ret;
+    }
+    // All or nothing, else the connection is closed: EfviTcp.h:73-79 (client: through
+    // writeSome, the timer re-armed either way) and 236-244 (server: re-armed on success).
+    bool writeNonblock(const void* data, uint32_t size, bool more = false) {
+      if constexpr (Derived::kClient) {
+        if ((uint32_t)writeSome(data, size, more) != size) {
+          close("send buffer full");
+          return false;
+        }
+      } else {
+        if (send(data, size, more) != size) {
+          close("send buffer full");
+          return false;
+        }
+        if (kSendTimeoutMs) setUserTimer(0, kSendTimeoutMs);
+      }
+      return true;
+    }
+    // TcpConn::send (TcpConn.h:58-61): bytes accepted into the send buffer.
+    uint32_t send(const void* data, uint32_t size, bool more = false) {
+      if (fin_sent_) return 0;
+      return eng_->sendPartial(*this, (const uint8_t*)data, size, !more);
+    }
+    uint32_t getSendable() const { // TcpConn.h:47-50
+      if (fin_sent_) return 0;
+      return (send_una_ + kSendBufCnt - 1 - data_next_) * smss_ - data_next_size_;
+    }
+    void sendFin() { eng_->sendFin(*this); }
+    void setUserTimer(uint32_t timer_id, uint32_t duration_ms) { eng_->setUserTimer(*this, timer_id, duration_ms); }
+
+   private:
+    friend class TcpEngine;
+    friend Derived;
+    struct Seg {
+      uint32_t seq = 0;
+      uint32_t send_ts = 0;
+      uint16_t len = 0; // payload bytes
+      bool fin = false;
+      bool syn_ack = false; // the SYN segment carried ACK (a server's SYN-ACK)
+    };
+    Seg& seg(uint32_t idx) { return segs_[idx & (kSendBufCnt - 1)]; }
+    uint8_t* segData(uint32_t idx) { return data_.get() + (size_t)(idx & (kSendBufCnt - 1)) * kSegCap; }
+
+    TcpEngine* eng_ = nullptr;
+    uint32_t id_ = 0;
+    uint64_t key_ = 0;
+    uint32_t peer_ip_ = 0;     // network order
+    uint16_t peer_port_ = 0;   // network order
+    uint16_t local_port_ = 0;  // network order
+    uint8_t peer_mac_[6] = {};
+    RxConn<IConf> rx_;
+    // send side (TcpConn.h:861-898)
+    std::unique_ptr<Seg[]> segs_;
+    std::unique_ptr<uint8_t[]> data_;
+    uint32_t send_una_ = 0, send_next_ = 0, data_next_ = 0, data_next_size_ = 0, recover_ = 0;
+    uint32_t smss_ = 536, send_wnd_seq_ = 0, rto_ = 1000, srtt_ = 0, rttvar_ = 0, dup_ack_cnt_ = 0, retries_ = 0;
+    bool established_ = false, fin_sent_ = true, fin_received_ = true, fast_re_ = false, in_recover_ = false;
+    TimerNode timers_[4]; // resend, delayed ACK, user 0 (send timeout), user 1 (recv timeout)
+  };
+
+  TcpEngine() : conns_(kMaxConn), tws_(kMaxTw) {}
+  TcpEngine(const TcpEngine&) = delete;
+  TcpEngine& operator=(const TcpEngine&) = delete;
+
+  Link& link() { return link_; }
+  // Drop checksum-failed frames before they touch any state (what the NIC's RX checksum
+  // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.
+  void setDropBadChecksum(bool drop) { drop_bad_ = drop; }
+  const ConnTable& table() const { return table_; }
+  uint32_t nowTs() const { return wheel_.now(); }
+  // Frames built since the last flush (checksums not yet filled).
+  uint32_t pendingTx() const { return tx_n_; }
+  // Fill the pending frames' checksums (one pn_tx_fill launch) and send them in order.
+  const char* flushTx() {
+    if (!tx_n_) return nullptr;
+    const char* e = be_.fillTx(tx_n_);
+    if (e) {
+      err_ = e;
+    } else {
+      for (uint32_t i = 0; i < tx_n_; i++) {
+        const uint8_t* f = be_.txSlots() + (size_t)i * Backend::kStride + Backend::kFrameOff;
+        link_.send(f, 14 + srv_detail::rd16(f + 16));
+      }
+    }
+    tx_n_ = 0;
+    return e;
+  }
+
+ protected:
+  struct Tw { // Core.h:186-197 TimeWaitConn
+    uint64_t key = 0;
+    uint8_t peer_mac[6] = {};
+    uint32_t peer_ip = 0;
+    uint16_t peer_port = 0, local_port = 0;
+    uint32_t seq_num = 0, ack_num = 0;
+    TimerNode timer;
+  };
+
+  // The pollnet wrapper's TmpHandler (EfviTcp.h:107-147 client, 264-307 server): the reference's
+  // event callbacks mapped onto the user's handler; callbacks it does not define are skipped.
+  template <class Handler>
+  struct H {
+    Handler& u;
+    void connected(Conn& c) {
+      if constexpr (srv_detail::has_onTcpConnected<Handler, Conn>::value) u.onTcpConnected(c);
+    }
+    void disconnect(Conn& c) {
+      if constexpr (srv_detail::has_onTcpDisconnect<Handler, Conn>::value) u.onTcpDisconnect(c);
+    }
+    void connectFailed() {
+      if constexpr (srv_detail::has_onTcpConnectFailed<Handler, Conn>::value) u.onTcpConnectFailed();
+    }
+    void sendTimeout(Conn& c) {
+      if constexpr (srv_detail::has_onSendTimeout<Handler, Conn>::value) u.onSendTimeout(c);
+    }
+    void recvTimeout(Conn& c) {
+      if constexpr (srv_detail::has_onRecvTimeout<Handler, Conn>::value) u.onRecvTimeout(c);
+    }
+    bool allow(uint32_t ip_be, uint16_t port_be) {
+      if constexpr (srv_detail::has_allowNewConnection<Handler, Conn>::value) return u.allowNewConnection(ip_be, port_be);
+      return true;
+    }
+    uint32_t data(Conn& c, const uint8_t* d, uint32_t n) { return u.onTcpData(c, d, n); }
+  };
+
+  Derived& self() { return static_cast<Derived&>(*this); }
+
+  static int64_t getns() {
+    timespec ts;
+    ::clock_gettime(CLOCK_REALTIME, &ts);
+    return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+  }
+
+  // Core::init's state (Core.h:253-330): local address, table, id stacks, timer wheel, buffers.
+  const char* initEngine(const char* local_ip, int64_t now_ns) {
+    closeAll();
+    ready_ = false;
+    local_ip_ = link_.localIp();
+    if (local_ip && std::strcmp(local_ip, "0.0.0.0") != 0) {
+      in_addr a;
+      if (inet_pton(AF_INET, local_ip, &a) != 1) return "invalid local ip";
+      local_ip_ = a.s_addr;
+    }
+    std::memcpy(local_mac_, link_.localMac(), 6);
+    if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
+    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch)) return e;
+    free_conns_.clear();
+    for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i
+    free_tws_.clear();
+    for (uint32_t i = kMaxTw; i-- > 0;) free_tws_.push_back(i);
+    conn_cnt_ = tw_cnt_ = 0;
+    for (auto& c : conns_) // unlink before the wheel's heads are reset
+      for (auto& t : c.timers_) t.unlink();
+    for (auto& tw : tws_) tw.timer.unlink();
+    wheel_.reset((uint32_t)(now_ns >> 20));
+    for (uint32_t i = 0; i < kMaxConn; i++) {
+      Conn& c = conns_[i];
+      c.eng_ = this;
+      c.id_ = i;
+      if (!c.segs_) {
+        c.segs_.reset(new typename Conn::Seg[kSendBufCnt]);
+        c.data_.reset(new uint8_t[(size_t)kSendBufCnt * kSegCap]);
+      }
+      for (uint32_t k = 0; k < 4; k++) {
+        c.timers_[k].owner = i;
+        c.timers_[k].kind = k;
+      }
+      c.established_ = false;
+      c.fin_sent_ = c.fin_received_ = true;
+    }
+    for (uint32_t i = 0; i < kMaxTw; i++) tws_[i].timer.owner = kMaxConn + i;
+    tx_n_ = rx_pending_ = 0;
+    dirty_ = true;
+    ready_ = true;
+    return nullptr;
+  }
+
+  void closeAll() { // TcpServer::close / TcpClient::close: close() every connection (RST if established)
+    if (!ready_) return;
+    for (auto& c : conns_)
+      if (c.eng_ && !c.isClosed()) closeConn(c);
+    flushTx();
+  }
+
+  // One poll: a timer tick, the RX batch (classified on the GPU, dispatched in ring order),
+  // the TX batch (checksums on the GPU).  With a latency budget the frames of several polls
+  // accumulate in the ring (timers and TX still run every poll) until the ring is full or
+  // the oldest has waited the budget: one launch per budget instead of one per poll.
+  template <class HH>
+  void pollEngine(HH& h, int64_t now) {
+    wheel_.tick((uint32_t)(now >> 20), [&](TimerNode* n) { onTimer(h, n); }); // Core::pollTime
+    const uint32_t got = link_.fill(be_.rxSlots() + (size_t)rx_pending_ * Backend::kStride, Backend::kStride,
+                                    Backend::kFrameOff, kRxBatch - rx_pending_);
+    if (got && rx_pending_ == 0) rx_first_ns_ = now;
+    rx_pending_ += got;
+    const bool due = rx_pending_ == kRxBatch || now - rx_first_ns_ >= (int64_t)kRxBudgetUs * 1000;
+    const uint32_t n = due ? rx_pending_ : 0;
+    if (n) {
+      rx_pending_ = 0;
+      if (dirty_ && Backend::kSnapshot) {
+        if ((err_ = be_.syncTable(table_))) return;
+      }
+      dirty_ = false;
+      const char* e = be_.classify(n, table_, [&](uint64_t key, const pn_result& r, const uint8_t* eth) {
+        onFrame(h, key, r, eth);
+      });
+      if (e) err_ = e;
+    }
+    flushTx();
+  }
+
+  // ---- one received frame (Core::pollNet RX branch + the endpoint's recv handler) ----
+  template <class HH>
+  void onFrame(HH& h, uint64_t key, const pn_result& rec, const uint8_t* eth) {
+    if (rec.flags & (PN_F_NOT_TCP | PN_F_TRUNC | PN_F_BADOFF)) return;
+    if (!self().accepts(eth)) return; // the NIC filter (Core.h:335-383)
+    if (drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
+    pn_result r = rec;
+    if (dirty_ && Backend::kSnapshot) { // the table changed earlier in this batch: probe the live one
+      uint32_t conn_id = PN_MISS;
+      const bool hit = table_.find(key, nullptr, &conn_id);
+      r.conn_id = conn_id;
+      r.flags = (uint16_t)((r.flags & ~(PN_F_HIT | PN_F_TW)) | (hit ? PN_F_HIT : 0) |
+                           (hit && conn_id >= kMaxConn ? PN_F_TW : 0));
+    }
+    if (r.flags & PN_F_TW) { // Core.h:510-524
+      Tw& tw = tws_[r.conn_id - kMaxConn];
+      const bool seq_expected = seqRaw(r) == tw.ack_num;
+      if (r.flags & PN_F_RST) {
+        if (seq_expected) {
+          tw.timer.unlink();
+          delEntry(key);
+        }
+      } else if (!seq_expected || segLen(eth, r)) {
+        ackTW(tw);
+      }
+      return;
+    }
+    if (!(r.flags & PN_F_HIT)) {
+      self().onMiss(h, key, r, eth);
+      return;
+    }
+    Conn& c = conns_[r.conn_id];
+    if (!c.established_ && !self().onHandshake(h, c, r, eth)) return;
+    onPack(h, c, eth, r);
+  }
+
+  static uint32_t seqRaw(const pn_result& r) { return r.seq - ((r.flags & PN_F_SYN) ? 1u : 0u); } // rec.seq = seq + syn
+  static uint32_t ackNum(const uint8_t* eth) { return srv_detail::rd32(eth + 34 + 8); }
+  static uint32_t segLen(const uint8_t* eth, const pn_result& r) { // tot_len - 20 - doff*4 + syn + fin
+    const uint32_t tot = srv_detail::rd16(eth + 16), doff = eth[34 + 12] >> 4;
+    return tot - 20 - doff * 4 + ((r.flags & PN_F_SYN) ? 1 : 0) + ((r.flags & PN_F_FIN) ? 1 : 0);
+  }
+
+  // ---- connection setup (TcpConn::reset / onSyn / sendSyn / onEstablished) ----
+  // Take a connection id and a table entry for key (TcpServer.h:88-89, TcpClient.h:67-69).
+  Conn* newConn(uint64_t key) {
+    if (free_conns_.empty()) return nullptr;
+    const uint32_t id = free_conns_.back();
+    free_conns_.pop_back();
+    ++conn_cnt_;
+    table_.add(key, id);
+    dirty_ = true;
+    return &conns_[id];
+  }
+  void resetConn(Conn& c, uint64_t key, const uint8_t* peer_mac, uint32_t peer_ip, uint16_t peer_port,
+                 uint16_t local_port) { // TcpConn.h:150-186
+    c.key_ = key;
+    std::memcpy(c.peer_mac_, peer_mac, 6);
+    c.peer_ip_ = peer_ip;
+    c.peer_port_ = peer_port;
+    c.local_port_ = local_port;
+    c.err_ = nullptr;
+    c.established_ = c.fin_sent_ = c.fin_received_ = c.fast_re_ = c.in_recover_ = false;
+    c.send_una_ = c.send_next_ = c.data_next_size_ = c.dup_ack_cnt_ = c.retries_ = 0;
+    c.data_next_ = 1;
+    c.smss_ = 536;
+    c.rx_.resetRecv();
+    // genISN (TcpConn.h:856-858): connHashKey(peer) + now_ts; keeps send window 0 until established
+    c.send_wnd_seq_ = (uint32_t)key + wheel_.now();
+    c.seg(0).seq = c.send_wnd_seq_;
+  }
+  void onSyn(Conn& c, const uint8_t* eth, const pn_result& r) { // TcpConn.h:339-375
+    const uint8_t* opt = eth + 54;
+    const uint8_t* data = eth + 34 + (eth[46] >> 4) * 4;
+    while (opt < data) {
+      const uint8_t kind = *opt++;
+      if (kind <= 1) continue;
+      const uint8_t len = *opt++;
+      if (kind == 2 && len == 4) c.smss_ = std::min<uint32_t>(kSendMTU - 40, srv_detail::rd16(opt));
+      if (len > 2) opt += len - 2;
+    }
+    c.rx_.open(seqRaw(r));
+    c.fin_received_ = false;
+  }
+  void sendSyn(Conn& c) { // TcpConn.h:197-230: SYN, with ACK when a SYN was received (pending_ack)
+    c.rto_ = 1000;
+    typename Conn::Seg& s = c.seg(c.send_next_);
+    s.len = 0;
+    s.fin = false;
+    s.syn_ack = c.rx_.pendingAck();
+    emit(c, s.seq, s.syn_ack ? kSynAck : kSyn, nullptr, 0);
+    advanceNext(c, 1);
+  }
+  template <class HH>
+  void onEstablished(HH& h, Conn& c, const uint8_t* eth) { // TcpConn.h:377-418
+    c.send_wnd_seq_ = ackNum(eth) + srv_detail::rd16(eth + 34 + 14);
+    c.established_ = true;
+    c.srtt_ = std::max(1u, wheel_.now() - c.seg(c.send_una_).send_ts);
+    c.rttvar_ = c.srtt_ >> 1;
+    updateRto(c);
+    // onConnectionEstablished (EfviTcp.h:131-135, 296-300)
+    if (kSendTimeoutMs) setUserTimer(c, 0, kSendTimeoutMs);
+    if (kRecvTimeoutMs) setUserTimer(c, 1, kRecvTimeoutMs);
+    h.connected(c);
+  }
+  void updateRto(Conn& c) { c.rto_ = std::max(kMinRtoMS, c.srtt_ + std::max(1u, c.rttvar_ << 2)); }
+
+  // ---- segment processing of a connection (TcpConn::onPack) ----
+  template <class HH>
+  struct PackAdapter {
+    TcpEngine& s;
+    HH& h;
+    Conn& c;
+    const uint8_t* eth;
+    uint32_t onData(RxConn<IConf>&, const uint8_t* d, uint32_t n) { // EfviTcp.h:136-139, 301-304
+      if (kRecvTimeoutMs) s.setUserTimer(c, 1, kRecvTimeoutMs);
+      return h.data(c, d, n);
+    }
+    void onFin(RxConn<IConf>&, const uint8_t* d, uint32_t n) { // EfviTcp.h:121-125, 283-288
+      c.fin_received_ = true;
+      if (n) h.data(c, d, n);
+      c.err_ = "remote close";
+      s.closeConn(c); // RST (the wrapper's Conn::close -> TcpConn::close)
+      h.disconnect(c);
+    }
+    void onReset(RxConn<IConf>&) { // onConnectionReset (EfviTcp.h:111-114, 269-272)
+      c.err_ = "connection reset";
+      h.disconnect(c);
+    }
+    void onAckField(RxConn<IConf>&, bool no_text) { s.onAck(c, eth, no_text); }
+  };
+
+  template <class HH>
+  void onPack(HH& h, Conn& c, const uint8_t* eth, const pn_result& r) {
+    PackAdapter<HH> a{*this, h, c, eth};
+    const RxAck ack = c.rx_.onSegment(a, eth, r);
+    if (c.rx_.closed() && !c.isClosed()) { // RST accepted, or receive buffer full (TcpConn.h:526-531, 741-745)
+      if (ack.rst)
+        closeConn(c); // close(): RST to the peer
+      else
+        onClose(c, false);
+      return;
+    }
+    // as in the reference, an ACK still owed is sent even when a callback closed the
+    // connection (a close() sends an RST first, which clears the owed ACK)
+    if (ack.send) sendAck(c, ack.immediate);
+    // TcpConn.h:765-768: both FINs exchanged and everything acknowledged -> TIME_WAIT
+    if (c.fin_sent_ && c.rx_.finReceived() && c.established_ && c.send_una_ == c.data_next_) {
+      c.err_ = "connection closed"; // onConnectionClosed (EfviTcp.h:116-119, 278-281)
+      h.disconnect(c);
+      onClose(c, true);
+    }
+  }
+
+  // Step 5: the ACK field (TcpConn.h:536-665; pollnet: no cwnd, no window scaling).
+  void onAck(Conn& c, const uint8_t* eth, bool no_text) {
+    const uint32_t ack_num = ackNum(eth);
+    bool window_updated = false;
+    if (!c.fin_sent_) {
+      const uint32_t w = ack_num + srv_detail::rd16(eth + 34 + 14);
+      if ((int32_t)(w - c.send_wnd_seq_) > 0) {
+        window_updated = true;
+        c.send_wnd_seq_ = w;
+      }
+    }
+    const uint32_t old_una = c.send_una_;
+    while (c.send_una_ != c.send_next_ && (int32_t)(ack_num - c.seg(c.send_una_ + 1).seq) >= 0) c.send_una_++;
+    if (old_una != c.send_una_) { // new data acknowledged
+      c.dup_ack_cnt_ = 0;
+      c.retries_ = 0;
+      const int rtt = std::max(1, (int)(wheel_.now() - c.seg(old_una).send_ts));
+      c.rttvar_ -= (int)(c.rttvar_ - std::abs(rtt - (int)c.srtt_)) >> 2;
+      c.srtt_ -= (int)(c.srtt_ - rtt) >> 3;
+      updateRto(c);
+      c.timers_[0].unlink();
+      if (c.send_una_ != c.send_next_) wheel_.add(c.rto_, &c.timers_[0]);
+      if (c.in_recover_) {
+        if ((int32_t)(c.send_una_ - c.recover_) < 0) {
+          resendUna(c); // partial ACK
+        } else {
+          if ((int32_t)(c.send_una_ - c.recover_) > 0) c.in_recover_ = false;
+          c.fast_re_ = false;
+        }
+      }
+    } else if (c.send_una_ != c.send_next_ && !window_updated && no_text) { // duplicate ACK
+      if (++c.dup_ack_cnt_ == 3 && !c.in_recover_) {
+        c.fast_re_ = c.in_recover_ = true;
+        c.recover_ = c.send_next_;
+        resendUna(c);
+      }
+    }
+    sendQueued(c);
+  }
+
+  // Transmit queued segments the window now admits (TcpConn.h:646-660).
+  void sendQueued(Conn& c) {
+    while (uint32_t size = (c.data_next_ == c.send_next_ ? c.data_next_size_ : c.smss_)) {
+      typename Conn::Seg& s = c.seg(c.send_next_);
+      if ((int32_t)(s.seq + size - c.send_wnd_seq_) > 0) break;
+      if (c.data_next_ == c.send_next_) {
+        s.fin = c.fin_sent_;
+        s.len = (uint16_t)(size - (s.fin ? 1 : 0));
+        emit(c, s.seq, s.fin ? kFinAck : kData, c.segData(c.send_next_), s.len);
+        advanceData(c);
+      } else {
+        s.len = (uint16_t)size;
+        s.fin = false;
+        emit(c, s.seq, kData, c.segData(c.send_next_), s.len);
+      }
+      advanceNext(c, size);
+    }
+  }
+
+  void advanceNext(Conn& c, uint32_t inc) { // TcpConn.h:327-333
+    typename Conn::Seg& s = c.seg(c.send_next_);
+    s.send_ts = wheel_.now();
+    if (c.send_next_ == c.send_una_) wheel_.add(c.rto_, &c.timers_[0]);
+    const uint32_t seq = s.seq;
+    c.seg(++c.send_next_).seq = seq + inc;
+  }
+  void advanceData(Conn& c) {
+    c.data_next_++;
+    c.data_next_size_ = 0;
+  }
+
+  // TcpConn::sendPartial (TcpConn.h:232-256): append, cut segments at SMSS, send what fits.
+  uint32_t sendPartial(Conn& c, const uint8_t* d, uint32_t size, bool last) {
+    const uint8_t* p = d;
+    while (size && c.send_una_ + kSendBufCnt - 1 != c.data_next_) {
+      const uint32_t n = std::min(c.smss_ - c.data_next_size_, size);
+      std::memcpy(c.segData(c.data_next_) + c.data_next_size_, p, n);
+      p += n;
+      size -= n;
+      c.data_next_size_ += n;
+      typename Conn::Seg& s = c.seg(c.data_next_);
+      const bool can_send =
+          c.data_next_ == c.send_next_ && (int32_t)(s.seq + c.data_next_size_ - c.send_wnd_seq_) <= 0;
+      if (c.data_next_size_ == c.smss_ || (last && can_send)) {
+        if (can_send) {
+          s.len = (uint16_t)c.data_next_size_;
+          s.fin = false;
+          emit(c, s.seq, kData, c.segData(c.data_next_), s.len);
+          advanceNext(c, c.data_next_size_);
+        }
+        advanceData(c);
+      }
+    }
+    return (uint32_t)(p - d);
+  }
+
+  void sendFin(Conn& c) { // TcpConn.h:69-84
+    if (c.fin_sent_ || !c.eng_) return;
+    if (c.send_una_ + kSendBufCnt - 1 == c.data_next_) {
+      closeConn(c);
+      return;
+    }
+    c.fin_sent_ = true;
+    c.rx_.setFinSent();
+    c.data_next_size_++;
+    if (c.data_next_ == c.send_next_ && c.data_next_size_ == 1) {
+      typename Conn::Seg& s = c.seg(c.data_next_);
+      s.fin = true;
+      s.len = 0;
+      emit(c, s.seq, kFinAck, nullptr, 0);
+      advanceNext(c, 1);
+      advanceData(c);
+    }
+  }
+
+  void sendAck(Conn& c, bool immediate) { // TcpConn.h:335-343
+    if (kDelayedAckMS == 0 || immediate) {
+      emit(c, c.seg(c.send_next_).seq, kAck, nullptr, 0);
+      return;
+    }
+    if (c.timers_[1].unlinked()) wheel_.add(std::max(1u, kDelayedAckMS), &c.timers_[1]);
+  }
+
+  void resendUna(Conn& c) { // TcpConn.h:771-790 (pollnet: no ssthresh)
+    c.retries_++;
+    typename Conn::Seg& s = c.seg(c.send_una_);
+    if (!c.established_ && c.send_una_ == 0)
+      emit(c, s.seq, s.syn_ack ? kSynAck : kSyn, nullptr, 0);
+    else
+      emit(c, s.seq, s.fin ? kFinAck : kData, c.segData(c.send_una_), s.len);
+    s.send_ts = wheel_.now();
+  }
+
+  void setUserTimer(Conn& c, uint32_t id, uint32_t ms) { // TcpConn.h:86-90
+    TimerNode& t = c.timers_[2 + id];
+    t.unlink();
+    if (ms) wheel_.add(ms, &t);
+  }
+
+  // TcpConn::close (TcpConn.h:92-102): RST if established, then release the entry.
+  void closeConn(Conn& c) {
+    if (c.isClosed()) return;
+    if (c.established_) emit(c, c.seg(c.send_next_).seq, kRstAck, nullptr, 0);
+    onClose(c, false);
+  }
+
+  // TcpConn::onClose (TcpConn.h:420-435): leave the table, or enter TIME_WAIT.
+  void onClose(Conn& c, bool enter_tw) {
+    if (c.isClosed()) return;
+    c.fin_sent_ = c.fin_received_ = true;
+    c.established_ = false;
+    for (auto& t : c.timers_) t.unlink();
+    if (!enter_tw || tw_cnt_ == kMaxTw) { // Core::enterTW: TIME_WAIT table full -> delete (Core.h:608-611)
+      delEntry(c.key_);
+      return;
+    }
+    // Core::enterTW (Core.h:607-638)
+    free_conns_.push_back(c.id_);
+    --conn_cnt_;
+    const uint32_t tw_id = free_tws_.back();
+    free_tws_.pop_back();
+    ++tw_cnt_;
+    table_.enterTW(c.key_, tw_id);
+    dirty_ = true;
+    Tw& tw = tws_[tw_id];
+    tw.key = c.key_;
+    std::memcpy(tw.peer_mac, c.peer_mac_, 6);
+    tw.peer_ip = c.peer_ip_;
+    tw.peer_port = c.peer_port_;
+    tw.local_port = c.local_port_;
+    tw.seq_num = c.seg(c.send_next_).seq;
+    tw.ack_num = c.rx_.ackSeq();
+    wheel_.add(kTimeWaitTimeout, &tw.timer);
+  }
+
+  // Core::delConnEntry (Core.h:578-605) with its id bookkeeping.
+  void delEntry(uint64_t key) {
+    uint32_t id = PN_MISS;
+    if (!table_.find(key, nullptr, &id)) return;
+    if (id < kMaxConn) {
+      free_conns_.push_back(id);
+      --conn_cnt_;
+    } else {
+      free_tws_.push_back(id - kMaxConn);
+      --tw_cnt_;
+    }
+    table_.del(key);
+    dirty_ = true;
+  }
+
+  template <class HH>
+  void onTimer(HH& h, TimerNode* n) { // TcpConn::onTimer (TcpConn.h:792-836), TIME_WAIT expiry (Core.h:740-744)
+    if (n->owner >= kMaxConn) {
+      delEntry(tws_[n->owner - kMaxConn].key);
+      return;
+    }
+    Conn& c = conns_[n->owner];
+    switch (n->kind) {
+      case 0: { // retransmission
+        if (c.retries_ >= std::min(31u, !c.established_ ? kSynRetries : kTcpRetries)) {
+          c.err_ = "connection timeout"; // onConnectionTimeout (EfviTcp.h:115-119, 273-276)
+          if (c.established_) h.disconnect(c);
+          else if (Derived::kClient) h.connectFailed();
+          closeConn(c);
+          break;
+        }
+        resendUna(c);
+        c.fast_re_ = false;
+        c.in_recover_ = true;
+        c.recover_ = c.send_next_;
+        c.rto_ = std::min(c.rto_ << 1, kMaxRtoMS);
+        wheel_.add(c.rto_, &c.timers_[0]);
+        break;
+      }
+      case 1: sendAck(c, true); break;
+      case 2: h.sendTimeout(c); break;
+      default: h.recvTimeout(c); break;
+    }
+  }
+
+  // ---- frame building: headers only; pn_tx_fill writes both checksums at flush ----
+  enum Kind { kSyn, kSynAck, kData, kFinAck, kAck, kRstAck };
+  uint8_t* txFrame() {
+    if (tx_n_ == kTxBatch) flushTx();
+    return be_.txSlots() + (size_t)tx_n_++ * Backend::kStride + Backend::kFrameOff;
+  }
+  void header(uint8_t* f, const uint8_t* dst_mac, uint32_t dst_ip, uint16_t src_port, uint16_t dst_port, uint32_t seq,
+              uint32_t ack, uint8_t doff_words, uint8_t flags, uint16_t window, uint32_t tcp_len) {
+    using namespace srv_detail;
+    std::memcpy(f, dst_mac, 6);
+    std::memcpy(f + 6, local_mac_, 6);
+    f[12] = 0x08;
+    f[13] = 0x00;
+    uint8_t* ip = f + 14; // SendBuf's fixed IP header (Core.h:291-301)
+    ip[0] = 0x45;
+    ip[1] = 0;
+    wr16(ip + 2, (uint16_t)(20 + tcp_len));
+    wr16(ip + 4, 0);
+    wr16(ip + 6, 0x4000);
+    ip[8] = 64;
+    ip[9] = 6;
+    wr16(ip + 10, 0);
+    std::memcpy(ip + 12, &local_ip_, 4);
+    std::memcpy(ip + 16, &dst_ip, 4);
+    uint8_t* tcp = ip + 20;
+    std::memcpy(tcp, &src_port, 2);
+    std::memcpy(tcp + 2, &dst_port, 2);
+    wr32(tcp + 4, seq);
+    wr32(tcp + 8, ack);
+    tcp[12] = (uint8_t)(doff_words << 4);
+    tcp[13] = flags;
+    wr16(tcp + 14, window);
+    wr32(tcp + 16, 0); // checksum (filled on the GPU), urgent pointer
+  }
+  // A segment of connection c (TcpConn::sendBuf, TcpConn.h:310-323): ack = what was received
+  // so far (updateLastAck, TcpConn.h:838-843), window = free receive buffer.
+  void emit(Conn& c, uint32_t seq, Kind k, const uint8_t* payload, uint32_t len) {
+    c.timers_[1].unlink();
+    c.rx_.ackSent();
+    const uint32_t ack = c.rx_.ackSeq();
+    const uint16_t win = (uint16_t)std::min<uint32_t>(65535u, c.rx_.window());
+    uint8_t* f = txFrame();
+    enum : uint8_t { FIN = 1, SYN = 2, RST = 4, PSH = 8, ACK = 16 };
+    const uint16_t sp = c.local_port_, dp = c.peer_port_;
+    switch (k) {
+      case kSyn:
+      case kSynAck: // MSS option (TcpConn.h:207-214)
+        header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 6, (uint8_t)(SYN | (k == kSynAck ? ACK : 0)), win, 24);
+        f[54] = 2;
+        f[55] = 4;
+        srv_detail::wr16(f + 56, (uint16_t)PN_RECV_MSS);
+        break;
+      case kData:
+      case kFinAck:
+        header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, (uint8_t)(PSH | ACK | (k == kFinAck ? FIN : 0)), win,
+               20 + len);
+        if (len) std::memcpy(f + 54, payload, len);
+        break;
+      case kAck: header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, PSH | ACK, win, 20); break;
+      case kRstAck: header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, RST | PSH | ACK, win, 20); break;
+    }
+  }
+  // Core::rspRst (Core.h:400-423): answer a segment nobody owns.  RSTs and TIME_WAIT ACKs
+  // share one send buffer in the reference (the last SendBuf), whose window field is never
+  // written (0) and whose ack_num an ACK-less RST does not rewrite: rst_ack_ is that field.
+  // (One difference: the reference skips the RST while that buffer's previous frame is
+  // still in the NIC's TX queue, Core.h:404; here every RST goes out.)
+  void rspRst(const uint8_t* eth, const pn_result& r) {
+    using namespace srv_detail;
+    if (r.flags & PN_F_RST) return;
+    const uint8_t* tcp = eth + 34;
+    uint32_t src_ip;
+    uint16_t src_port, dst_port;
+    std::memcpy(&src_ip, eth + 26, 4);
+    std::memcpy(&src_port, tcp, 2);
+    std::memcpy(&dst_port, tcp + 2, 2);
+    uint8_t* f = txFrame();
+    if (r.flags & PN_F_ACK) { // ack_num keeps what the shared buffer last carried
+      header(f, eth + 6, src_ip, dst_port, src_port, rd32(tcp + 8), rst_ack_, 5, 0x04, 0, 20);
+    } else {
+      rst_ack_ = rd32(tcp + 4) + segLen(eth, r);
+      header(f, eth + 6, src_ip, dst_port, src_port, 0, rst_ack_, 5, 0x14, 0, 20);
+    }
+  }
+  // Core::ackTW (Core.h:425-446)
+  void ackTW(const Tw& tw) {
+    uint8_t* f = txFrame();
+    rst_ack_ = tw.ack_num;
+    header(f, tw.peer_mac, tw.peer_ip, tw.local_port, tw.peer_port, tw.seq_num, tw.ack_num, 5, 0x10, 0, 20);
+  }
+
+  Link link_;
+  Backend be_;
+  ConnTable table_;
+  TimerWheel wheel_;
+  std::vector<Conn> conns_;
+  std::vector<Tw> tws_;
+  std::vector<uint32_t> free_conns_, free_tws_;
+  uint32_t conn_cnt_ = 0, tw_cnt_ = 0, tx_n_ = 0, rx_pending_ = 0;
+  int64_t rx_first_ns_ = 0;
+  uint32_t local_ip_ = 0, rst_ack_ = 0;
+  uint8_t local_mac_[6] = {};
+  bool ready_ = false, dirty_ = true, drop_bad_ = true;
+  const char* err_ = "Closed";
+};
+
+} // namespace pollnet_amd

@@ -3,7 +3,7 @@
 # efvitcp/Core.h needs <etherfabric/*.h> (ef_vi, not installed) and stand-ins for those
 # headers are not allowed, so it is not built.
 REFDIR ?= /root/reference
-all: _ref/libref_tcpstream.so _ref/ref_socket_c1 _ref/tcpserver_handler.inc _ref/libref_core.so
+all: _ref/libref_tcpstream.so _ref/ref_socket_c1 _ref/tcpserver_handler.inc _ref/tcpclient_handler.inc _ref/libref_core.so
 
 _ref/libref_tcpstream.so: ref_tcpstream.cc $(REFDIR)/TcpStream.h
 	mkdir -p _ref
@@ -24,6 +24,12 @@ _ref/tcpserver_handler.inc: $(REFDIR)/example/tcpserver.cc
 	mkdir -p _ref
 	sed -n '61,90p' $< > $@
 	grep -q 'onTcpData' $@ && grep -q '} handler;' $@
+
+# The handler of the reference's example client (example/tcpclient.cc:68-95), the same way.
+_ref/tcpclient_handler.inc: $(REFDIR)/example/tcpclient.cc
+	mkdir -p _ref
+	sed -n '68p' $< | grep -q struct && sed -n '70p' $< | grep -q onTcpConnectFailed && sed -n '95p' $< | grep -q '} handler;'
+	sed -n '68,95p' $< > $@
 
 # The reference's own Core.h code for the hot path (CSum, headers, connHashKey, the conn
 # table's member functions, Core::checksum), extracted verbatim by line range and compiled

@@ -1,0 +1,249 @@
+// GpuTcpClient talking to GpuTcpServer: both of the reference's example programs' handlers
+// (example/tcpclient.cc:68-95 and example/tcpserver.cc:61-90, extracted verbatim into
+// oracle/_ref/ by oracle/ref.mk) compiled unchanged against the two drop-ins, connected by an
+// in-memory wire that loses frames in both directions, under a simulated clock advancing one
+// millisecond per poll.  The example client writes a 16-B Packet {ts, val} on every send
+// timeout (1 s); the example server echoes it; the client prints each echo's value and
+// latency.  `cout`, `exit`, `getns()` and the globals the handlers name (`client`, `server`,
+// `pack`) are test-local: getns() is the simulated clock.
+//
+// Runs: twin (both ends on the sequential oracle backend) and, with `gpu`, both ends on the
+// GPU backend — every poll of either end one pn_classify launch for what it received and one
+// pn_tx_fill launch for what it sent.  Checks: the client connects, gets every value echoed
+// in order (the stream is reliable over the lossy wire), both handler logs and every frame on
+// the wire equal between the two runs; then the client closes (RST), the server sees it go, and
+// the client reconnects (its retry interval has passed).
+//   argv: twin | gpu            exit 0 = pass
+#include <arpa/inet.h>
+
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/pollnet_amd/tcp_client.hpp"
+#include "../../include/pollnet_amd/tcp_server.hpp"
+#include "segframes.hpp"
+#include "server_harness.hpp"
+
+using namespace std;
+using namespace pollnet_amd;
+
+struct ServerConf { // example/tcpserver.cc:4-14
+  static const uint32_t RecvBufSize = 4096;
+  static const uint32_t MaxConns = 10;
+  static const uint32_t SendTimeoutSec = 0;
+  static const uint32_t RecvTimeoutSec = 10;
+  static const uint32_t ConnSendBufCnt = 64;
+  static const uint32_t RxBatch = 256;
+  static const uint32_t TxBatch = 64;
+  struct UserData {
+    struct sockaddr_in addr;
+  };
+};
+struct ClientConf { // example/tcpclient.cc:3-14
+  static const uint32_t RecvBufSize = 4096;
+  static const uint32_t ConnRetrySec = 5;
+  static const uint32_t ConnTimeoutSec = 5;
+  static const uint32_t SendTimeoutSec = 1;
+  static const uint32_t RecvTimeoutSec = 3;
+  static const uint32_t ConnSendBufCnt = 64;
+  static const uint32_t RxBatch = 256;
+  static const uint32_t TxBatch = 64;
+  struct UserData {};
+};
+
+// Two queues; what one end sends reaches the other end's next fill, unless lost.
+struct Wire {
+  std::vector<std::vector<uint8_t>> to_server, to_client, log; // log: every frame sent, both ways
+  std::mt19937 loss{0x10553u};
+  uint32_t drops = 0;
+  uint32_t loss_pct = 4;
+  void carry(std::vector<std::vector<uint8_t>>& q, const uint8_t* eth, uint32_t len) {
+    log.emplace_back(eth, eth + len);
+    if (loss() % 100 < loss_pct) {
+      drops++;
+      return;
+    }
+    q.emplace_back(eth, eth + len);
+  }
+};
+static Wire* g_wire = nullptr;
+
+static const uint8_t kServerMac[6] = {2, 0, 0, 0, 0, 1}, kClientMac[6] = {2, 0, 0, 0, 0, 2};
+
+template <bool kServerSide>
+struct WireLink {
+  const char* open(const char*) { return nullptr; }
+  uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
+    auto& q = kServerSide ? g_wire->to_server : g_wire->to_client;
+    uint32_t n = 0;
+    for (; n < cap && n < q.size(); n++) {
+      uint8_t* s = slots + (size_t)n * stride;
+      std::memset(s, 0, stride);
+      std::memcpy(s + off, q[n].data(), q[n].size());
+    }
+    q.erase(q.begin(), q.begin() + n);
+    return n;
+  }
+  void send(const uint8_t* eth, uint32_t len) { g_wire->carry(kServerSide ? g_wire->to_client : g_wire->to_server, eth, len); }
+  uint32_t localIp() const { return htonl(kServerSide ? 0x0a000001 : 0x0a000002); }
+  const uint8_t* localMac() const { return kServerSide ? kServerMac : kClientMac; }
+  const char* resolveMac(uint32_t, uint8_t* mac) {
+    std::memcpy(mac, kServerSide ? kClientMac : kServerMac, 6);
+    return nullptr;
+  }
+};
+
+static const int64_t kT0 = (int64_t)1700000000 << 30; // simulated clock origin (ns)
+static int64_t g_now = kT0;
+
+// The example client's `Packet` and `getns()` (example/tcpclient.cc:32-36, timestamp.h)
+struct Packet {
+  uint64_t ts = 0;
+  uint64_t val = 0;
+};
+static uint64_t getns() { return (uint64_t)g_now; }
+
+#define PN_DEFINE_ENDS(NS, BACKEND)                                                 \
+  namespace NS {                                                                    \
+  using TcpServer = GpuTcpServer<ServerConf, WireLink<true>, BACKEND>;              \
+  using TcpClient = GpuTcpClient<ClientConf, WireLink<false>, BACKEND>;             \
+  TcpServer& server = *new TcpServer;                                               \
+  TcpClient& client = *new TcpClient;                                               \
+  Packet pack;                                                                      \
+  namespace srv {                                                                   \
+  LogStream cout;                                                                   \
+  int exits = 0;                                                                    \
+  void exit(int) { ++exits; }                                                       \
+  void pollOnce() {
+#define PN_END_SERVER                                                               \
+  server.poll(handler, g_now);                                                      \
+  }                                                                                 \
+  }                                                                                 \
+  namespace cli {                                                                   \
+  LogStream cout;                                                                   \
+  int exits = 0;                                                                    \
+  void exit(int) { ++exits; }                                                       \
+  void pollOnce() {
+#define PN_END_CLIENT                                                               \
+  client.poll(handler, g_now);                                                      \
+  }                                                                                 \
+  }                                                                                 \
+  }
+
+PN_DEFINE_ENDS(on_twin, OracleBackend)
+#include "../../oracle/_ref/tcpserver_handler.inc"
+PN_END_SERVER
+#include "../../oracle/_ref/tcpclient_handler.inc"
+PN_END_CLIENT
+
+PN_DEFINE_ENDS(on_gpu, GpuBackend)
+#include "../../oracle/_ref/tcpserver_handler.inc"
+PN_END_SERVER
+#include "../../oracle/_ref/tcpclient_handler.inc"
+PN_END_CLIENT
+
+struct Result {
+  std::string srv_log, cli_log;
+  std::vector<std::vector<uint8_t>> wire;
+  uint32_t drops = 0, echoed = 0, conns_after = 0;
+  bool connected = false, closed_seen = false;
+};
+
+template <class S, class C>
+static bool run(S& server, C& client, void (*poll_srv)(), void (*poll_cli)(), LogStream& slog, LogStream& clog,
+                Result& out) {
+  Wire w;
+  g_wire = &w;
+  g_now = kT0;
+  if (!server.initWithLink("10.0.0.1", 1234, g_now)) return std::printf("server init: %s\n", server.getLastError()), false;
+  if (!client.initWithLink("10.0.0.2", "10.0.0.1", 1234, 40000, g_now))
+    return std::printf("client init: %s\n", client.getLastError()), false;
+  const int64_t ms = 1 << 20; // one tick (ns >> 20)
+  for (int t = 0; t < 22000; t++) {  // ~22 s of simulated time: ~20 send timeouts
+    g_now += ms;
+    poll_cli();
+    poll_srv();
+  }
+  out.connected = client.isConnected();
+  // the client closes (RST): the server must see the connection go
+  client.close("bye");
+  for (int t = 0; t < 3000; t++) { // the reconnect, and its first send timeout
+    g_now += ms;
+    poll_cli();
+    poll_srv();
+  }
+  out.conns_after = server.getConnCnt();
+  out.srv_log = slog.os.str();
+  out.cli_log = clog.os.str();
+  out.wire = w.log;
+  out.drops = w.drops;
+  static Wire sink; // frames sent after the run (the ends' destructors RST open connections)
+  g_wire = &sink;
+  return true;
+}
+
+static int check(const char* tag, const Result& r) {
+  int fail = 0;
+  // the client printed "recv val: k ..." for k = 1, 2, ... in order
+  uint32_t expect = 1;
+  std::istringstream is(r.cli_log);
+  std::string line;
+  while (std::getline(is, line)) {
+    unsigned v;
+    if (std::sscanf(line.c_str(), "recv val: %u", &v) == 1) {
+      if (v != expect) fail++;
+      expect++;
+    }
+  }
+  const uint32_t echoed = expect - 1;
+  uint32_t bad = 0;
+  for (auto& f0 : r.wire) {
+    std::vector<uint8_t> f(f0);
+    f.resize(f0.size() + 2, 0);
+    const pn_result x = segtest::classify(f.data(), (uint32_t)f.size());
+    bad += (x.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK);
+  }
+  const bool disc = r.srv_log.find("client disconnected") != std::string::npos;
+  size_t conns = 0;
+  for (size_t p = 0; (p = r.srv_log.find("new connection from", p)) != std::string::npos; p++) conns++;
+  std::printf("%s: %zu frames on the wire (%u lost, %u bad checksums), client connected %d, %u values echoed in "
+              "order, server saw the close %d, connections accepted %zu, open after the close %u\n",
+              tag, r.wire.size(), r.drops, bad, r.connected, echoed, disc, conns, r.conns_after);
+  // after close("bye") the client reconnects at once (ConnRetrySec = 5 s have long passed,
+  // EfviTcp.h:92-104): the server sees the old connection go and a new one arrive
+  if (!r.connected || echoed < 18 || bad || !disc || conns != 2 || r.conns_after != 1) fail++;
+  if (r.cli_log.find("onTcpConnected") == std::string::npos) fail++;
+  return fail;
+}
+
+int main(int argc, char** argv) {
+  const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
+  int fail = 0;
+  Result tw;
+  if (!run(on_twin::server, on_twin::client, on_twin::srv::pollOnce, on_twin::cli::pollOnce, on_twin::srv::cout,
+           on_twin::cli::cout, tw))
+    return 3;
+  fail += check("twin", tw);
+  if (argc > 2) std::printf("server log:\n%s\nclient log:\n%s\n", tw.srv_log.c_str(), tw.cli_log.c_str());
+  if (gpu) {
+    Result g;
+    if (!run(on_gpu::server, on_gpu::client, on_gpu::srv::pollOnce, on_gpu::cli::pollOnce, on_gpu::srv::cout,
+             on_gpu::cli::cout, g))
+      return 5;
+    fail += check("gpu", g);
+    const bool logs = g.srv_log == tw.srv_log && g.cli_log == tw.cli_log;
+    const bool wire = g.wire == tw.wire;
+    std::printf("gpu: handler logs %s, wire frames %s (%zu)\n", logs ? "identical" : "DIFFERENT",
+                wire ? "identical" : "DIFFERENT", g.wire.size());
+    fail += !logs + !wire;
+    delete &on_gpu::client;
+    delete &on_gpu::server;
+  }
+  std::printf("%s\n", fail ? "FAIL" : "PASS");
+  return fail ? 1 : 0;
+}

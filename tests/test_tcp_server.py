@@ -63,3 +63,30 @@ def test_gpu_server_reactive_peers_match_twin():
     p = _peer("gpu")
     assert p.returncode == 0, p.stdout + p.stderr
     assert "gpu: handler log identical, TX frames identical" in p.stdout, p.stdout
+
+
+CLISRV = os.path.join(ROOT, "tests", "cpp", "test_tcp_client_server")
+
+
+def _clisrv(mode):
+    if not os.path.exists(CLISRV):
+        if not os.path.isdir("/root/reference"):
+            pytest.skip("tests/cpp/test_tcp_client_server not built (its handler texts come from /root/reference)")
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tcp_client_server"], check=True, capture_output=True)
+    return subprocess.run([CLISRV, mode], capture_output=True, text=True, timeout=300)
+
+
+def test_client_server_twin_reference_examples():
+    """GpuTcpClient <-> GpuTcpServer over a lossy in-memory wire, running the reference's
+    example client and server handlers (tcpclient.cc:68-95, tcpserver.cc:61-90) unchanged:
+    connect, 1-s send timeouts echoed in order, close, reconnect (sequential backends)."""
+    p = _clisrv("twin")
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "PASS" in p.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_client_server_match_twin():
+    p = _clisrv("gpu")
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "gpu: handler logs identical, wire frames identical" in p.stdout, p.stdout
