@@ -26,6 +26,8 @@ RXCONNTEST = tests/cpp/test_rx_conn
 TCPRXTEST = tests/cpp/test_gpu_tcp_rx
 TCPRXBENCH = bench/bench_tcp_rx
 LATBENCH = bench/bench_latency
+SRVBENCH = bench/bench_tcp_server
+PINBENCH = bench/bench_pinned
 RINGTEST = tests/cpp/test_rx_ring
 STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
@@ -33,7 +35,7 @@ SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
 CLISRVTEST = tests/cpp/test_tcp_client_server
 
-all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
@@ -89,6 +91,16 @@ $(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_am
 	$(HIPCC) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
+# GpuTcpServer::poll throughput (handshake, RX, ACKs) on the GPU vs the same server on the sequential backend
+$(SRVBENCH): bench/bench_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp \
+  include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
+	$(HIPCC) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
+
+# zero-copy classify from host rings of each pinned-memory kind: PCIe rate and staleness
+$(PINBENCH): bench/bench_pinned.cpp $(HDRS) $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+
 # receive-side server loop on the GPU vs a sequential twin with reference semantics
 $(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
@@ -117,6 +129,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 .PHONY: all ref clean

@@ -1,0 +1,277 @@
+// Throughput of the drop-in server itself (include/pollnet_amd/tcp_server.hpp): frames in
+// the RX ring -> GpuTcpServer::poll(handler) -> onTcpData, with the server's own ACKs built,
+// checksummed (pn_tx_fill) and handed to the link — the whole EfviTcpServer::poll path
+// (EfviTcp.h:258-307 -> TcpServer::poll, TcpServer.h:70-112 -> TcpConn::onPack), against the
+// same server on the sequential backend (every frame classified by the CPU restatement of
+// Core::pollNet's per-frame work, checksums included, TX checksums on the CPU; one thread).
+//
+// Workload: n_flows peers connect (SYN, SYN-ACK, ACK through the server's own handshake),
+// then each poll hands the server RxBatch in-order MSS segments (1514-B frames, 1460-B
+// payload, ACK|PSH), RxBatch / n_flows per flow; the handler reads each delivery's first 8
+// bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
+// plays the NIC: the ring slots keep their frames between polls and only the sequence number
+// and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
+//   argv: n_flows (256)  polls (400)  [cpu]    prints one JSON line; exit 0 = all data delivered
+//         (cpu: the sequential-backend legs only, no GPU needed)
+#include <arpa/inet.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../include/pollnet_amd/tcp_server.hpp"
+#include "../tests/cpp/segframes.hpp"
+#include "../tests/cpp/server_harness.hpp"
+
+using namespace pollnet_amd;
+using Clock = std::chrono::steady_clock;
+static double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+static const uint8_t kServerMac[6] = {2, 0, 0, 0, 0, 1};
+static const uint32_t kPayload = 1460;
+
+// The peers and the NIC: n_flows clients, frames written into the server's RX ring.
+struct BenchLink {
+  enum Phase { Syn, Ack, Data, Idle } phase = Idle;
+  uint32_t n_flows = 0;
+  std::vector<uint32_t> cli_isn, srv_isn, sum_base; // sum_base: TCP sum of the data frame with seq = 0
+  std::vector<uint8_t> payload = std::vector<uint8_t>(kPayload);
+  uint64_t poll_no = 0;           // data polls so far
+  uint8_t* written = nullptr;     // ring whose slots hold full data frames
+  uint32_t written_n = 0;
+  uint64_t acks = 0, rsts = 0, synacks = 0, other = 0;
+  uint8_t other_flags = 0;
+  double fill_s = 0;
+
+  static uint32_t ip(uint32_t f) { return 0x0a010000u | f; }
+  static uint16_t port(uint32_t f) { return (uint16_t)(32768 + (f * 7919) % 28000); }
+  void setup(uint32_t n) {
+    n_flows = n;
+    cli_isn.resize(n);
+    srv_isn.assign(n, 0);
+    sum_base.resize(n);
+    for (uint32_t f = 0; f < n; f++) cli_isn[f] = 0x10000000u * (f & 15) + f * 7919u;
+    for (uint32_t i = 0; i < kPayload; i++) payload[i] = (uint8_t)(i * 31 + 7);
+  }
+  segtest::Seg seg(uint32_t f, uint8_t flags, uint32_t seq, uint32_t ack) const {
+    segtest::Seg s;
+    s.src_ip = ip(f);
+    s.src_port = port(f);
+    s.seq = seq;
+    s.ack = ack;
+    s.flags = flags;
+    return s;
+  }
+  uint32_t dataSeq(uint32_t f, uint64_t k) const { return cli_isn[f] + 1 + (uint32_t)(k * kPayload); }
+
+  const char* open(const char*) { return nullptr; }
+  uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
+    const auto t0 = Clock::now();
+    uint32_t n = 0;
+    if (phase == Syn || phase == Ack) {
+      for (uint32_t f = 0; f < n_flows && f < cap; f++, n++) {
+        segtest::Seg s = phase == Syn ? seg(f, segtest::SYN, cli_isn[f], 0)
+                                      : seg(f, segtest::ACK, cli_isn[f] + 1, srv_isn[f] + 1);
+        if (phase == Syn) s.opts = {2, 4, 0x05, 0xb4}; // MSS 1460
+        segtest::build(slots + (size_t)f * stride + off, s);
+      }
+      phase = Idle;
+    } else if (phase == Data) {
+      const uint32_t per_flow = cap / n_flows;
+      n = per_flow * n_flows;
+      if (written != slots || written_n != n) { // first data poll: whole frames
+        for (uint32_t i = 0; i < n; i++) {
+          const uint32_t f = i % n_flows;
+          segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, srv_isn[f] + 1);
+          s.payload = payload.data();
+          s.len = kPayload;
+          uint8_t* eth = slots + (size_t)i * stride + off;
+          segtest::build(eth, s);
+          if (i < n_flows) { // the sum without the checksum field and with seq 0
+            const uint16_t c = (uint16_t)(eth[50] << 8 | eth[51]);
+            sum_base[f] = (uint16_t)~c;
+          }
+        }
+        written = slots;
+        written_n = n;
+      }
+      for (uint32_t i = 0; i < n; i++) { // seq and checksum of segment k of flow f
+        const uint32_t f = i % n_flows;
+        const uint32_t seq = dataSeq(f, poll_no * per_flow + i / n_flows);
+        uint8_t* tcp = slots + (size_t)i * stride + off + 34;
+        segtest::put32(tcp + 4, seq);
+        uint32_t acc = sum_base[f] + (seq >> 16) + (seq & 0xffff);
+        acc = (acc & 0xffff) + (acc >> 16);
+        acc = (acc & 0xffff) + (acc >> 16);
+        segtest::put16(tcp + 16, (uint16_t)~acc);
+      }
+      poll_no++;
+    }
+    fill_s += secs(t0, Clock::now());
+    return n;
+  }
+  void send(const uint8_t* eth, uint32_t) {
+    const uint8_t flags = eth[47];
+    if (flags & segtest::RST) {
+      rsts++;
+    } else if ((flags & (segtest::SYN | segtest::ACK)) == (segtest::SYN | segtest::ACK)) {
+      const uint16_t dport = (uint16_t)(eth[36] << 8 | eth[37]);
+      for (uint32_t f = 0; f < n_flows; f++)
+        if (port(f) == dport) srv_isn[f] = (uint32_t)eth[38] << 24 | eth[39] << 16 | eth[40] << 8 | eth[41];
+      synacks++;
+    } else if ((flags & ~segtest::PSH) == segtest::ACK) { // pure ACKs carry PSH, as all of efvitcp's frames (TcpConn.h:427)
+      acks++;
+    } else {
+      other++;
+      other_flags = flags;
+    }
+  }
+  uint32_t localIp() const { return htonl(0x0a000001); }
+  const uint8_t* localMac() const { return kServerMac; }
+  const char* resolveMac(uint32_t, uint8_t*) { return "not used by a server"; }
+};
+
+struct Handler {
+  uint64_t bytes = 0, calls = 0, sink = 0, connected = 0, disconnected = 0;
+  template <class C>
+  uint32_t onTcpData(C&, const uint8_t* d, uint32_t n) {
+    uint64_t w;
+    std::memcpy(&w, d, 8);
+    sink ^= w;
+    bytes += n;
+    calls++;
+    return 0;
+  }
+  template <class C>
+  void onTcpConnected(C&) {
+    connected++;
+  }
+  template <class C>
+  void onTcpDisconnect(C&) {
+    disconnected++;
+  }
+};
+
+template <uint32_t kBatch, uint32_t kChunk = 0>
+struct Conf {
+  static const uint32_t RecvBufSize = 65536;
+  static const uint32_t MaxConns = 1024;
+  static const uint32_t SendTimeoutSec = 0;
+  static const uint32_t RecvTimeoutSec = 0;
+  static const uint32_t ConnSendBufCnt = 16; // the server sends no data
+  static const uint32_t RxBatch = kBatch;
+  static const uint32_t TxBatch = kBatch;
+  static const uint32_t RxChunk = kChunk;
+  struct UserData {};
+};
+
+struct Run {
+  double mfps = 0, us_poll = 0, acks_per_frame = 0, fill_share = 0, classify_share = 0, tx_share = 0;
+  bool ok = false;
+  std::string err;
+};
+
+template <uint32_t kBatch, class Backend, uint32_t kChunk = 0>
+static Run runOne(uint32_t n_flows, uint32_t polls) {
+  Run out;
+  using Server = GpuTcpServer<Conf<kBatch, kChunk>, BenchLink, Backend>;
+  auto srv = std::make_unique<Server>();
+  srv->link().setup(n_flows);
+  if (!srv->initWithLink("10.0.0.1", 1234)) {
+    out.err = srv->getLastError();
+    return out;
+  }
+  Handler h;
+  BenchLink& link = srv->link();
+  link.phase = BenchLink::Syn;
+  srv->poll(h);
+  link.phase = BenchLink::Ack;
+  srv->poll(h);
+  if (h.connected != n_flows || link.rsts) {
+    out.err = "handshake: " + std::to_string(h.connected) + " connected, " + std::to_string(link.rsts) + " RSTs";
+    return out;
+  }
+  link.phase = BenchLink::Data;
+  const uint32_t warm = 8;
+  for (uint32_t p = 0; p < warm; p++) srv->poll(h);
+  const uint64_t bytes0 = h.bytes, acks0 = link.acks;
+  link.fill_s = 0;
+  const auto t0 = Clock::now();
+  for (uint32_t p = 0; p < polls; p++) srv->poll(h);
+  const double t = secs(t0, Clock::now());
+  const uint64_t frames = (uint64_t)polls * (kBatch / n_flows) * n_flows;
+  out.mfps = frames / t / 1e6;
+  out.us_poll = t * 1e6 / polls;
+  out.acks_per_frame = (double)(link.acks - acks0) / frames;
+  out.fill_share = link.fill_s / t;
+  // the legs on their own, same frames: classify (+ the record walk, no dispatch) and the
+  // TX checksum fill of one poll's ACKs
+  const uint32_t n = (kBatch / n_flows) * n_flows, acks = (uint32_t)(out.acks_per_frame * n + 0.5);
+  auto& be = srv->backend();
+  const auto c0 = Clock::now();
+  for (uint32_t p = 0; p < polls; p++)
+    if (be.classify(n, srv->table(), [](uint64_t, const pn_result&, const uint8_t*) {})) break;
+  const auto c1 = Clock::now();
+  for (uint32_t p = 0; p < polls && acks; p++)
+    if (be.fillTx(acks)) break;
+  out.classify_share = secs(c0, c1) / t;
+  out.tx_share = secs(c1, Clock::now()) / t;
+  out.ok = h.bytes - bytes0 == frames * kPayload && h.bytes == (uint64_t)link.poll_no * (kBatch / n_flows) * n_flows * kPayload &&
+           !link.rsts && !link.other && !h.disconnected && srv->getLastError() == nullptr;
+  if (!out.ok)
+    out.err = srv->getLastError() ? srv->getLastError()
+                                  : "delivered " + std::to_string(h.bytes - bytes0) + " of " + std::to_string(frames * kPayload) +
+                                        " B, " + std::to_string(link.rsts) + " RSTs, " + std::to_string(link.other) +
+                                        " other frames (flags " + std::to_string(link.other_flags) + "), " + std::to_string(h.disconnected) + " disconnects";
+  return out;
+}
+
+static std::string json(const Run& r) {
+  char b[384];
+  if (!r.err.empty() && !r.ok) {
+    std::snprintf(b, sizeof b, "{\"error\": \"%s\"}", r.err.c_str());
+    return b;
+  }
+  std::snprintf(b, sizeof b,
+                "{\"mframes_per_s\": %.3f, \"gbit_per_s\": %.1f, \"us_per_poll\": %.1f, \"acks_per_frame\": %.3f, "
+                "\"link_fill_share\": %.3f, \"classify_share\": %.3f, \"tx_fill_share\": %.3f}",
+                r.mfps, r.mfps * 1514 * 8 / 1e3, r.us_poll, r.acks_per_frame, r.fill_share, r.classify_share, r.tx_share);
+  return b;
+}
+
+int main(int argc, char** argv) {
+  const uint32_t n_flows = argc > 1 ? std::atoi(argv[1]) : 256;
+  const uint32_t polls = argc > 2 ? std::atoi(argv[2]) : 400;
+  if (n_flows == 0 || n_flows > 512 || 512 % n_flows) {
+    std::fprintf(stderr, "n_flows must divide 512\n");
+    return 2;
+  }
+  std::string lines;
+  bool ok = true;
+  auto leg = [&](const char* name, const Run& r) {
+    lines += std::string(lines.empty() ? "" : ", ") + "\"" + name + "\": " + json(r);
+    ok = ok && r.ok;
+  };
+  const bool cpu_only = argc > 3 && std::strcmp(argv[3], "cpu") == 0;
+  if (!cpu_only) {
+    leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
+    leg("gpu_rxbatch_4096", runOne<4096, GpuBackend>(n_flows, polls));
+    leg("gpu_rxbatch_16384", runOne<16384, GpuBackend>(n_flows, polls / 4));
+    leg("gpu_rxbatch_512_chunk_128", runOne<512, GpuBackend, 128>(n_flows, polls));
+    leg("gpu_rxbatch_4096_chunk_512", runOne<4096, GpuBackend, 512>(n_flows, polls));
+    leg("gpu_rxbatch_4096_chunk_1024", runOne<4096, GpuBackend, 1024>(n_flows, polls));
+    leg("gpu_rxbatch_16384_chunk_2048", runOne<16384, GpuBackend, 2048>(n_flows, polls / 4));
+    leg("gpu_rxbatch_16384_chunk_4096", runOne<16384, GpuBackend, 4096>(n_flows, polls / 4));
+  }
+  leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
+  leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
+  std::printf("{\"bench\": \"tcp_server_poll\", \"workload\": \"%u flows connected through the server's handshake, "
+              "in-order 1514-B frames (1460-B payload), RxBatch frames per poll, handler consumes, server ACKs\", "
+              "%s, \"delivered_ok\": %s}\n",
+              n_flows, lines.c_str(), ok ? "true" : "false");
+  return ok ? 0 : 1;
+}

@@ -67,6 +67,8 @@ PN_CONF_OPT(ConnSendBufCnt, uint32_t, 1024) // EfviTcp.h:181
 PN_CONF_OPT(RxBatch, uint32_t, 512)         // frames per poll (RecvBufCnt = 512, EfviTcp.h:186)
 PN_CONF_OPT(RxLatencyBudgetUs, uint32_t, 0) // hold received frames up to this long for a fuller batch
 PN_CONF_OPT(TxBatch, uint32_t, 1024)        // frames per pn_tx_fill launch
+PN_CONF_OPT(RxChunk, uint32_t, 0)           // frames per classify launch within a poll (0 = RxBatch): chunk
+                                            // k+1 is on the GPU while chunk k is dispatched
 PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
 PN_CONF_OPT(Device, int, 0)
 PN_CONF_OPT(ReferenceLiteralTable, bool, false) // PN_TABLE_REFERENCE_LITERAL: the reference's rehash, defect kept
@@ -276,8 +278,11 @@ class GpuBackend {
     if (tx_ring_) (void)hipHostFree(tx_ring_);
   }
 
-  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap) {
-    if (const char* e = rx_.init(device, kStride, kFrameOff, rx_cap, GpuRx::Mode::ZeroCopy)) return e;
+  // rx_chunk: frames per classify launch (a poll's frames go in chunks, the next one on the
+  // GPU while the host dispatches the current one; 0 = one launch per poll).
+  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0) {
+    const uint32_t chunk = rx_chunk && rx_chunk < rx_cap ? rx_chunk : rx_cap;
+    if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy)) return e;
     if (hipHostMalloc((void**)&rx_ring_, (size_t)kStride * rx_cap, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(rx ring) failed";
     if (hipHostMalloc((void**)&tx_ring_, (size_t)kStride * tx_cap, hipHostMallocDefault) != hipSuccess)
@@ -336,6 +341,7 @@ class TcpEngine {
   static constexpr uint32_t kRxBatch = srv_detail::opt_RxBatch<Conf>::value;
   static constexpr uint32_t kTxBatch = srv_detail::opt_TxBatch<Conf>::value;
   static constexpr uint32_t kRxBudgetUs = srv_detail::opt_RxLatencyBudgetUs<Conf>::value;
+  static constexpr uint32_t kRxChunk = srv_detail::opt_RxChunk<Conf>::value;
   static constexpr uint32_t kSendTimeoutMs = srv_detail::opt_SendTimeoutSec<Conf>::value * 1000;
   static constexpr uint32_t kRecvTimeoutMs = srv_detail::opt_RecvTimeoutSec<Conf>::value * 1000;
   static_assert(kSendBufCnt >= 4 && !(kSendBufCnt & (kSendBufCnt - 1)), "ConnSendBufCnt must be a power of 2");
@@ -428,6 +434,7 @@ class TcpEngine {
   TcpEngine& operator=(const TcpEngine&) = delete;
 
   Link& link() { return link_; }
+  Backend& backend() { return be_; } // measurement: the per-frame legs timed on their own
   // Drop checksum-failed frames before they touch any state (what the NIC's RX checksum
   // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.
   void setDropBadChecksum(bool drop) { drop_bad_ = drop; }
@@ -508,7 +515,7 @@ class TcpEngine {
     }
     std::memcpy(local_mac_, link_.localMac(), 6);
     if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
-    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch)) return e;
+    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk)) return e;
     free_conns_.clear();
     for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i
     free_tws_.clear();

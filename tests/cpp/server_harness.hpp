@@ -43,7 +43,7 @@ struct OracleBackend {
   static constexpr bool kSnapshot = false;
   static constexpr uint32_t kStride = 2048, kFrameOff = 2;
   std::vector<uint8_t> rx, tx;
-  const char* init(int, uint32_t rx_cap, uint32_t tx_cap) {
+  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0) {
     rx.assign((size_t)kStride * rx_cap, 0);
     tx.assign((size_t)kStride * tx_cap, 0);
     return nullptr;
