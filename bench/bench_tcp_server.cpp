@@ -41,7 +41,7 @@ struct BenchLink {
   std::vector<uint32_t> cli_isn, srv_isn, sum_base; // sum_base: TCP sum of the data frame with seq = 0
   std::vector<uint8_t> payload = std::vector<uint8_t>(kPayload);
   uint64_t poll_no = 0;           // data polls so far
-  uint8_t* written = nullptr;     // ring whose slots hold full data frames
+  uint8_t* written[2] = {nullptr, nullptr}; // rings (halves, pipelined) whose slots hold full data frames
   uint32_t written_n = 0;
   uint64_t acks = 0, rsts = 0, synacks = 0, other = 0;
   uint8_t other_flags = 0;
@@ -83,7 +83,7 @@ struct BenchLink {
     } else if (phase == Data) {
       const uint32_t per_flow = cap / n_flows;
       n = per_flow * n_flows;
-      if (written != slots || written_n != n) { // first data poll: whole frames
+      if ((written[0] != slots && written[1] != slots) || written_n != n) { // first data poll: whole frames
         for (uint32_t i = 0; i < n; i++) {
           const uint32_t f = i % n_flows;
           segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, srv_isn[f] + 1);
@@ -96,7 +96,8 @@ struct BenchLink {
             sum_base[f] = (uint16_t)~c;
           }
         }
-        written = slots;
+        if (written_n != n) written[0] = written[1] = nullptr;
+        (written[0] ? written[1] : written[0]) = slots;
         written_n = n;
       }
       for (uint32_t i = 0; i < n; i++) { // seq and checksum of segment k of flow f
@@ -156,7 +157,7 @@ struct Handler {
   }
 };
 
-template <uint32_t kBatch, uint32_t kChunk = 0>
+template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false>
 struct Conf {
   static const uint32_t RecvBufSize = 65536;
   static const uint32_t MaxConns = 1024;
@@ -166,6 +167,7 @@ struct Conf {
   static const uint32_t RxBatch = kBatch;
   static const uint32_t TxBatch = kBatch;
   static const uint32_t RxChunk = kChunk;
+  static const bool RxPipeline = kPipe;
   struct UserData {};
 };
 
@@ -175,10 +177,10 @@ struct Run {
   std::string err;
 };
 
-template <uint32_t kBatch, class Backend, uint32_t kChunk = 0>
+template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false>
 static Run runOne(uint32_t n_flows, uint32_t polls) {
   Run out;
-  using Server = GpuTcpServer<Conf<kBatch, kChunk>, BenchLink, Backend>;
+  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe>, BenchLink, Backend>;
   auto srv = std::make_unique<Server>();
   srv->link().setup(n_flows);
   if (!srv->initWithLink("10.0.0.1", 1234)) {
@@ -189,7 +191,9 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
   BenchLink& link = srv->link();
   link.phase = BenchLink::Syn;
   srv->poll(h);
+  srv->poll(h); // (pipelined: the SYNs are dispatched one poll later)
   link.phase = BenchLink::Ack;
+  srv->poll(h);
   srv->poll(h);
   if (h.connected != n_flows || link.rsts) {
     out.err = "handshake: " + std::to_string(h.connected) + " connected, " + std::to_string(link.rsts) + " RSTs";
@@ -203,6 +207,9 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
   const auto t0 = Clock::now();
   for (uint32_t p = 0; p < polls; p++) srv->poll(h);
   const double t = secs(t0, Clock::now());
+  const uint64_t timed_bytes = h.bytes - bytes0;
+  link.phase = BenchLink::Idle;
+  srv->poll(h); // pipelined: the last batch is still in flight
   const uint64_t frames = (uint64_t)polls * (kBatch / n_flows) * n_flows;
   out.mfps = frames / t / 1e6;
   out.us_poll = t * 1e6 / polls;
@@ -220,11 +227,11 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
     if (be.fillTx(acks)) break;
   out.classify_share = secs(c0, c1) / t;
   out.tx_share = secs(c1, Clock::now()) / t;
-  out.ok = h.bytes - bytes0 == frames * kPayload && h.bytes == (uint64_t)link.poll_no * (kBatch / n_flows) * n_flows * kPayload &&
+  out.ok = timed_bytes == frames * kPayload && h.bytes == (uint64_t)link.poll_no * (kBatch / n_flows) * n_flows * kPayload &&
            !link.rsts && !link.other && !h.disconnected && srv->getLastError() == nullptr;
   if (!out.ok)
     out.err = srv->getLastError() ? srv->getLastError()
-                                  : "delivered " + std::to_string(h.bytes - bytes0) + " of " + std::to_string(frames * kPayload) +
+                                  : "delivered " + std::to_string(timed_bytes) + " of " + std::to_string(frames * kPayload) +
                                         " B, " + std::to_string(link.rsts) + " RSTs, " + std::to_string(link.other) +
                                         " other frames (flags " + std::to_string(link.other_flags) + "), " + std::to_string(h.disconnected) + " disconnects";
   return out;
@@ -266,9 +273,13 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_4096_chunk_1024", runOne<4096, GpuBackend, 1024>(n_flows, polls));
     leg("gpu_rxbatch_16384_chunk_2048", runOne<16384, GpuBackend, 2048>(n_flows, polls / 4));
     leg("gpu_rxbatch_16384_chunk_4096", runOne<16384, GpuBackend, 4096>(n_flows, polls / 4));
+    leg("gpu_rxbatch_512_pipelined", runOne<512, GpuBackend, 0, true>(n_flows, polls));
+    leg("gpu_rxbatch_4096_pipelined", runOne<4096, GpuBackend, 0, true>(n_flows, polls));
+    leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
   }
   leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
   leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
+  leg("cpu_rxbatch_4096_pipelined", runOne<4096, OracleBackend, 0, true>(n_flows, polls / 4));
   std::printf("{\"bench\": \"tcp_server_poll\", \"workload\": \"%u flows connected through the server's handshake, "
               "in-order 1514-B frames (1460-B payload), RxBatch frames per poll, handler consumes, server ACKs\", "
               "%s, \"delivered_ok\": %s}\n",

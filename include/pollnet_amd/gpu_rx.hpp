@@ -155,6 +155,29 @@ class GpuRx {
         n, table, launch_k, [&](uint32_t i) { return ring + offsets[i]; }, recv_handler, tw_handler);
   }
 
+  // The two halves of pollBatch, for a caller that overlaps one batch's classify with other
+  // host work (e.g. dispatching the previous batch): submit issues the classify of n <=
+  // max_batch slots into record buffer b (0 or 1; at most one batch per buffer in flight),
+  // complete waits for it and dispatches its records exactly as pollBatch does.  The slots
+  // must stay untouched in between.
+  const char* submit(const uint8_t* host_slots, uint32_t n, uint32_t b) {
+    if (n > cap_ || b > 1) return "submit: n > max_batch or buffer > 1";
+    if (mode_ == Mode::ZeroCopy)
+      if (const char* e = check_pinned(host_slots)) return e;
+    const char* e = launch_at(host_slots, n, b);
+    if (e) (void)hipStreamSynchronize(stream_);
+    return e;
+  }
+  template <class RecvHandler, class TwHandler>
+  const char* complete(const uint8_t* host_slots, uint32_t n, uint32_t b, const ConnTable& table,
+                       RecvHandler&& recv_handler, TwHandler&& tw_handler) {
+    if (n > cap_ || b > 1) return "complete: n > max_batch or buffer > 1";
+    if (hipEventSynchronize(done_[b]) != hipSuccess) return "hipEventSynchronize failed";
+    auto eth_of = [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; };
+    walk(h_res_[b], 0, n, table, eth_of, recv_handler, tw_handler);
+    return nullptr;
+  }
+
   pn_ctx* ctx() { return ctx_; }
   hipStream_t stream() { return stream_; }
   Mode mode() const { return mode_; }
@@ -189,31 +212,39 @@ class GpuRx {
         if (const char* e = launch_k(k + 1)) return e;
       if (hipEventSynchronize(done_[k & 1]) != hipSuccess) return "hipEventSynchronize failed";
       const uint32_t base = k * cap_, m = std::min(cap_, n - base);
-      const pn_result* res = h_res_[k & 1];
-      for (uint32_t i = 0; i < m; i++) {
-        const uint8_t* eth = eth_of(base + i);
-        const pn_result& r = res[i];
-        uint32_t ip_be;
-        uint16_t port_be;
-        std::memcpy(&ip_be, eth + 14 + 12, 4);  // ip_hdr->src_ip
-        std::memcpy(&port_be, eth + 14 + 20, 2); // tcp_hdr->src_port (tcp = ip + 20)
-        const uint64_t key = pn_conn_hash_key(ip_be, port_be);
-        if (r.flags & PN_F_TW) {
-          tw_handler(key, r.conn_id - max_conn_, eth, r);
-        } else {
-          uint32_t idx = PN_MISS;
-          if (!(r.flags & PN_F_HIT)) table.find(key, &idx, nullptr);
-          recv_handler(key, r, eth, idx);
-        }
-      }
+      walk(h_res_[k & 1], base, m, table, eth_of, recv_handler, tw_handler);
     }
     return nullptr;
+  }
+  // Dispatch records res[0, m) of frames base.. in order.
+  template <class EthOf, class RecvHandler, class TwHandler>
+  void walk(const pn_result* res, uint32_t base, uint32_t m, const ConnTable& table, EthOf& eth_of,
+            RecvHandler& recv_handler, TwHandler& tw_handler) {
+    for (uint32_t i = 0; i < m; i++) {
+      const uint8_t* eth = eth_of(base + i);
+      const pn_result& r = res[i];
+      uint32_t ip_be;
+      uint16_t port_be;
+      std::memcpy(&ip_be, eth + 14 + 12, 4);  // ip_hdr->src_ip
+      std::memcpy(&port_be, eth + 14 + 20, 2); // tcp_hdr->src_port (tcp = ip + 20)
+      const uint64_t key = pn_conn_hash_key(ip_be, port_be);
+      if (r.flags & PN_F_TW) {
+        tw_handler(key, r.conn_id - max_conn_, eth, r);
+      } else {
+        uint32_t idx = PN_MISS;
+        if (!(r.flags & PN_F_HIT)) table.find(key, &idx, nullptr);
+        recv_handler(key, r, eth, idx);
+      }
+    }
   }
 
   // Issue chunk k (H2D + classify + D2H, or one zero-copy classify) into buffer k&1.
   const char* launch(const uint8_t* host_slots, uint32_t n, uint32_t k) {
-    const uint32_t base = k * cap_, m = std::min(cap_, n - base), b = k & 1;
-    const uint8_t* src = host_slots + (size_t)base * stride_;
+    const uint32_t base = k * cap_;
+    return launch_at(host_slots + (size_t)base * stride_, std::min(cap_, n - base), k & 1);
+  }
+  // Issue the m slots at src into buffer b.
+  const char* launch_at(const uint8_t* src, uint32_t m, uint32_t b) {
     if (mode_ == Mode::ZeroCopy) {
       if (pn_classify(ctx_, src, stride_, off_, m, h_res_[b], stream_)) return pn_last_error(ctx_);
     } else {

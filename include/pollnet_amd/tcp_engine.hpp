@@ -69,6 +69,8 @@ PN_CONF_OPT(RxLatencyBudgetUs, uint32_t, 0) // hold received frames up to this l
 PN_CONF_OPT(TxBatch, uint32_t, 1024)        // frames per pn_tx_fill launch
 PN_CONF_OPT(RxChunk, uint32_t, 0)           // frames per classify launch within a poll (0 = RxBatch): chunk
                                             // k+1 is on the GPU while chunk k is dispatched
+PN_CONF_OPT(RxPipeline, bool, false)        // throughput mode: a poll's frames are classified while the
+                                            // previous poll's are dispatched (one poll of added latency)
 PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
 PN_CONF_OPT(Device, int, 0)
 PN_CONF_OPT(ReferenceLiteralTable, bool, false) // PN_TABLE_REFERENCE_LITERAL: the reference's rehash, defect kept
@@ -274,24 +276,46 @@ class GpuBackend {
   GpuBackend(const GpuBackend&) = delete;
   GpuBackend& operator=(const GpuBackend&) = delete;
   ~GpuBackend() {
+    if (tx_stream_) {
+      (void)hipStreamSynchronize(tx_stream_);
+      (void)hipStreamDestroy(tx_stream_);
+    }
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
   }
 
   // rx_chunk: frames per classify launch (a poll's frames go in chunks, the next one on the
-  // GPU while the host dispatches the current one; 0 = one launch per poll).
-  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0) {
+  // GPU while the host dispatches the current one; 0 = one launch per poll).  rx_halves = 2:
+  // two RX rings of rx_cap slots for launch/collect (one in flight while the other fills).
+  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1) {
+    if (rx_ring_) (void)hipHostFree(rx_ring_);
+    if (tx_ring_) (void)hipHostFree(tx_ring_);
+    rx_ring_ = tx_ring_ = nullptr;
     const uint32_t chunk = rx_chunk && rx_chunk < rx_cap ? rx_chunk : rx_cap;
     if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy)) return e;
-    if (hipHostMalloc((void**)&rx_ring_, (size_t)kStride * rx_cap, hipHostMallocDefault) != hipSuccess)
+    // the TX fill has a stream of its own: pipelined, it runs beside the next batch's classify
+    if (!tx_stream_ && hipStreamCreateWithFlags(&tx_stream_, hipStreamNonBlocking) != hipSuccess)
+      return "hipStreamCreate(tx) failed";
+    rx_cap_ = rx_cap;
+    const size_t rx_bytes = (size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1);
+    if (hipHostMalloc((void**)&rx_ring_, rx_bytes, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(rx ring) failed";
     if (hipHostMalloc((void**)&tx_ring_, (size_t)kStride * tx_cap, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(tx batch) failed";
-    std::memset(rx_ring_, 0, (size_t)kStride * rx_cap);
+    std::memset(rx_ring_, 0, rx_bytes);
     std::memset(tx_ring_, 0, (size_t)kStride * tx_cap);
     return nullptr;
   }
-  uint8_t* rxSlots() { return rx_ring_; }
+  uint8_t* rxSlots(uint32_t half = 0) { return rx_ring_ + (size_t)half * rx_cap_ * kStride; }
+  // Pipelined RX: launch classifies the first n slots of one half against the snapshot on the
+  // device (syncTable); collect waits for it and calls f(key, rec, eth) in ring order.
+  const char* launch(uint32_t half, uint32_t n, const ConnTable&) { return rx_.submit(rxSlots(half), n, half); }
+  template <class F>
+  const char* collect(uint32_t half, uint32_t n, const ConnTable& t, F&& f) {
+    return rx_.complete(
+        rxSlots(half), n, half, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
+        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
+  }
   uint8_t* txSlots() { return tx_ring_; }
   const char* syncTable(const ConnTable& t) { return rx_.syncTable(t); }
   // f(key, rec, eth) for the n frames of the RX ring, in ring order.
@@ -303,16 +327,18 @@ class GpuBackend {
   }
   // IP + TCP checksums of the first n TX slots (PN_TX_TCP: SendBuf::setOptDataLen, Core.h:157-163).
   const char* fillTx(uint32_t n) {
-    if (pn_tx_fill(rx_.ctx(), tx_ring_, kStride, kFrameOff, n, nullptr, PN_TX_TCP, rx_.stream()))
+    if (pn_tx_fill(rx_.ctx(), tx_ring_, kStride, kFrameOff, n, nullptr, PN_TX_TCP, tx_stream_))
       return pn_last_error(rx_.ctx());
-    if (hipStreamSynchronize(rx_.stream()) != hipSuccess) return "hipStreamSynchronize(tx_fill) failed";
+    if (hipStreamSynchronize(tx_stream_) != hipSuccess) return "hipStreamSynchronize(tx_fill) failed";
     return nullptr;
   }
 
  private:
   GpuRx rx_;
+  hipStream_t tx_stream_ = nullptr;
   uint8_t* rx_ring_ = nullptr;
   uint8_t* tx_ring_ = nullptr;
+  uint32_t rx_cap_ = 0;
 };
 
 
@@ -342,6 +368,8 @@ class TcpEngine {
   static constexpr uint32_t kTxBatch = srv_detail::opt_TxBatch<Conf>::value;
   static constexpr uint32_t kRxBudgetUs = srv_detail::opt_RxLatencyBudgetUs<Conf>::value;
   static constexpr uint32_t kRxChunk = srv_detail::opt_RxChunk<Conf>::value;
+  static constexpr bool kRxPipeline = srv_detail::opt_RxPipeline<Conf>::value;
+  static_assert(!(kRxPipeline && kRxChunk), "RxPipeline and RxChunk are alternatives");
   static constexpr uint32_t kSendTimeoutMs = srv_detail::opt_SendTimeoutSec<Conf>::value * 1000;
   static constexpr uint32_t kRecvTimeoutMs = srv_detail::opt_RecvTimeoutSec<Conf>::value * 1000;
   static_assert(kSendBufCnt >= 4 && !(kSendBufCnt & (kSendBufCnt - 1)), "ConnSendBufCnt must be a power of 2");
@@ -435,6 +463,8 @@ class TcpEngine {
 
   Link& link() { return link_; }
   Backend& backend() { return be_; } // measurement: the per-frame legs timed on their own
+  // Records re-resolved on the host because the table changed after their snapshot.
+  uint64_t reResolved() const { return re_resolved_; }
   // Drop checksum-failed frames before they touch any state (what the NIC's RX checksum
   // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.
   void setDropBadChecksum(bool drop) { drop_bad_ = drop; }
@@ -515,7 +545,8 @@ class TcpEngine {
     }
     std::memcpy(local_mac_, link_.localMac(), 6);
     if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
-    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk)) return e;
+    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1))
+      return e;
     free_conns_.clear();
     for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i
     free_tws_.clear();
@@ -541,8 +572,9 @@ class TcpEngine {
       c.fin_sent_ = c.fin_received_ = true;
     }
     for (uint32_t i = 0; i < kMaxTw; i++) tws_[i].timer.owner = kMaxConn + i;
-    tx_n_ = rx_pending_ = 0;
-    dirty_ = true;
+    tx_n_ = rx_pending_ = cur_ = 0;
+    fl_n_[0] = fl_n_[1] = 0;
+    ++tver_;
     ready_ = true;
     return nullptr;
   }
@@ -561,7 +593,7 @@ class TcpEngine {
   template <class HH>
   void pollEngine(HH& h, int64_t now) {
     wheel_.tick((uint32_t)(now >> 20), [&](TimerNode* n) { onTimer(h, n); }); // Core::pollTime
-    const uint32_t got = link_.fill(be_.rxSlots() + (size_t)rx_pending_ * Backend::kStride, Backend::kStride,
+    const uint32_t got = link_.fill(be_.rxSlots(cur_) + (size_t)rx_pending_ * Backend::kStride, Backend::kStride,
                                     Backend::kFrameOff, kRxBatch - rx_pending_);
     if (got && rx_pending_ == 0) rx_first_ns_ = now;
     rx_pending_ += got;
@@ -569,14 +601,29 @@ class TcpEngine {
     const uint32_t n = due ? rx_pending_ : 0;
     if (n) {
       rx_pending_ = 0;
-      if (dirty_ && Backend::kSnapshot) {
+      if (Backend::kSnapshot && tver_ != synced_ver_) {
         if ((err_ = be_.syncTable(table_))) return;
+        synced_ver_ = tver_;
       }
-      dirty_ = false;
-      const char* e = be_.classify(n, table_, [&](uint64_t key, const pn_result& r, const uint8_t* eth) {
-        onFrame(h, key, r, eth);
-      });
-      if (e) err_ = e;
+    }
+    auto frame = [&](uint64_t key, const pn_result& r, const uint8_t* eth) { onFrame(h, key, r, eth); };
+    if constexpr (kRxPipeline) {
+      // launch this poll's frames, then dispatch the previous poll's while they are classified
+      if (n) {
+        if ((err_ = be_.launch(cur_, n, table_))) return;
+        fl_n_[cur_] = n;
+        fl_ver_[cur_] = tver_;
+      }
+      const uint32_t prev = cur_ ^ 1;
+      if (const uint32_t m = fl_n_[prev]) {
+        fl_n_[prev] = 0;
+        disp_ver_ = fl_ver_[prev];
+        if (const char* e = be_.collect(prev, m, table_, frame)) err_ = e;
+      }
+      if (n) cur_ ^= 1;
+    } else if (n) {
+      disp_ver_ = tver_;
+      if (const char* e = be_.classify(n, table_, frame)) err_ = e;
     }
     flushTx();
   }
@@ -588,7 +635,10 @@ class TcpEngine {
     if (!self().accepts(eth)) return; // the NIC filter (Core.h:335-383)
     if (drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
     pn_result r = rec;
-    if (dirty_ && Backend::kSnapshot) { // the table changed earlier in this batch: probe the live one
+    // the record came from a table snapshot that has changed since (earlier in this batch, or,
+    // pipelined, after the launch): probe the live table
+    if ((Backend::kSnapshot || kRxPipeline) && tver_ != disp_ver_) {
+      ++re_resolved_;
       uint32_t conn_id = PN_MISS;
       const bool hit = table_.find(key, nullptr, &conn_id);
       r.conn_id = conn_id;
@@ -632,7 +682,7 @@ class TcpEngine {
     free_conns_.pop_back();
     ++conn_cnt_;
     table_.add(key, id);
-    dirty_ = true;
+    ++tver_;
     return &conns_[id];
   }
   void resetConn(Conn& c, uint64_t key, const uint8_t* peer_mac, uint32_t peer_ip, uint16_t peer_port,
@@ -898,7 +948,7 @@ class TcpEngine {
     free_tws_.pop_back();
     ++tw_cnt_;
     table_.enterTW(c.key_, tw_id);
-    dirty_ = true;
+    ++tver_;
     Tw& tw = tws_[tw_id];
     tw.key = c.key_;
     std::memcpy(tw.peer_mac, c.peer_mac_, 6);
@@ -922,7 +972,7 @@ class TcpEngine {
       --tw_cnt_;
     }
     table_.del(key);
-    dirty_ = true;
+    ++tver_;
   }
 
   template <class HH>
@@ -1057,7 +1107,12 @@ class TcpEngine {
   int64_t rx_first_ns_ = 0;
   uint32_t local_ip_ = 0, rst_ack_ = 0;
   uint8_t local_mac_[6] = {};
-  bool ready_ = false, dirty_ = true, drop_bad_ = true;
+  // table versions: tver_ counts table changes; synced_ver_ is the device snapshot's, disp_ver_
+  // that of the records being dispatched; fl_* the pipelined batch in flight per ring half
+  uint64_t tver_ = 1, synced_ver_ = 0, disp_ver_ = 0, fl_ver_[2] = {0, 0};
+  uint32_t cur_ = 0, fl_n_[2] = {0, 0};
+  uint64_t re_resolved_ = 0;
+  bool ready_ = false, drop_bad_ = true;
   const char* err_ = "Closed";
 };
 

@@ -29,7 +29,10 @@
 //     entry, the handshake ACK must acknowledge the ISN (else RST), then the connection is
 //     established and the same segment goes on to onPack.
 // Conf::RxLatencyBudgetUs (default 0: every poll with frames classifies them) lets frames of
-// consecutive polls accumulate for up to that long before one launch takes them all.
+// consecutive polls accumulate for up to that long before one launch takes them all;
+// Conf::RxChunk splits a poll's classify into launches overlapped with dispatch; Conf::RxPipeline
+// dispatches each poll's frames in the next poll, their classify overlapped with this poll's
+// dispatch (throughput mode).
 #pragma once
 
 #include "tcp_engine.hpp"

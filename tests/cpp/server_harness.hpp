@@ -43,28 +43,53 @@ struct OracleBackend {
   static constexpr bool kSnapshot = false;
   static constexpr uint32_t kStride = 2048, kFrameOff = 2;
   std::vector<uint8_t> rx, tx;
-  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0) {
-    rx.assign((size_t)kStride * rx_cap, 0);
+  std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
+  uint32_t cap = 0;
+  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0, uint32_t rx_halves = 1) {
+    cap = rx_cap;
+    rx.assign((size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1), 0);
     tx.assign((size_t)kStride * tx_cap, 0);
+    recs[0].assign(rx_cap, pn_result{});
+    recs[1].assign(rx_cap, pn_result{});
     return nullptr;
   }
-  uint8_t* rxSlots() { return rx.data(); }
+  uint8_t* rxSlots(uint32_t half = 0) { return rx.data() + (size_t)half * cap * kStride; }
   uint8_t* txSlots() { return tx.data(); }
   const char* syncTable(const pollnet_amd::ConnTable&) { return nullptr; }
+  static uint64_t keyOf(const uint8_t* eth) {
+    uint32_t ip_be;
+    uint16_t port_be;
+    std::memcpy(&ip_be, eth + 26, 4);
+    std::memcpy(&port_be, eth + 34, 2);
+    return pn_conn_hash_key(ip_be, port_be);
+  }
+  static void one(const uint8_t* eth, const pollnet_amd::ConnTable& t, pn_result* r) {
+    uint32_t ne = 0;
+    uint64_t mask = 0;
+    const pn_conn_entry* e = t.entries(&ne, &mask);
+    orc_classify_frame(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), r);
+  }
+  // sequential: each frame against the live table, just before its dispatch
   template <class F>
   const char* classify(uint32_t n, const pollnet_amd::ConnTable& t, F&& f) {
     for (uint32_t i = 0; i < n; i++) {
       const uint8_t* eth = rx.data() + (size_t)i * kStride + kFrameOff;
-      uint32_t ne = 0;
-      uint64_t mask = 0;
-      const pn_conn_entry* e = t.entries(&ne, &mask);
       pn_result r;
-      orc_classify_frame(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), &r);
-      uint32_t ip_be;
-      uint16_t port_be;
-      std::memcpy(&ip_be, eth + 26, 4);
-      std::memcpy(&port_be, eth + 34, 2);
-      f(pn_conn_hash_key(ip_be, port_be), r, eth);
+      one(eth, t, &r);
+      f(keyOf(eth), r, eth);
+    }
+    return nullptr;
+  }
+  // pipelined: the whole half against the table as it is at launch (the GPU's snapshot)
+  const char* launch(uint32_t half, uint32_t n, const pollnet_amd::ConnTable& t) {
+    for (uint32_t i = 0; i < n; i++) one(rxSlots(half) + (size_t)i * kStride + kFrameOff, t, &recs[half][i]);
+    return nullptr;
+  }
+  template <class F>
+  const char* collect(uint32_t half, uint32_t n, const pollnet_amd::ConnTable&, F&& f) {
+    for (uint32_t i = 0; i < n; i++) {
+      const uint8_t* eth = rxSlots(half) + (size_t)i * kStride + kFrameOff;
+      f(keyOf(eth), recs[half][i], eth);
     }
     return nullptr;
   }

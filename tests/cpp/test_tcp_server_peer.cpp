@@ -31,6 +31,7 @@
 using namespace pollnet_amd;
 
 struct PeerConf {
+  static const bool RxPipeline = false;
   static const uint32_t RecvBufSize = 8192;
   static const uint32_t MaxConns = 48;
   static const uint32_t SendTimeoutSec = 0;
@@ -48,6 +49,15 @@ struct PeerConf {
 // the same with received frames held up to 3 ms for a fuller GPU batch
 struct PeerConfBudget : PeerConf {
   static const uint32_t RxLatencyBudgetUs = 3000;
+};
+// a poll's frames classified in launches of 16 (the next on the GPU while one is dispatched)
+struct PeerConfChunk : PeerConf {
+  static const uint32_t RxChunk = 16;
+};
+// throughput mode: each poll's frames dispatched in the next poll, classified meanwhile
+// against the table as it was at their launch (re-resolved where it has changed since)
+struct PeerConfPipe : PeerConf {
+  static const bool RxPipeline = true;
 };
 
 static const int64_t kT0 = (int64_t)777777 << 20;
@@ -423,8 +433,11 @@ static int scenario(bool gpu, const std::vector<Client>& pop, const char* name) 
   int fail = 0;
   Run<OracleBackend, Conf> twin;
   if (!twin.go(pop)) return 100;
-  std::printf("[%s]\n", name);
+  std::printf("[%s] twin: %llu records re-resolved against the live table\n", name,
+              (unsigned long long)twin.srv->reResolved());
   fail += check("twin", twin);
+  // pipelined, connections are accepted between a batch's launch and its dispatch
+  if (Conf::RxPipeline && !twin.srv->reResolved()) fail++, std::printf("FAIL: no re-resolved record\n");
   if (gpu) {
     Run<GpuBackend, Conf> g;
     if (!g.go(pop)) return 100;
@@ -447,6 +460,8 @@ int main(int argc, char** argv) {
   const auto pop = population();
   int fail = scenario<PeerConf>(gpu, pop, "classify every poll");
   fail += scenario<PeerConfBudget>(gpu, pop, "3-ms RX latency budget");
+  fail += scenario<PeerConfChunk>(gpu, pop, "RX chunks of 16");
+  fail += scenario<PeerConfPipe>(gpu, pop, "pipelined RX (dispatch one poll later)");
   std::printf("%s\n", fail ? "FAIL" : "PASS");
   return fail ? 1 : 0;
 }
