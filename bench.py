@@ -102,57 +102,87 @@ def cpu_threads():
     return min(n, q) if q else n
 
 
-def cpu_baseline(slots, n, entries, mask, max_conn, budget_s):
-    """The oracle (a C port of the reference path, "port") on this host's cores:
-    'ref parse + checksum' (Core::checksum + pollNet + onPack header, Core.h:448-526,
-    TcpConn.h:469-473), all available cores and 1 thread, plus the release path (no checksum)."""
+def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
+    """The reference's own per-frame code, compiled from /root/reference into oracle/_ref/libref_core.so
+    (kind "reference": Core::checksum + connHashKey + findConnEntry + the TIME_WAIT test + TcpConn::onPack's
+    head, oracle/ref_core.cc ref_bench_batch), on this host's cores; the oracle's C port of the same path
+    ("port", oracle/pn_oracle.c orc_refsum_batch) and the release path (no checksum) beside it.  Falls back
+    to the port as the headline when libref_core.so is absent.  The reference's digest over the sample is
+    compared with the same digest of the GPU's records for those frames."""
     import pollnet_amd as pa
     from oracle import pyoracle as orc
 
     threads = cpu_threads()
     sample = min(n, 1 << 18)  # 256 Ki frames (~0.4 GB of frame bytes)
     wire = pa.wire_bytes(slots, STRIDE, FRAME_OFF, sample)
+    ref = None
+    try:
+        ref = orc.RefBench(entries) if orc.ref_core() is not None else None
+    except (OSError, AttributeError):
+        ref = None
 
-    def rate(fn_threads, release, secs):
+    def port(th, release=False):
+        orc.classify_batch(slots, STRIDE, FRAME_OFF, sample, entries, mask, max_conn, threads=th, release=release,
+                           ref_only=not release)
+
+    def reference(th):
+        ref.batch(slots, STRIDE, FRAME_OFF, sample, th)
+
+    def rate(fn, th, secs):
         t0 = time.perf_counter()
         passes = 0
         while True:
-            orc.classify_batch(slots, STRIDE, FRAME_OFF, sample, entries, mask, max_conn, threads=fn_threads,
-                               release=release, ref_only=not release)
+            fn(th)
             passes += 1
             el = time.perf_counter() - t0
             if el >= secs:
                 return passes * sample / el, passes * wire * 8 / el / 1e9, passes
 
+    head = reference if ref is not None else port
     c1 = c1_socket_loopback()
     # the box's share of a large host can be smaller than its affinity mask: probe a few thread
     # counts up to the available cores and measure at the fastest (stated in the line)
     sweep = {}
     for t in sorted({c for c in (8, 16, 32, 64, threads) if c <= threads}):
-        sweep[t] = round(rate(t, False, budget_s * 0.06)[1], 1)
-    threads = max(sweep, key=sweep.get)
-    fr_mt, gb_mt, p_mt = rate(threads, False, budget_s * 0.4)
-    fr_1, gb_1, p_1 = rate(1, False, budget_s * 0.3)
-    fr_rel, gb_rel, _ = rate(1, True, budget_s * 0.2)
-    return {
+        sweep[t] = round(rate(head, t, budget_s * 0.05)[1], 1)
+    best = max(sweep, key=sweep.get)
+    fr_mt, gb_mt, p_mt = rate(head, best, budget_s * 0.3)
+    fr_1, gb_1, _ = rate(head, 1, budget_s * 0.2)
+    fr_rel, gb_rel, _ = rate(lambda th: port(th, True), 1, budget_s * 0.1)
+    code = ("the reference's own Core.h / TcpConn.h code (oracle/ref_core.cc ref_bench_batch, compiled from "
+            "/root/reference by oracle/ref.mk, g++ -O3 -march=x86-64-v3)" if ref is not None else
+            "'ref parse + checksum' port (oracle/pn_oracle.c orc_refsum_batch, -O3 -march=x86-64-v3)")
+    out = {
         "value": round(gb_mt, 2),
         "unit": "Gbit/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"'ref parse + checksum' (orc_refsum_batch: Core::checksum + pollNet + onPack header) over "
-                  f"{sample} frames of the same workload, {p_mt} passes; oracle/pn_oracle.c -O3 -march=x86-64-v3, "
-                  f"contiguous index shards over {threads} threads, the fastest of a sweep up to this process's "
-                  f"{cpu_threads()} available cores (CPU affinity {len(os.sched_getaffinity(0))}, cgroup CPU quota "
-                  f"{cgroup_cpu_quota()}, machine {os.cpu_count()})",
+        "cores": best,
+        "kind": "reference" if ref is not None else "port",
+        "sample": f"Core::checksum + pollNet's key/probe/TIME_WAIT test + onPack's payload head per frame, {code}, "
+                  f"over {sample} frames of the same workload, {p_mt} passes; contiguous index shards over {best} "
+                  f"threads, the fastest of a sweep up to this process's {cpu_threads()} available cores (CPU "
+                  f"affinity {len(os.sched_getaffinity(0))}, cgroup CPU quota {cgroup_cpu_quota()}, machine "
+                  f"{os.cpu_count()})",
         "mframes_per_s": round(fr_mt / 1e6, 3),
         "thread_sweep_gbit_per_s": sweep,
         "single_thread": {"value": round(gb_1, 2), "unit": "Gbit/s", "mframes_per_s": round(fr_1 / 1e6, 3),
                           "cores": 1},
         "release_path_no_checksum_1t": {"value": round(gb_rel, 2), "unit": "Gbit/s",
-                                        "mframes_per_s": round(fr_rel / 1e6, 3), "cores": 1},
+                                        "mframes_per_s": round(fr_rel / 1e6, 3), "cores": 1, "kind": "port"},
         "host_cpu": _cpu_model(),
         "c1_socket_loopback_ref": c1,
     }
+    if ref is not None:
+        fr_p, gb_p, _ = rate(port, best, budget_s * 0.15)
+        fr_p1, gb_p1, _ = rate(port, 1, budget_s * 0.1)
+        out["port"] = {"value": round(gb_p, 2), "unit": "Gbit/s", "mframes_per_s": round(fr_p / 1e6, 3),
+                       "cores": best, "single_thread_gbit_per_s": round(gb_p1, 2),
+                       "code": "oracle/pn_oracle.c orc_refsum_batch (the oracle's restatement of the same path)"}
+        if gpu_records is not None:
+            digest, n_valid = ref.batch(slots, STRIDE, FRAME_OFF, sample, best)
+            rec = np.ascontiguousarray(gpu_records[: sample * 16]).view(pa.RESULT_DTYPE)
+            out["reference_agrees_with_gpu_records"] = digest == orc.records_digest(rec)
+            out["reference_frames_verified"] = n_valid
+    return out
 
 
 def c1_socket_loopback(seconds=1.5):
@@ -442,7 +472,17 @@ def secondary_tx(torch, pa, n, steps, stream):
 
 
 # ----------------------------------------------------------------------------- ranks
+def _json_stdout():
+    """stdout carries the one JSON line only: fd 1 is pointed at stderr for everything else
+    (gloo's C++ connection log, library prints) and the line goes to the saved original."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(saved, "w")
+
+
 def run_rank(rank, world, local_rank, args):
+    json_out = _json_stdout()
     import torch
     import torch.distributed as dist
 
@@ -619,11 +659,13 @@ def run_rank(rank, world, local_rank, args):
         except Exception as ex:  # measured extra; never blocks the bench line
             out["e2e_pinned_host"] = {"error": str(ex)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(slots, n, entries, mask, table.max_conn_cnt, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(slots, n, entries, mask, table.max_conn_cnt, args.cpu_seconds,
+                                           gpu_records=got0 if (R > 1 or lo == 0) else None)
     if rank == 0:
         if "WORLD_SIZE" not in os.environ or os.environ.get("PN_BENCH_SPAWNED") == "1":
             assert out["n_gpus"] == args.gpus, (out["n_gpus"], args.gpus)
-        print(json.dumps(out), flush=True)
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

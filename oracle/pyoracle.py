@@ -228,6 +228,9 @@ def ref_core():
             ("ref_table_entries", _u32, [_vp, _vp, _vp, _vp]),
             ("ref_table_debug_exits", _i32, [_vp]),
             ("ref_table_total_size", _u32, []),
+            ("ref_bench_new", _vp, [_vp, _vp, _u32]),
+            ("ref_bench_free", None, [_vp]),
+            ("ref_bench_batch", _u64, [_vp, _vp, _u32, _u32, _u32, _i32, _vp]),
         ):
             f = getattr(lib, name)
             f.restype, f.argtypes = res, args
@@ -274,3 +277,47 @@ class RefCoreTable:
     @property
     def debug_exits(self):
         return int(self.lib.ref_table_debug_exits(self.h))
+
+
+class RefBench:
+    """The reference's own per-frame code (Core::checksum, connHashKey + findConnEntry, the
+    TIME_WAIT test, TcpConn::onPack's head; oracle/ref_core.cc ref_bench_batch) over a slot ring,
+    with a MaxConnCnt = 1024 table holding the given entries: bench.py's CPU baseline of kind
+    "reference".  batch() returns (digest, frames verified)."""
+
+    def __init__(self, entries: np.ndarray):
+        self.lib = ref_core()
+        ent = np.ascontiguousarray(entries, dtype=ENTRY_DTYPE)
+        live = ent[ent["key"] != np.uint64(1 << 63)]
+        keys = np.ascontiguousarray(live["key"])
+        cids = np.ascontiguousarray(live["conn_id"])
+        self.h = self.lib.ref_bench_new(keys.ctypes.data, cids.ctypes.data, len(live))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.lib.ref_bench_free(self.h)
+            self.h = None
+
+    def batch(self, slots: np.ndarray, stride: int, frame_off: int, n: int, threads: int = 1):
+        assert slots.dtype == np.uint8 and slots.flags.c_contiguous and slots.size >= n * stride
+        valid = _u32(0)
+        d = self.lib.ref_bench_batch(self.h, slots.ctypes.data, stride, frame_off, n, threads, C.byref(valid))
+        return int(d), int(valid.value)
+
+
+def records_digest(rec: np.ndarray) -> int:
+    """ref_bench_batch's digest (oracle/ref_core.cc ref_frame_digest) computed from pn_result
+    records: (IP_OK and TCP_OK, HIT, TW, conn_id on hit, payload_off, payload_len, seq)."""
+    u = np.uint64
+    fl = rec["flags"].astype(u)
+    verified = ((fl & u(3)) == u(3)).astype(u)
+    hit = (fl >> u(2)) & u(1)
+    tw = (fl >> u(3)) & u(1)
+    conn = np.where(hit == u(1), rec["conn_id"].astype(u), u(0xFFFFFFFF))
+    x = verified | (hit << u(1)) | (tw << u(2)) | (conn << u(3))
+    plen = rec["payload_len"].astype(np.int64).astype(np.uint32).astype(u)
+    with np.errstate(over="ignore"):
+        x ^= ((rec["payload_off"].astype(u) << u(32)) | plen) * u(0x9E3779B97F4A7C15)
+        x ^= rec["seq"].astype(u) * u(0xC2B2AE3D27D4EB4F)
+        d = (x * u(0xD6E8FEB86659FD93)) ^ (x >> u(29))
+        return int(d.sum(dtype=u))

@@ -58,4 +58,4 @@ _ref/onpack_head.inc: $(REFDIR)/efvitcp/TcpConn.h
 	sed -n '468p' $< | grep -q 'void onPack' && sed -n '473p' $< | grep -q 'seq_num' && sed -n '474p' $< | grep -q got_ts
 	sed -n '469,473p' $< > $@
 _ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc _ref/onpack_head.inc
-	g++ -O2 -std=c++17 -fPIC -shared -Wno-unused-result -o $@ ref_core.cc
+	g++ -O3 -march=x86-64-v3 -std=c++17 -fPIC -shared -pthread -Wno-unused-result -o $@ ref_core.cc

@@ -14,7 +14,8 @@
 // and execution continues (the reference process would end there).  No ef_vi header is
 // needed or faked: none of these lines touches ef_vi.
 // Nothing here is shipped or used by the product path; tests/test_ref_core.py pins the
-// oracle (oracle/pn_oracle.c) and the product's conn table against it.
+// oracle (oracle/pn_oracle.c) and the product's conn table against it, and bench.py times
+// ref_bench_batch as its CPU baseline (kind "reference": the reference's own code, run here).
 #define EFVITCP_DEBUG
 #include <arpa/inet.h>
 
@@ -25,7 +26,9 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <utility>
+#include <vector>
 
 namespace efvitcp {
 using std::endl;
@@ -198,6 +201,92 @@ uint32_t ref_table_entries(void* tp, uint64_t* keys, uint32_t* conn_ids, uint64_
   return Ref::TotalTableSize;
 }
 uint32_t ref_table_total_size() { return Ref::TotalTableSize; }
+
+// ---- the CPU baseline: the reference's own per-frame code over a ring of slots ----
+// Per frame, in pollNet's order (Core.h:503-510, debug build): Core::checksum (Core.h:448-472),
+// key = connHashKey(src_ip, src_port), entry = findConnEntry(key), the TIME_WAIT test, and
+// TcpConn::onPack's payload extent and seq (TcpConn.h:469-473).  The table is the bench's
+// (MaxConnCnt = MaxTimeWaitConnCnt = 1024, pollnet_amd.rx.GenParams), one copy per thread.
+// Each frame folds into a digest over (verified, hit, tw, conn_id, payload_off, payload_len,
+// seq) so the work is observable and comparable with the oracle's records
+// (tests/test_ref_core.py).
+using RefBench = efvitcp::RefCore<1024, 1024>;
+
+void* ref_bench_new(const uint64_t* keys, const uint32_t* conn_ids, uint32_t n) {
+  RefBench* t = new RefBench();
+  for (uint32_t i = 0; i < n; i++) {
+    efvitcp::ConnHashEntry* e = t->findConnEntry(keys[i]);
+    if (e->key == keys[i]) continue;
+    if (conn_ids[i] < 1024) t->conn_cnt++;
+    else t->tw_cnt++;
+    t->addConnEntry(e, keys[i], conn_ids[i]);
+  }
+  return t;
+}
+void ref_bench_free(void* t) { delete static_cast<RefBench*>(t); }
+
+static inline uint64_t ref_frame_digest(RefBench& t, uint8_t* eth) {
+  using namespace efvitcp;
+  IpHeader* ip_hdr = reinterpret_cast<IpHeader*>(eth + sizeof(EtherHeader));
+  const int exits0 = t.exits;
+  t.checksum(ip_hdr);
+  const bool verified = t.exits == exits0;
+  TcpHeader* th = reinterpret_cast<TcpHeader*>(ip_hdr + 1);
+  const uint64_t key = connHashKey(ip_hdr->src_ip, th->src_port);
+  ConnHashEntry* entry = t.findConnEntry(key);
+  const bool hit = entry->key == key;
+  const bool tw = hit && entry->conn_id >= 1024;
+#include "_ref/onpack_head.inc"
+  (void)opt;
+  const uint64_t conn = hit ? entry->conn_id : 0xffffffffu;
+  uint64_t x = (uint64_t)verified | (uint64_t)hit << 1 | (uint64_t)tw << 2 | conn << 3;
+  x ^= ((uint64_t)(uint32_t)(data - eth) << 32 | (uint32_t)(int32_t)(data_end - data)) * 0x9E3779B97F4A7C15ull;
+  x ^= (uint64_t)seq_num * 0xC2B2AE3D27D4EB4Full;
+  return x * 0xD6E8FEB86659FD93ull ^ (x >> 29);
+}
+
+// Frames [0, n) of the slot ring, split into contiguous shards over `threads` threads (each
+// with its own copy of the table).  Returns the digest (sum over frames, order-free); *n_valid
+// = frames whose checksums verified.
+uint64_t ref_bench_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off, uint32_t n, int threads,
+                         uint32_t* n_valid) {
+  RefBench* proto = static_cast<RefBench*>(tp);
+  if (threads < 1) threads = 1;
+  std::vector<uint64_t> dig(threads, 0);
+  std::vector<uint32_t> valid(threads, 0);
+  auto work = [&](int w) {
+    std::unique_ptr<RefBench> t(new RefBench()); // the table members the functions read
+    t->conn_cnt = proto->conn_cnt;
+    t->tw_cnt = proto->tw_cnt;
+    t->tbl_mask = proto->tbl_mask;
+    std::memcpy(t->conn_tbl, proto->conn_tbl, sizeof(t->conn_tbl));
+    const uint32_t b = (uint32_t)((uint64_t)n * w / threads), e = (uint32_t)((uint64_t)n * (w + 1) / threads);
+    uint64_t d = 0;
+    uint32_t v = 0;
+    int exits_cleared = 0;
+    for (uint32_t i = b; i < e; i++) {
+      const int exits0 = t->exits;
+      d += ref_frame_digest(*t, slots + (size_t)i * stride + off);
+      if (t->exits == exits0) {
+        v++;
+      } else if (t->exits - exits_cleared > 256) { // drop the debug build's prints now and then
+        t->cout.os.str(std::string());
+        exits_cleared = t->exits;
+      }
+    }
+    dig[w] = d;
+    valid[w] = v;
+  };
+  std::vector<std::thread> pool;
+  for (int w = 1; w < threads; w++) pool.emplace_back(work, w);
+  work(0);
+  for (auto& th : pool) th.join();
+  uint64_t d = 0;
+  uint32_t v = 0;
+  for (int w = 0; w < threads; w++) d += dig[w], v += valid[w];
+  if (n_valid) *n_valid = v;
+  return d;
+}
 // how many times the debug build's rehash check fired (Core.h:665-669: it would have exited)
 int ref_table_debug_exits(void* tp) { return static_cast<Ref*>(tp)->exits; }
 

@@ -145,6 +145,8 @@ def test_bench_spawns_ranks_itself():
                        capture_output=True, text=True, timeout=240, env={k: v for k, v in os.environ.items()
                                                                         if k not in ("WORLD_SIZE", "RANK")})
     assert p.returncode == 0, p.stderr[-3000:]
-    line = json.loads(p.stdout.strip().splitlines()[-1])
+    lines = p.stdout.strip().splitlines()
+    assert len(lines) == 1, lines  # stdout is the JSON line alone (gloo's own log goes to stderr)
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
     assert line["config"]["global_frames"] == 2 * 65536

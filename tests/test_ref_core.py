@@ -186,3 +186,46 @@ def test_conn_table_matches_reference_member_functions(seed, steps, cluster):
     for k, cid in live.items():  # the product's default table finds every live key
         _, hit, got = pt.find(k)
         assert hit and got == cid
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_reference_batch_digest_equals_oracle_records(cfg):
+    """ref_bench_batch (bench.py's "reference" CPU baseline: the reference's own per-frame code over
+    a slot ring, threaded) does the same work as the oracle: its digest over (verified, hit, TW,
+    conn_id, payload_off, payload_len, seq) equals the one computed from the oracle's records."""
+    p = pa.rx.GenParams.for_config(cfg)
+    n = 1 << 14
+    slots = pa.gen_frames(p, n, threads=4)
+    entries, mask = pa.gen_conn_table(p).snapshot()
+    rec = orc.classify_batch(slots, 2048, 2, n, entries, mask, p.max_conn_cnt, threads=4)
+    rb = orc.RefBench(entries)
+    for threads in (1, 3):
+        digest, n_valid = rb.batch(slots, 2048, 2, n, threads)
+        assert digest == orc.records_digest(rec)
+        assert n_valid == int(((rec["flags"] & 3) == 3).sum())
+
+
+@pytest.mark.gpu
+def test_gpu_records_digest_equals_reference_batch():
+    """The GPU's records for C5 frames (options, odd lengths, bad checksums, probe cluster) against
+    the reference's own code run on this host: equal digests."""
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    p = pa.rx.GenParams.for_config(5)
+    n = 1 << 15
+    slots = pa.gen_frames(p, n, threads=4)
+    table = pa.gen_conn_table(p)
+    entries, mask = table.snapshot()
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        frames = torch.from_numpy(np.ascontiguousarray(slots).reshape(-1)).cuda()
+        res = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+        ctx.classify(frames, 2048, 2, n, res, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        rec = res.cpu().numpy().view(pa.RESULT_DTYPE)
+    finally:
+        ctx.close()
+    digest, _ = orc.RefBench(entries).batch(slots, 2048, 2, n, 4)
+    assert digest == orc.records_digest(rec)
