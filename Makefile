@@ -28,6 +28,7 @@ TCPRXBENCH = bench/bench_tcp_rx
 LATBENCH = bench/bench_latency
 SRVBENCH = bench/bench_tcp_server
 PINBENCH = bench/bench_pinned
+TXSMALLBENCH = bench/bench_tx_small
 RINGTEST = tests/cpp/test_rx_ring
 STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
@@ -97,6 +98,10 @@ $(SRVBENCH): bench/bench_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server
 	$(HIPCC) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
+# TX fill at small batch sizes, one in-place launch vs two phases (variant 41: make TUNING=1; not in `all`)
+$(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $(LIB) $(TUNING_LIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+
 # zero-copy classify from host rings of each pinned-memory kind: PCIe rate and staleness
 $(PINBENCH): bench/bench_pinned.cpp $(HDRS) $(LIB)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
@@ -129,6 +134,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 .PHONY: all ref clean

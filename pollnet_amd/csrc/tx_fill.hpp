@@ -66,9 +66,10 @@ constexpr uint32_t kPatchOk = 1u << 16, kPatchLen = 2u << 16;
 
 __device__ __forceinline__ void st16(uint8_t* p, uint32_t v) { *reinterpret_cast<uint16_t*>(p) = (uint16_t)v; }
 
-// Where the field values go.  WB = -2 (production): the patch record.  Tuning variants
-// (scripts/tx_variants.py): WB = 0 2-byte stores straight into the frame; WB = 128 patch
-// the cooperative LDS tile and write back the slot's whole first line; WB = -1 nothing.
+// Where the field values go.  WB = -2 (production above kTxInPlaceMaxFrames): the patch record.
+// WB = 0 (production up to it): 2-byte stores straight into the frame.  Tuning variants
+// (scripts/tx_variants.py): WB = 128 patch the cooperative LDS tile and write back the slot's
+// whole first line; WB = -1 nothing.
 constexpr int kWbPatch = -2;
 
 // MODE: PN_TX_TCP, PN_TX_UDP_EFVI or PN_TX_UDP.
@@ -267,29 +268,45 @@ inline bool coop_layout(const TArgs& a) {
   return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }
 
-template <int MIS, int MODE>
+// Up to this many frames a call is ONE launch writing the fields in place: the batch's lines
+// are still cached when they are written, and the patch launch's ≈2-µs boundary is the larger
+// cost (1.5-4.6 µs less per call from 16 to 65,536 frames, pinned host or device memory,
+// bench/bench_tx_small, profiles/r02/tx_fill_small_batches.json).  Above it the two phases
+// (§12: the in-place writes' write-back would land in the rest of the stream).
+constexpr uint32_t kTxInPlaceMaxFrames = 65536;
+
+template <int MIS, int MODE, int WB>
 void launch(const TArgs& a, hipStream_t s) {
   const dim3 grid((a.n + a.fpw - 1) / a.fpw), block(kWave);
   // XCD-contiguous group order, as the RX kernel: -1.7 % (profiles/r01_experiments/tx_xcd_order_off{2,14}.json)
   if (coop_layout(a)) {
-    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, WB, 0, 0, 0, true>), grid, block, 0, s, a);
     return;
   }
-  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, kWbPatch, 0, 0, 0, true>), grid, block, 0, s, a);
+  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, WB, 0, 0, 0, true>), grid, block, 0, s, a);
+}
+
+template <int MODE, int WB>
+void launch_mis(const TArgs& a, uint32_t mis, hipStream_t s) {
+  switch (mis) {
+    case 0: launch<0, MODE, WB>(a, s); break;
+    case 2: launch<2, MODE, WB>(a, s); break;
+    case 4: launch<4, MODE, WB>(a, s); break;
+    case 6: launch<6, MODE, WB>(a, s); break;
+    case 8: launch<8, MODE, WB>(a, s); break;
+    case 10: launch<10, MODE, WB>(a, s); break;
+    case 12: launch<12, MODE, WB>(a, s); break;
+    default: launch<14, MODE, WB>(a, s); break;
+  }
 }
 
 template <int MODE>
 void launch_mode(const TArgs& a, uint32_t mis, hipStream_t s) {
-  switch (mis) {
-    case 0: launch<0, MODE>(a, s); break;
-    case 2: launch<2, MODE>(a, s); break;
-    case 4: launch<4, MODE>(a, s); break;
-    case 6: launch<6, MODE>(a, s); break;
-    case 8: launch<8, MODE>(a, s); break;
-    case 10: launch<10, MODE>(a, s); break;
-    case 12: launch<12, MODE>(a, s); break;
-    default: launch<14, MODE>(a, s); break;
+  if (a.n <= kTxInPlaceMaxFrames) {
+    launch_mis<MODE, 0>(a, mis, s);
+    return;
   }
+  launch_mis<MODE, kWbPatch>(a, mis, s);
   hipLaunchKernelGGL((tx_patch_kernel<MODE>), dim3((a.n + 255) / 256), dim3(256), 0, s, a);
 }
 

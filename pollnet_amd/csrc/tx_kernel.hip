@@ -12,8 +12,10 @@ extern "C" int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint3
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  rc = ensure_patch(ctx, n, s);
-  if (rc) return rc;
+  if (n > kTxInPlaceMaxFrames) { // the two-phase form's patch records (ctx scratch)
+    rc = ensure_patch(ctx, n, s);
+    if (rc) return rc;
+  }
   TArgs a;
   a.frames = (uint8_t*)frames;
   a.lens = lens;

@@ -69,6 +69,20 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
       case 17: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, 0>), grid, block, 0, s, a); return 0;
       case 18: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 0, 0>), grid, block, 0, s, a); return 0;
       case 19: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, 0>), grid, block, 0, s, a); return 0;
+      // the product's launch shape (frames_per_wave(n) per wave, XCD order): 40 = pn_tx_fill's
+      // two phases, 41 = one launch writing the fields in place (small batches: one launch fewer)
+      case 40: case 41: {
+        TArgs b = a;
+        b.fpw = frames_per_wave(n);
+        const dim3 g((n + b.fpw - 1) / b.fpw);
+        if (variant == 41) {
+          hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 0, 0, 0, 0, true>), g, block, 0, s, b);
+        } else {
+          hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), g, block, 0, s, b);
+          hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
+        }
+        return 0;
+      }
       default: return -1;
     }
   };

@@ -219,7 +219,8 @@ def test_gpu_fill_equals_reference_frames(mode, frame_off, lens_too):
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_gpu_fill_random_bytes_all_layouts(mode):
     """Arbitrary bytes (any tot_len, incl. out-of-range ones left untouched), every
-    (frame_off + 14) % 16 class, every line offset of the window block, jumbo slots, ragged n."""
+    (frame_off + 14) % 16 class, every line offset of the window block, jumbo slots, ragged n,
+    both launch forms (in place up to 65,536 frames, two-phase above)."""
     torch, pa = _gpu()
     ctx = pa.RxContext(0)
     rng = np.random.default_rng(mode + 100)
@@ -231,7 +232,10 @@ def test_gpu_fill_random_bytes_all_layouts(mode):
                                  (2048, 18, 300), (2048, 50, 64), (2048, 66, 200), (2048, 98, 70), (2048, 114, 150),
                                  (2048, 126, 129),
                                  # 32 frames per wave (frames_per_wave; 64 in the full-size round trip below)
-                                 (2048, 14, 40000)]:
+                                 (2048, 14, 40000),
+                                 # the one-launch in-place form up to kTxInPlaceMaxFrames = 65,536 frames,
+                                 # the two-phase form (patch records + patch launch) above it
+                                 (2048, 14, 65536), (2048, 2, 70001), (2048, 0, 65537)]:
         avail = stride - frame_off
         slots = rng.integers(0, 256, (n, stride), dtype=np.uint8)
         tot = rng.integers(0, avail + 64, n)
