@@ -417,6 +417,27 @@ def secondary_rx(torch, pa, cfg, n, steps, stream, packed=False):
     return out
 
 
+def server_poll():
+    """The drop-in server itself (bench/bench_tcp_server quick, DESIGN §14): GpuTcpServer::poll over
+    256 connections receiving in-order 1514-B segments from a pinned host ring (handshake, RX, the
+    server's ACKs), GPU backend at RxBatch 512 and pipelined at 16384, and the same server on the
+    sequential CPU backend (the oracle classifying each frame on one core).  PCIe-bound: every frame
+    crosses it for its checksums."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "bench", "bench_tcp_server")
+    if not os.path.exists(exe):
+        return {"error": "bench/bench_tcp_server not built"}
+    try:
+        r = subprocess.run([exe, "256", "400", "quick"], capture_output=True, text=True, timeout=90)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        if r.returncode != 0:
+            line["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
+        return line
+    except Exception as ex:  # measured extra; never blocks the bench line
+        return {"error": repr(ex)}
+
+
 def secondary_tx(torch, pa, n, steps, stream):
     """TX checksum fill (pn_tx_fill, PN_TX_TCP) over C2 batches with both checksum fields
     scrambled, at the ring layout (frame_off 2) and efvitcp's SendBuf layout (frame_off 14 =
@@ -644,6 +665,7 @@ def run_rank(rank, world, local_rank, args):
             sec["tx_fill"] = secondary_tx(torch, pa, n, 20, stream)
         except Exception as ex:  # measured extras; never block the bench line
             sec["error"] = repr(ex)
+        sec["tcp_server_poll"] = server_poll()
         sec["seconds"] = round(time.perf_counter() - t_sec, 1)
         out["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_e2e:

@@ -11,8 +11,9 @@
 // bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
-//   argv: n_flows (256)  polls (400)  [cpu]    prints one JSON line; exit 0 = all data delivered
-//         (cpu: the sequential-backend legs only, no GPU needed)
+//   argv: n_flows (256)  polls (400)  [cpu|quick]   prints one JSON line; exit 0 = all data delivered
+//         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512, GPU
+//         pipelined 16384 and CPU 512 only — bench.py's secondary.tcp_server_poll)
 #include <arpa/inet.h>
 
 #include <chrono>
@@ -264,7 +265,11 @@ int main(int argc, char** argv) {
     ok = ok && r.ok;
   };
   const bool cpu_only = argc > 3 && std::strcmp(argv[3], "cpu") == 0;
-  if (!cpu_only) {
+  if (argc > 3 && std::strcmp(argv[3], "quick") == 0) { // bench.py's secondary leg: three lines
+    leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
+    leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
+    leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
+  } else if (!cpu_only) {
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_4096", runOne<4096, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_16384", runOne<16384, GpuBackend>(n_flows, polls / 4));
@@ -277,9 +282,11 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_4096_pipelined", runOne<4096, GpuBackend, 0, true>(n_flows, polls));
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
   }
-  leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
-  leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
-  leg("cpu_rxbatch_4096_pipelined", runOne<4096, OracleBackend, 0, true>(n_flows, polls / 4));
+  if (argc <= 3 || std::strcmp(argv[3], "quick") != 0) {
+    leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
+    leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
+    leg("cpu_rxbatch_4096_pipelined", runOne<4096, OracleBackend, 0, true>(n_flows, polls / 4));
+  }
   std::printf("{\"bench\": \"tcp_server_poll\", \"workload\": \"%u flows connected through the server's handshake, "
               "in-order 1514-B frames (1460-B payload), RxBatch frames per poll, handler consumes, server ACKs\", "
               "%s, \"delivered_ok\": %s}\n",
