@@ -13,7 +13,7 @@
 // in order (the stream is reliable over the lossy wire), both handler logs and every frame on
 // the wire equal between the two runs; then the client closes (RST), the server sees it go, and
 // the client reconnects (its retry interval has passed).
-//   argv: twin | gpu            exit 0 = pass
+//   argv: twin | gpu  [runs]  [show]   exit 0 = pass (runs: loss patterns, seed 0..runs-1)
 #include <arpa/inet.h>
 
 #include <cstdio>
@@ -59,7 +59,8 @@ struct ClientConf { // example/tcpclient.cc:3-14
 // Two queues; what one end sends reaches the other end's next fill, unless lost.
 struct Wire {
   std::vector<std::vector<uint8_t>> to_server, to_client, log; // log: every frame sent, both ways
-  std::mt19937 loss{0x10553u};
+  std::mt19937 loss;
+  explicit Wire(uint32_t seed = 0) : loss(0x10553u + 0x9E3779B9u * seed) {}
   uint32_t drops = 0;
   uint32_t loss_pct = 4;
   void carry(std::vector<std::vector<uint8_t>>& q, const uint8_t* eth, uint32_t len) {
@@ -156,8 +157,10 @@ struct Result {
 
 template <class S, class C>
 static bool run(S& server, C& client, void (*poll_srv)(), void (*poll_cli)(), LogStream& slog, LogStream& clog,
-                Result& out) {
-  Wire w;
+                Result& out, uint32_t seed) {
+  Wire w(seed);
+  slog.os.str(std::string());
+  clog.os.str(std::string());
   g_wire = &w;
   g_now = kT0;
   if (!server.initWithLink("10.0.0.1", 1234, g_now)) return std::printf("server init: %s\n", server.getLastError()), false;
@@ -223,24 +226,33 @@ static int check(const char* tag, const Result& r) {
 
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
+  const uint32_t runs = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1; // loss patterns (run k: seed k)
+  const bool show = argc > 3;
   int fail = 0;
-  Result tw;
-  if (!run(on_twin::server, on_twin::client, on_twin::srv::pollOnce, on_twin::cli::pollOnce, on_twin::srv::cout,
-           on_twin::cli::cout, tw))
-    return 3;
-  fail += check("twin", tw);
-  if (argc > 2) std::printf("server log:\n%s\nclient log:\n%s\n", tw.srv_log.c_str(), tw.cli_log.c_str());
+  for (uint32_t seed = 0; seed < runs; seed++) {
+    if (runs > 1) std::printf("== loss pattern %u ==\n", seed);
+    on_twin::pack = Packet{}; // the example client's running counter starts over
+    on_gpu::pack = Packet{};
+    Result tw;
+    if (!run(on_twin::server, on_twin::client, on_twin::srv::pollOnce, on_twin::cli::pollOnce, on_twin::srv::cout,
+             on_twin::cli::cout, tw, seed))
+      return 3;
+    fail += check("twin", tw);
+    if (show) std::printf("server log:\n%s\nclient log:\n%s\n", tw.srv_log.c_str(), tw.cli_log.c_str());
+    if (gpu) {
+      Result g;
+      if (!run(on_gpu::server, on_gpu::client, on_gpu::srv::pollOnce, on_gpu::cli::pollOnce, on_gpu::srv::cout,
+               on_gpu::cli::cout, g, seed))
+        return 5;
+      fail += check("gpu", g);
+      const bool logs = g.srv_log == tw.srv_log && g.cli_log == tw.cli_log;
+      const bool wire = g.wire == tw.wire;
+      std::printf("gpu: handler logs %s, wire frames %s (%zu)\n", logs ? "identical" : "DIFFERENT",
+                  wire ? "identical" : "DIFFERENT", g.wire.size());
+      fail += !logs + !wire;
+    }
+  }
   if (gpu) {
-    Result g;
-    if (!run(on_gpu::server, on_gpu::client, on_gpu::srv::pollOnce, on_gpu::cli::pollOnce, on_gpu::srv::cout,
-             on_gpu::cli::cout, g))
-      return 5;
-    fail += check("gpu", g);
-    const bool logs = g.srv_log == tw.srv_log && g.cli_log == tw.cli_log;
-    const bool wire = g.wire == tw.wire;
-    std::printf("gpu: handler logs %s, wire frames %s (%zu)\n", logs ? "identical" : "DIFFERENT",
-                wire ? "identical" : "DIFFERENT", g.wire.size());
-    fail += !logs + !wire;
     delete &on_gpu::client;
     delete &on_gpu::server;
   }

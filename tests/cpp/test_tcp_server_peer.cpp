@@ -80,13 +80,16 @@ struct Client {
   std::map<uint32_t, std::vector<uint8_t>> ooo;
 };
 
+// Population and loss seeds: run k of a soak (argv[2] runs) perturbs both; 0 = the original.
+static uint32_t g_seed = 0;
+
 // The client population as a link: fill() = frames the clients send this tick,
 // send() = a frame from the server, handed to its client.
 struct PeerLink {
   std::vector<Client> clients;
   std::vector<std::vector<uint8_t>> q;   // client -> server, this tick
   std::vector<std::vector<uint8_t>> out; // every server frame (the comparison)
-  std::mt19937 loss{0xD20Bu};
+  std::mt19937 loss{0xD20Bu ^ g_seed};
   uint32_t tick = 0;
   uint32_t drops_c2s = 0, drops_s2c = 0;
 
@@ -335,7 +338,7 @@ struct Run {
 };
 
 static std::vector<Client> population() {
-  std::mt19937_64 rng(0xC11E27ull);
+  std::mt19937_64 rng(0xC11E27ull + 0x9E3779B97F4A7C15ull * g_seed);
   std::vector<Client> cs(120);
   for (uint32_t i = 0; i < cs.size(); i++) {
     Client& c = cs[i];
@@ -457,11 +460,16 @@ static int scenario(bool gpu, const std::vector<Client>& pop, const char* name) 
 
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
-  const auto pop = population();
-  int fail = scenario<PeerConf>(gpu, pop, "classify every poll");
-  fail += scenario<PeerConfBudget>(gpu, pop, "3-ms RX latency budget");
-  fail += scenario<PeerConfChunk>(gpu, pop, "RX chunks of 16");
-  fail += scenario<PeerConfPipe>(gpu, pop, "pipelined RX (dispatch one poll later)");
+  const uint32_t runs = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1; // soak: more populations and loss patterns
+  int fail = 0;
+  for (g_seed = 0; g_seed < runs; g_seed++) {
+    if (runs > 1) std::printf("== population %u ==\n", g_seed);
+    const auto pop = population();
+    fail += scenario<PeerConf>(gpu, pop, "classify every poll");
+    fail += scenario<PeerConfBudget>(gpu, pop, "3-ms RX latency budget");
+    fail += scenario<PeerConfChunk>(gpu, pop, "RX chunks of 16");
+    fail += scenario<PeerConfPipe>(gpu, pop, "pipelined RX (dispatch one poll later)");
+  }
   std::printf("%s\n", fail ? "FAIL" : "PASS");
   return fail ? 1 : 0;
 }

@@ -42,51 +42,56 @@ def test_gpu_server_matches_twin(per_poll):
 PEER = os.path.join(ROOT, "tests", "cpp", "test_tcp_server_peer")
 
 
-def _peer(mode):
+def _peer(mode, populations=1):
     if not os.path.exists(PEER):
         subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tcp_server_peer"], check=True, capture_output=True)
-    return subprocess.run([PEER, mode], capture_output=True, text=True, timeout=300)
+    return subprocess.run([PEER, mode, str(populations)], capture_output=True, text=True, timeout=300)
 
 
 def test_server_twin_reactive_peers():
     """120 reactive in-memory TCP clients with 3 % loss each way and a 1-ms-per-poll
     clock: handshake / SYN-ACK and RTO retransmission, delayed ACKs, window-limited
     sends, receive timeouts, admission refusal, server FINs — echoes intact, idle flows
-    timed out, nothing left open (sequential twin alone, no GPU)."""
-    p = _peer("twin")
+    timed out, nothing left open (sequential twin alone, no GPU); 6 populations and loss
+    patterns, 4 RX modes each."""
+    p = _peer("twin", 6)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout
 
 
 @pytest.mark.gpu
 def test_gpu_server_reactive_peers_match_twin():
-    p = _peer("gpu")
+    """The same on the GPU backend, 4 populations x 4 RX modes (every poll, latency budget,
+    chunks, pipelined): handler log and every TX frame equal to the twin's in each run."""
+    p = _peer("gpu", 4)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert "gpu: handler log identical, TX frames identical" in p.stdout, p.stdout
+    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 16, p.stdout
 
 
 CLISRV = os.path.join(ROOT, "tests", "cpp", "test_tcp_client_server")
 
 
-def _clisrv(mode):
+def _clisrv(mode, runs=1):
     if not os.path.exists(CLISRV):
         if not os.path.isdir("/root/reference"):
             pytest.skip("tests/cpp/test_tcp_client_server not built (its handler texts come from /root/reference)")
         subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tcp_client_server"], check=True, capture_output=True)
-    return subprocess.run([CLISRV, mode], capture_output=True, text=True, timeout=300)
+    return subprocess.run([CLISRV, mode, str(runs)], capture_output=True, text=True, timeout=300)
 
 
 def test_client_server_twin_reference_examples():
     """GpuTcpClient <-> GpuTcpServer over a lossy in-memory wire, running the reference's
     example client and server handlers (tcpclient.cc:68-95, tcpserver.cc:61-90) unchanged:
-    connect, 1-s send timeouts echoed in order, close, reconnect (sequential backends)."""
-    p = _clisrv("twin")
+    connect, 1-s send timeouts echoed in order, close, reconnect (sequential backends);
+    8 loss patterns."""
+    p = _clisrv("twin", 8)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout
 
 
 @pytest.mark.gpu
 def test_gpu_client_server_match_twin():
-    p = _clisrv("gpu")
+    """Both ends on the GPU backend, 4 loss patterns: logs and wire frames equal the twin's."""
+    p = _clisrv("gpu", 4)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert "gpu: handler logs identical, wire frames identical" in p.stdout, p.stdout
+    assert p.stdout.count("gpu: handler logs identical, wire frames identical") == 4, p.stdout
