@@ -276,10 +276,8 @@ class GpuBackend {
   GpuBackend(const GpuBackend&) = delete;
   GpuBackend& operator=(const GpuBackend&) = delete;
   ~GpuBackend() {
-    if (tx_stream_) {
-      (void)hipStreamSynchronize(tx_stream_);
-      (void)hipStreamDestroy(tx_stream_);
-    }
+    drain(); // a pipelined batch may still be reading the ring
+    if (tx_stream_) (void)hipStreamDestroy(tx_stream_);
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
   }
@@ -288,6 +286,7 @@ class GpuBackend {
   // GPU while the host dispatches the current one; 0 = one launch per poll).  rx_halves = 2:
   // two RX rings of rx_cap slots for launch/collect (one in flight while the other fills).
   const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1) {
+    drain();
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
     rx_ring_ = tx_ring_ = nullptr;
@@ -334,6 +333,12 @@ class GpuBackend {
   }
 
  private:
+  // Wait for every launch that may read the rings (before they are freed).
+  void drain() {
+    if (rx_.stream()) (void)hipStreamSynchronize(rx_.stream());
+    if (tx_stream_) (void)hipStreamSynchronize(tx_stream_);
+  }
+
   GpuRx rx_;
   hipStream_t tx_stream_ = nullptr;
   uint8_t* rx_ring_ = nullptr;
