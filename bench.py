@@ -28,6 +28,7 @@ import argparse
 import hashlib
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -417,6 +418,44 @@ def secondary_rx(torch, pa, cfg, n, steps, stream, packed=False):
     return out
 
 
+def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
+    """pn_match_streams (TcpStream::filterPacket on the GPU, SURVEY §8(f) rank 3, DESIGN §11) over the
+    resident C2 batches, rotating (their header lines exceed the memory-side cache): 8 wildcard filters,
+    the frames' flow matching only the last; HIP events on the launch stream.  Algorithmic bytes per
+    frame: the 64-B header window read + the 4-B stream id written.  The first 65,536 ids are checked
+    against the numpy restatement of filterPacket (tests/streams_np.py)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from streams_np import match_streams_np
+
+    flt = np.zeros(8, pa.STREAM_FILTER_DTYPE)
+    for k in range(7):  # flows that are not in the batch
+        flt[k] = (int.from_bytes(bytes([10, 9, k, 1]), "little"), 0, int.from_bytes((5000 + k).to_bytes(2, "big"), "little"), 0, 0)
+    flt[7] = (0, 0, 0, int.from_bytes((1234).to_bytes(2, "big"), "little"), 0)  # dst port 1234: every frame
+    ids = torch.empty(n, dtype=torch.int32, device="cuda")
+    ctx.match_streams(frames_b[0], STRIDE, FRAME_OFF, n, flt, ids, stream)
+    torch.cuda.synchronize()
+    k = min(n, 65536)
+    ok = bool(np.array_equal(ids[:k].cpu().numpy().view(np.uint32), match_streams_np(slots[:k], FRAME_OFF, flt)))
+    R = len(frames_b)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for _ in range(5):
+        ev[0].record(stream)
+        for r in range(20):
+            ctx.match_streams(frames_b[r % R], STRIDE, FRAME_OFF, n, flt, ids, stream)
+        ev[1].record(stream)
+        torch.cuda.synchronize()
+        ts.append(ev[0].elapsed_time(ev[1]) / 20)
+    ms = statistics.median(ts)
+    return {"kernel": "match_streams_kernel", "frames": n, "resident_batches": R, "filters": 8, "kernel_ms": round(ms, 5),
+            "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
+            "algorithmic_bytes_per_launch": n * (64 + 4),
+            "achieved_gbs": round(n * (64 + 4) / (ms * 1e-3) / 1e9, 1),
+            "line_gbs": round(n * (128 + 4) / (ms * 1e-3) / 1e9, 1),
+            "first_65536_ids_vs_numpy": ok,
+            "note": "one 128-B line per 2-KiB slot is a strided gather; DESIGN §11 compares it with the same-pattern ceiling"}
+
+
 def server_poll():
     """The drop-in server itself (bench/bench_tcp_server quick, DESIGN §14): GpuTcpServer::poll over
     256 connections receiving in-order 1514-B segments from a pinned host ring (handshake, RX, the
@@ -657,6 +696,10 @@ def run_rank(rank, world, local_rank, args):
     if rank == 0 and world == 1 and not args.no_secondary and cfg == 2 and n == 1 << 20:
         t_sec = time.perf_counter()
         sec = {}
+        try:  # on the rotating C2 batches, before they are released
+            sec["match_streams"] = secondary_streams(torch, pa, ctx, frames_b, slots, n, stream)
+        except Exception as ex:  # measured extra; never blocks the bench line
+            sec["match_streams"] = {"error": repr(ex)}
         del frames_b[1:]  # the C2 batches rotated above are done; make room for the others
         torch.cuda.empty_cache()
         try:
