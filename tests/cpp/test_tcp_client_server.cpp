@@ -109,10 +109,18 @@ struct Packet {
 };
 static uint64_t getns() { return (uint64_t)g_now; }
 
-#define PN_DEFINE_ENDS(NS, BACKEND)                                                 \
+// the same ends in the pipelined RX mode (each poll's frames dispatched in the next poll)
+struct ServerConfPipe : ServerConf {
+  static const bool RxPipeline = true;
+};
+struct ClientConfPipe : ClientConf {
+  static const bool RxPipeline = true;
+};
+
+#define PN_DEFINE_ENDS(NS, BACKEND, SCONF, CCONF)                                   \
   namespace NS {                                                                    \
-  using TcpServer = GpuTcpServer<ServerConf, WireLink<true>, BACKEND>;              \
-  using TcpClient = GpuTcpClient<ClientConf, WireLink<false>, BACKEND>;             \
+  using TcpServer = GpuTcpServer<SCONF, WireLink<true>, BACKEND>;                   \
+  using TcpClient = GpuTcpClient<CCONF, WireLink<false>, BACKEND>;                  \
   TcpServer& server = *new TcpServer;                                               \
   TcpClient& client = *new TcpClient;                                               \
   Packet pack;                                                                      \
@@ -136,13 +144,25 @@ static uint64_t getns() { return (uint64_t)g_now; }
   }                                                                                 \
   }
 
-PN_DEFINE_ENDS(on_twin, OracleBackend)
+PN_DEFINE_ENDS(on_twin, OracleBackend, ServerConf, ClientConf)
 #include "../../oracle/_ref/tcpserver_handler.inc"
 PN_END_SERVER
 #include "../../oracle/_ref/tcpclient_handler.inc"
 PN_END_CLIENT
 
-PN_DEFINE_ENDS(on_gpu, GpuBackend)
+PN_DEFINE_ENDS(on_gpu, GpuBackend, ServerConf, ClientConf)
+#include "../../oracle/_ref/tcpserver_handler.inc"
+PN_END_SERVER
+#include "../../oracle/_ref/tcpclient_handler.inc"
+PN_END_CLIENT
+
+PN_DEFINE_ENDS(on_twin_pipe, OracleBackend, ServerConfPipe, ClientConfPipe)
+#include "../../oracle/_ref/tcpserver_handler.inc"
+PN_END_SERVER
+#include "../../oracle/_ref/tcpclient_handler.inc"
+PN_END_CLIENT
+
+PN_DEFINE_ENDS(on_gpu_pipe, GpuBackend, ServerConfPipe, ClientConfPipe)
 #include "../../oracle/_ref/tcpserver_handler.inc"
 PN_END_SERVER
 #include "../../oracle/_ref/tcpclient_handler.inc"
@@ -229,32 +249,44 @@ int main(int argc, char** argv) {
   const uint32_t runs = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1; // loss patterns (run k: seed k)
   const bool show = argc > 3;
   int fail = 0;
-  for (uint32_t seed = 0; seed < runs; seed++) {
-    if (runs > 1) std::printf("== loss pattern %u ==\n", seed);
-    on_twin::pack = Packet{}; // the example client's running counter starts over
-    on_gpu::pack = Packet{};
+  // one mode: the twin run, then (gpu) the GPU run, which must equal it frame for frame
+  auto mode = [&](const char* name, auto& ts, auto& tc, void (*tps)(), void (*tpc)(), LogStream& tsl, LogStream& tcl,
+                  Packet& tpack, auto& gs, auto& gc, void (*gps)(), void (*gpc)(), LogStream& gsl, LogStream& gcl,
+                  Packet& gpack, uint32_t seed) -> int {
+    int f = 0;
+    tpack = Packet{}; // the example client's running counter starts over
+    gpack = Packet{};
     Result tw;
-    if (!run(on_twin::server, on_twin::client, on_twin::srv::pollOnce, on_twin::cli::pollOnce, on_twin::srv::cout,
-             on_twin::cli::cout, tw, seed))
-      return 3;
-    fail += check("twin", tw);
+    if (!run(ts, tc, tps, tpc, tsl, tcl, tw, seed)) return 100;
+    f += check((std::string("twin") + name).c_str(), tw);
     if (show) std::printf("server log:\n%s\nclient log:\n%s\n", tw.srv_log.c_str(), tw.cli_log.c_str());
     if (gpu) {
       Result g;
-      if (!run(on_gpu::server, on_gpu::client, on_gpu::srv::pollOnce, on_gpu::cli::pollOnce, on_gpu::srv::cout,
-               on_gpu::cli::cout, g, seed))
-        return 5;
-      fail += check("gpu", g);
+      if (!run(gs, gc, gps, gpc, gsl, gcl, g, seed)) return 100;
+      f += check((std::string("gpu") + name).c_str(), g);
       const bool logs = g.srv_log == tw.srv_log && g.cli_log == tw.cli_log;
       const bool wire = g.wire == tw.wire;
-      std::printf("gpu: handler logs %s, wire frames %s (%zu)\n", logs ? "identical" : "DIFFERENT",
+      std::printf("gpu%s: handler logs %s, wire frames %s (%zu)\n", name, logs ? "identical" : "DIFFERENT",
                   wire ? "identical" : "DIFFERENT", g.wire.size());
-      fail += !logs + !wire;
+      f += !logs + !wire;
     }
+    return f;
+  };
+  for (uint32_t seed = 0; seed < runs; seed++) {
+    if (runs > 1) std::printf("== loss pattern %u ==\n", seed);
+    fail += mode("", on_twin::server, on_twin::client, on_twin::srv::pollOnce, on_twin::cli::pollOnce,
+                 on_twin::srv::cout, on_twin::cli::cout, on_twin::pack, on_gpu::server, on_gpu::client,
+                 on_gpu::srv::pollOnce, on_gpu::cli::pollOnce, on_gpu::srv::cout, on_gpu::cli::cout, on_gpu::pack, seed);
+    fail += mode(" (pipelined)", on_twin_pipe::server, on_twin_pipe::client, on_twin_pipe::srv::pollOnce,
+                 on_twin_pipe::cli::pollOnce, on_twin_pipe::srv::cout, on_twin_pipe::cli::cout, on_twin_pipe::pack,
+                 on_gpu_pipe::server, on_gpu_pipe::client, on_gpu_pipe::srv::pollOnce, on_gpu_pipe::cli::pollOnce,
+                 on_gpu_pipe::srv::cout, on_gpu_pipe::cli::cout, on_gpu_pipe::pack, seed);
   }
   if (gpu) {
     delete &on_gpu::client;
     delete &on_gpu::server;
+    delete &on_gpu_pipe::client;
+    delete &on_gpu_pipe::server;
   }
   std::printf("%s\n", fail ? "FAIL" : "PASS");
   return fail ? 1 : 0;

@@ -91,7 +91,9 @@ def test_client_server_twin_reference_examples():
 
 @pytest.mark.gpu
 def test_gpu_client_server_match_twin():
-    """Both ends on the GPU backend, 4 loss patterns: logs and wire frames equal the twin's."""
+    """Both ends on the GPU backend, 4 loss patterns, classify-every-poll and pipelined RX: logs
+    and wire frames equal the twin's."""
     p = _clisrv("gpu", 4)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("gpu: handler logs identical, wire frames identical") == 4, p.stdout
+    assert p.stdout.count("gpu (pipelined): handler logs identical, wire frames identical") == 4, p.stdout
