@@ -39,6 +39,9 @@ enum : int { kExactRange = 64 };
 // kCoopProbe: conn-table lookups that continue past the home slot are finished by the whole
 // wave, 64 entries per round trip (header_phase in rx_kernel.hip).
 enum : int { kCoopProbe = 256 };
+// Timing only (tuning library, packed indexed captures): phase 2 streams the wave's frames as ONE
+// contiguous byte range with fully used 1-KiB loads, summed into one garbage total (records wrong).
+enum : int { kAblContigStream = 512 };
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe;
 

@@ -358,7 +358,35 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
   }
   if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, stream_start((uint64_t)win), a);
-  stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
+  if constexpr (IDX && (ABL & kAblContigStream)) {
+    // timing only: [first frame's stream start, last frame's extent end) as one range, 16 x 1 KiB per round
+    const uint64_t w = (uint64_t)win;
+    const uint64_t lo64 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(w >> 32), 0) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)w, 0);
+    const uint32_t last = n_here - 1;
+    const uint64_t hw = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(w >> 32), last) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((uint32_t)w, last);
+    const uint64_t lo = (lo64 + stream_start(lo64)) & ~15ull;
+    const uint64_t hi = (hw + (uint32_t)(__builtin_amdgcn_readlane(st.end_rel, last) & ~1) + 15) & ~15ull;
+    const uint32_t len = hi > lo ? (uint32_t)(hi - lo) : 0u;
+    const __amdgpu_buffer_rsrc_t rc = frame_rsrc((const uint8_t*)lo, len);
+    uint32_t sum = 0;
+    for (uint32_t o = 0; o < len; o += 16 * 1024) {
+      u32x4 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b128(rc, o + j * 1024 + lane * 16, 0, LAUX);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        sum = dot2(v[j].x, 0x10001u, sum);
+        sum = dot2(v[j].y, 0x10001u, sum);
+        sum = dot2(v[j].z, 0x10001u, sum);
+        sum = dot2(v[j].w, 0x10001u, sum);
+      }
+    }
+    st.t_all += sum;
+  } else {
+    stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
+  }
   if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
 }
 

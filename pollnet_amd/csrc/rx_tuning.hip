@@ -157,7 +157,7 @@ extern "C" {
 // A/B-timed by scripts/bench_indexed.py; not part of the public header.
 int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
                                 uint32_t avail, void* results_dev, void* stream, int variant) {
-  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 3)
+  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 4)
     return set_err(ctx, PN_EINVAL, "indexed variant: bad args");
   KArgs a;
   a.frames = (const uint8_t*)base;
@@ -175,6 +175,8 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, kXcdOrder>(a, s); // window non-temporal
   else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0, 1, 0>(a, s);  // production window, blockIdx order
   else if (variant == 3) launch_one<0, 1, kProdAbl, 0, kStoreAux, 1, 0, 1, 0>(a, s);         // + stream at default policy
+  else if (variant == 4) // timing only (packed captures): the wave's frames streamed as one contiguous range
+    launch_one<0, 1, kProdAbl | kAblContigStream, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
   else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
