@@ -217,8 +217,10 @@ int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint
  * frame's own tot_len is used.  A frame whose tot_len is below the bare headers
  * (40 / 28) or runs past its slot (14 + tot_len > slot_stride - frame_off) is left
  * untouched.  Only the length and checksum fields are written.
- * Layout as pn_classify (frames in device memory, 16-byte aligned; SendBuf slots:
- * frame_off = 14, slot_stride = SendBufSize, Core.h:147-156, 232).  Asynchronous. */
+ * Layout as pn_classify (frames in device memory or pinned host memory read and patched in
+ * place, 16-byte aligned; SendBuf slots: frame_off = 14, slot_stride = SendBufSize,
+ * Core.h:147-156, 232).  Asynchronous.  Up to 65,536 frames one launch; above, two (the
+ * fields through ctx scratch). */
 #define PN_TX_TCP 0u
 #define PN_TX_UDP_EFVI 1u
 #define PN_TX_UDP 2u
