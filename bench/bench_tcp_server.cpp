@@ -192,10 +192,11 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
   BenchLink& link = srv->link();
   link.phase = BenchLink::Syn;
   srv->poll(h);
-  srv->poll(h); // (pipelined: the SYNs are dispatched one poll later)
+  // (pipelined: frames are dispatched one poll later and the replies sent one poll after that)
+  for (int k = 0; k < 8 && link.synacks < n_flows; k++) srv->poll(h);
   link.phase = BenchLink::Ack;
   srv->poll(h);
-  srv->poll(h);
+  for (int k = 0; k < 8 && h.connected < n_flows; k++) srv->poll(h);
   if (h.connected != n_flows || link.rsts) {
     out.err = "handshake: " + std::to_string(h.connected) + " connected, " + std::to_string(link.rsts) + " RSTs";
     return out;
@@ -211,6 +212,7 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
   const uint64_t timed_bytes = h.bytes - bytes0;
   link.phase = BenchLink::Idle;
   srv->poll(h); // pipelined: the last batch is still in flight
+  srv->poll(h);
   const uint64_t frames = (uint64_t)polls * (kBatch / n_flows) * n_flows;
   out.mfps = frames / t / 1e6;
   out.us_poll = t * 1e6 / polls;

@@ -285,7 +285,9 @@ class GpuBackend {
   // rx_chunk: frames per classify launch (a poll's frames go in chunks, the next one on the
   // GPU while the host dispatches the current one; 0 = one launch per poll).  rx_halves = 2:
   // two RX rings of rx_cap slots for launch/collect (one in flight while the other fills).
-  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1) {
+  // tx_halves = 2: two TX batches (one filled on the GPU while the other is built).
+  const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1,
+                   uint32_t tx_halves = 1) {
     drain();
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
@@ -296,13 +298,15 @@ class GpuBackend {
     if (!tx_stream_ && hipStreamCreateWithFlags(&tx_stream_, hipStreamNonBlocking) != hipSuccess)
       return "hipStreamCreate(tx) failed";
     rx_cap_ = rx_cap;
+    tx_cap_ = tx_cap;
     const size_t rx_bytes = (size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1);
+    const size_t tx_bytes = (size_t)kStride * tx_cap * (tx_halves == 2 ? 2 : 1);
     if (hipHostMalloc((void**)&rx_ring_, rx_bytes, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(rx ring) failed";
-    if (hipHostMalloc((void**)&tx_ring_, (size_t)kStride * tx_cap, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc((void**)&tx_ring_, tx_bytes, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(tx batch) failed";
     std::memset(rx_ring_, 0, rx_bytes);
-    std::memset(tx_ring_, 0, (size_t)kStride * tx_cap);
+    std::memset(tx_ring_, 0, tx_bytes);
     return nullptr;
   }
   uint8_t* rxSlots(uint32_t half = 0) { return rx_ring_ + (size_t)half * rx_cap_ * kStride; }
@@ -315,7 +319,7 @@ class GpuBackend {
         rxSlots(half), n, half, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
         [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
   }
-  uint8_t* txSlots() { return tx_ring_; }
+  uint8_t* txSlots(uint32_t half = 0) { return tx_ring_ + (size_t)half * tx_cap_ * kStride; }
   const char* syncTable(const ConnTable& t) { return rx_.syncTable(t); }
   // f(key, rec, eth) for the n frames of the RX ring, in ring order.
   template <class F>
@@ -324,10 +328,19 @@ class GpuBackend {
         rx_ring_, n, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
         [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
   }
-  // IP + TCP checksums of the first n TX slots (PN_TX_TCP: SendBuf::setOptDataLen, Core.h:157-163).
-  const char* fillTx(uint32_t n) {
-    if (pn_tx_fill(rx_.ctx(), tx_ring_, kStride, kFrameOff, n, nullptr, PN_TX_TCP, tx_stream_))
+  // IP + TCP checksums of the first n slots of a TX batch (PN_TX_TCP: SendBuf::setOptDataLen,
+  // Core.h:157-163).  fillTx waits for them; fillTxLaunch / fillTxWait split the same call
+  // (pipelined: the fill runs while the host dispatches the next batch).
+  const char* fillTx(uint32_t n, uint32_t half = 0) {
+    if (const char* e = fillTxLaunch(n, half)) return e;
+    return fillTxWait();
+  }
+  const char* fillTxLaunch(uint32_t n, uint32_t half) {
+    if (pn_tx_fill(rx_.ctx(), txSlots(half), kStride, kFrameOff, n, nullptr, PN_TX_TCP, tx_stream_))
       return pn_last_error(rx_.ctx());
+    return nullptr;
+  }
+  const char* fillTxWait() {
     if (hipStreamSynchronize(tx_stream_) != hipSuccess) return "hipStreamSynchronize(tx_fill) failed";
     return nullptr;
   }
@@ -343,7 +356,7 @@ class GpuBackend {
   hipStream_t tx_stream_ = nullptr;
   uint8_t* rx_ring_ = nullptr;
   uint8_t* tx_ring_ = nullptr;
-  uint32_t rx_cap_ = 0;
+  uint32_t rx_cap_ = 0, tx_cap_ = 0;
 };
 
 
@@ -475,20 +488,20 @@ class TcpEngine {
   void setDropBadChecksum(bool drop) { drop_bad_ = drop; }
   const ConnTable& table() const { return table_; }
   uint32_t nowTs() const { return wheel_.now(); }
-  // Frames built since the last flush (checksums not yet filled).
-  uint32_t pendingTx() const { return tx_n_; }
-  // Fill the pending frames' checksums (one pn_tx_fill launch) and send them in order.
+  // Frames built since the last flush (checksums not yet filled), plus (pipelined) those whose
+  // fill is still running.
+  uint32_t pendingTx() const { return tx_n_ + tx_fl_n_; }
+  // Fill the pending frames' checksums (one pn_tx_fill launch) and send them in order; a
+  // pipelined batch still being filled goes first.
   const char* flushTx() {
-    if (!tx_n_) return nullptr;
-    const char* e = be_.fillTx(tx_n_);
-    if (e) {
-      err_ = e;
-    } else {
-      for (uint32_t i = 0; i < tx_n_; i++) {
-        const uint8_t* f = be_.txSlots() + (size_t)i * Backend::kStride + Backend::kFrameOff;
-        link_.send(f, 14 + srv_detail::rd16(f + 16));
-      }
+    const char* e = completeTx();
+    if (!tx_n_) return e;
+    if (const char* e2 = be_.fillTx(tx_n_, tx_cur_)) {
+      err_ = e2;
+      tx_n_ = 0;
+      return e2;
     }
+    sendTx(tx_cur_, tx_n_);
     tx_n_ = 0;
     return e;
   }
@@ -550,7 +563,8 @@ class TcpEngine {
     }
     std::memcpy(local_mac_, link_.localMac(), 6);
     if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
-    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1))
+    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1,
+                                 kRxPipeline ? 2 : 1))
       return e;
     free_conns_.clear();
     for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i
@@ -577,7 +591,7 @@ class TcpEngine {
       c.fin_sent_ = c.fin_received_ = true;
     }
     for (uint32_t i = 0; i < kMaxTw; i++) tws_[i].timer.owner = kMaxConn + i;
-    tx_n_ = rx_pending_ = cur_ = 0;
+    tx_n_ = rx_pending_ = cur_ = tx_cur_ = tx_fl_n_ = 0;
     fl_n_[0] = fl_n_[1] = 0;
     ++tver_;
     ready_ = true;
@@ -589,6 +603,35 @@ class TcpEngine {
     for (auto& c : conns_)
       if (c.eng_ && !c.isClosed()) closeConn(c);
     flushTx();
+  }
+
+  // The link gets frames [0, n) of a TX batch, in order.
+  void sendTx(uint32_t half, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) {
+      const uint8_t* f = be_.txSlots(half) + (size_t)i * Backend::kStride + Backend::kFrameOff;
+      link_.send(f, 14 + srv_detail::rd16(f + 16));
+    }
+  }
+  // Pipelined TX: start filling the frames built so far and switch to the other batch ...
+  void launchTx() {
+    if (!tx_n_) return;
+    if (const char* e = be_.fillTxLaunch(tx_n_, tx_cur_)) {
+      err_ = e;
+      tx_n_ = 0;
+      return;
+    }
+    tx_fl_n_ = tx_n_;
+    tx_n_ = 0;
+    tx_cur_ ^= 1;
+  }
+  // ... and, a poll later, wait for that fill and send its frames.
+  const char* completeTx() {
+    if (!tx_fl_n_) return nullptr;
+    const uint32_t n = tx_fl_n_;
+    tx_fl_n_ = 0;
+    if (const char* e = be_.fillTxWait()) return err_ = e;
+    sendTx(tx_cur_ ^ 1, n);
+    return nullptr;
   }
 
   // One poll: a timer tick, the RX batch (classified on the GPU, dispatched in ring order),
@@ -613,12 +656,15 @@ class TcpEngine {
     }
     auto frame = [&](uint64_t key, const pn_result& r, const uint8_t* eth) { onFrame(h, key, r, eth); };
     if constexpr (kRxPipeline) {
-      // launch this poll's frames, then dispatch the previous poll's while they are classified
+      // launch this poll's frames; send what the previous poll built (its checksum fill ran
+      // meanwhile); dispatch the previous poll's frames while this poll's are classified; start
+      // the fill of what this poll built
       if (n) {
         if ((err_ = be_.launch(cur_, n, table_))) return;
         fl_n_[cur_] = n;
         fl_ver_[cur_] = tver_;
       }
+      completeTx();
       const uint32_t prev = cur_ ^ 1;
       if (const uint32_t m = fl_n_[prev]) {
         fl_n_[prev] = 0;
@@ -626,11 +672,14 @@ class TcpEngine {
         if (const char* e = be_.collect(prev, m, table_, frame)) err_ = e;
       }
       if (n) cur_ ^= 1;
-    } else if (n) {
-      disp_ver_ = tver_;
-      if (const char* e = be_.classify(n, table_, frame)) err_ = e;
+      launchTx();
+    } else {
+      if (n) {
+        disp_ver_ = tver_;
+        if (const char* e = be_.classify(n, table_, frame)) err_ = e;
+      }
+      flushTx();
     }
-    flushTx();
   }
 
   // ---- one received frame (Core::pollNet RX branch + the endpoint's recv handler) ----
@@ -1014,7 +1063,7 @@ class TcpEngine {
   enum Kind { kSyn, kSynAck, kData, kFinAck, kAck, kRstAck };
   uint8_t* txFrame() {
     if (tx_n_ == kTxBatch) flushTx();
-    return be_.txSlots() + (size_t)tx_n_++ * Backend::kStride + Backend::kFrameOff;
+    return be_.txSlots(tx_cur_) + (size_t)tx_n_++ * Backend::kStride + Backend::kFrameOff;
   }
   void header(uint8_t* f, const uint8_t* dst_mac, uint32_t dst_ip, uint16_t src_port, uint16_t dst_port, uint32_t seq,
               uint32_t ack, uint8_t doff_words, uint8_t flags, uint16_t window, uint32_t tcp_len) {
@@ -1116,6 +1165,7 @@ class TcpEngine {
   // that of the records being dispatched; fl_* the pipelined batch in flight per ring half
   uint64_t tver_ = 1, synced_ver_ = 0, disp_ver_ = 0, fl_ver_[2] = {0, 0};
   uint32_t cur_ = 0, fl_n_[2] = {0, 0};
+  uint32_t tx_cur_ = 0, tx_fl_n_ = 0; // TX batch being built; frames of the other one in its fill (pipelined)
   uint64_t re_resolved_ = 0;
   bool ready_ = false, drop_bad_ = true;
   const char* err_ = "Closed";

@@ -45,16 +45,18 @@ struct OracleBackend {
   std::vector<uint8_t> rx, tx;
   std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
   uint32_t cap = 0;
-  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0, uint32_t rx_halves = 1) {
+  uint32_t tcap = 0;
+  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0, uint32_t rx_halves = 1, uint32_t tx_halves = 1) {
     cap = rx_cap;
+    tcap = tx_cap;
     rx.assign((size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1), 0);
-    tx.assign((size_t)kStride * tx_cap, 0);
+    tx.assign((size_t)kStride * tx_cap * (tx_halves == 2 ? 2 : 1), 0);
     recs[0].assign(rx_cap, pn_result{});
     recs[1].assign(rx_cap, pn_result{});
     return nullptr;
   }
   uint8_t* rxSlots(uint32_t half = 0) { return rx.data() + (size_t)half * cap * kStride; }
-  uint8_t* txSlots() { return tx.data(); }
+  uint8_t* txSlots(uint32_t half = 0) { return tx.data() + (size_t)half * tcap * kStride; }
   const char* syncTable(const pollnet_amd::ConnTable&) { return nullptr; }
   static uint64_t keyOf(const uint8_t* eth) {
     uint32_t ip_be;
@@ -93,10 +95,13 @@ struct OracleBackend {
     }
     return nullptr;
   }
-  const char* fillTx(uint32_t n) {
-    orc_tx_fill_batch(tx.data(), kStride, kFrameOff, n, nullptr, PN_TX_TCP, 1);
+  const char* fillTx(uint32_t n, uint32_t half = 0) {
+    orc_tx_fill_batch(txSlots(half), kStride, kFrameOff, n, nullptr, PN_TX_TCP, 1);
     return nullptr;
   }
+  // pipelined: filled at launch; the engine sends the batch a poll later, as with the GPU
+  const char* fillTxLaunch(uint32_t n, uint32_t half) { return fillTx(n, half); }
+  const char* fillTxWait() { return nullptr; }
 };
 
 struct LogStream { // stands in for std::cout in the example's handler
