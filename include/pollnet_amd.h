@@ -136,8 +136,9 @@ int pn_device_count(int* n);
 
 /* Snapshot the conn table into device memory (synchronous H2D, ≤160 KiB for
  * 1024+1024 conns).  `entries` is host memory laid out as pn_conn_entry[n].
- * Waits for the last pn_classify issued on this ctx first, so a launch in flight
- * always sees the snapshot it was issued against. */
+ * Waits first for the device's work in flight (hipDeviceSynchronize; classify
+ * launches may be on any stream), so a launch in flight always sees the snapshot it
+ * was issued against.  A control-plane call: the launch path records nothing. */
 int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entries, uint64_t tbl_mask,
                       uint32_t max_conn_cnt);
 

@@ -7,8 +7,6 @@
 
 #include <cstdint>
 #include <string>
-#include <utility>
-#include <vector>
 
 #include "../../include/pollnet_amd.h"
 
@@ -19,10 +17,6 @@ struct pn_ctx {
   uint64_t mask = 0;
   uint32_t max_conn = 0;
   hipStream_t last_stream = nullptr;
-  // Streams with classify launches that read tbl_dev, each with an event recorded after
-  // its latest such launch: pn_set_conn_table waits for all of them before replacing
-  // the table (a launch on any stream may still be reading it).
-  std::vector<std::pair<hipStream_t, hipEvent_t>> table_readers;
   void* tx_patch = nullptr;       // pn_tx_fill's per-frame patch records (8 B each)
   uint32_t tx_patch_n = 0;
   hipStream_t tx_stream = nullptr; // stream of the last pn_tx_fill (the scratch is reused)
@@ -43,27 +37,13 @@ inline int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
   return set_err(ctx, PN_EHIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// After a launch that reads the device conn table on stream s.
-inline int note_table_reader(pn_ctx* ctx, hipStream_t s) {
-  hipEvent_t ev = nullptr;
-  for (auto& r : ctx->table_readers)
-    if (r.first == s) ev = r.second;
-  if (!ev) {
-    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-    if (e != hipSuccess) return hip_err(ctx, e, "hipEventCreate(table reader)");
-    ctx->table_readers.emplace_back(s, ev);
-  }
-  hipError_t e = hipEventRecord(ev, s);
-  if (e != hipSuccess) return hip_err(ctx, e, "hipEventRecord(table reader)");
-  return PN_OK;
-}
-
-// Before the device table is overwritten: every launch that may read it has finished.
+// Before the device table is overwritten or freed: every launch that may read it has finished.
+// Classify launches can be on any stream of the process (the caller's), so this waits for the
+// whole device: a control-plane call, kept off the launch path (a per-launch event record
+// costs ≈3-5 µs of idle GPU between back-to-back launches).
 inline int wait_table_readers(pn_ctx* ctx) {
-  for (auto& r : ctx->table_readers) {
-    hipError_t e = hipEventSynchronize(r.second);
-    if (e != hipSuccess) return hip_err(ctx, e, "hipEventSynchronize(table reader)");
-  }
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize(table readers)");
   return PN_OK;
 }
 

@@ -37,11 +37,9 @@ int pn_open(int device, pn_ctx** out) {
 
 void pn_close(pn_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->tbl_dev || ctx->tx_patch || !ctx->table_readers.empty()) {
+  if (ctx->tbl_dev || ctx->tx_patch) {
     (void)hipSetDevice(ctx->device);
-    (void)pn_internal::wait_table_readers(ctx);
-    for (auto& r : ctx->table_readers) (void)hipEventDestroy(r.second);
-    if (ctx->tx_patch) (void)hipStreamSynchronize(ctx->tx_stream);
+    (void)pn_internal::wait_table_readers(ctx); // also covers the last tx_fill's patch scratch
     if (ctx->tbl_dev) (void)hipFree(ctx->tbl_dev);
     if (ctx->tx_patch) (void)hipFree(ctx->tx_patch);
   }
@@ -58,7 +56,8 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   // classify launches on this ctx (any stream) may still be reading the table: let them
-  // finish before the snapshot is replaced (the copy below is not ordered against them)
+  // finish before the snapshot is replaced (the copy below is not ordered against them).
+  // Waiting here, not recording an event per launch, keeps the launch path free
   if (ctx->tbl_dev) {
     const int rc = pn_internal::wait_table_readers(ctx);
     if (rc) return rc;
@@ -118,7 +117,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify launch");
   ctx->last_stream = s;
-  return pn_internal::note_table_reader(ctx, s);
+  return PN_OK;
 }
 
 
@@ -161,7 +160,7 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
   ctx->last_stream = s;
-  return pn_internal::note_table_reader(ctx, s);
+  return PN_OK;
 }
 
 int pn_sync(pn_ctx* ctx) {

@@ -322,6 +322,41 @@ def test_side_stream_and_sync(torch_cuda, ctx):
     assert_same(res.cpu().numpy().view(pa.RESULT_DTYPE), exp)
 
 
+def test_table_replaced_while_classify_in_flight(torch_cuda):
+    """pn_set_conn_table right after classify launches on two side streams (and a TX fill on
+    a third, which becomes the ctx's last stream): every launch still sees the snapshot it
+    was issued against -- the replacement waits for the device, the launches record nothing."""
+    torch = torch_cuda
+    c = pa.RxContext(0)
+    p = pa.rx.GenParams.for_config(3)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = 1 << 20
+    s = pa.gen_frames(p, n)
+    exp = orc.classify_batch(s[:8192], STRIDE, FRAME_OFF, 8192, e, m, t.max_conn_cnt, threads=8)
+    other = np.zeros(len(e), pa.ENTRY_DTYPE)
+    other["key"] = pa.PN_EMPTY_KEY  # an empty table: every record would become a miss
+    c.set_conn_entries(e, m, t.max_conn_cnt)
+    frames = torch.from_numpy(s.reshape(-1)).cuda()
+    tx = torch.from_numpy(pa.gen_frames(pa.rx.GenParams.for_config(2), 4096).reshape(-1)).cuda()
+    torch.cuda.synchronize()
+    sa, sb, stx = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    ra = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    rb = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    for _ in range(3):
+        c.classify(frames, STRIDE, FRAME_OFF, n, ra, sa)
+        c.classify(frames, STRIDE, FRAME_OFF, n, rb, sb)
+        c.tx_fill(tx, STRIDE, FRAME_OFF, 4096, stream=stx)
+        c.set_conn_entries(other, m, t.max_conn_cnt)  # no sync before it
+        torch.cuda.synchronize()
+        for r in (ra, rb):
+            got = r.cpu().numpy().view(pa.RESULT_DTYPE)
+            assert_same(got[:8192], exp)
+            assert np.count_nonzero(got["flags"] & pa.F.HIT) > n // 2
+        c.set_conn_entries(e, m, t.max_conn_cnt)
+    c.close()
+
+
 def test_cpp_adapter_without_torch():
     """include/pollnet_amd/gpu_rx.hpp driven from a plain C++ process (only /opt/rocm's
     HIP runtime loaded): records and the pollNet-style TW/recv dispatch vs the oracle."""
