@@ -55,8 +55,12 @@ enum : int { kLaneMaskLoads = 2048 };
 enum : int { kSkipBatchGate = 4096 };
 // Tuning (with kSkipEmptyLoads): one branch per frame choosing both loads, the first only, or none.
 enum : int { kSkipPairBranch = 8192 };
+// With kSkipEmptyLoads: the skipping form of phase 2 only in waves that have a frame ending inside
+// its first stream KiB (one ballot per wave); a wave of full-size frames (every C2 wave) streams
+// with unconditional loads, the form without the branches.
+enum : int { kSkipWaveGate = 16384 };
 // The production RX configuration.
-constexpr int kProdAbl = kExactRange | kCoopProbe | kSkipEmptyLoads;
+constexpr int kProdAbl = kExactRange | kCoopProbe | kSkipEmptyLoads | kSkipWaveGate;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the

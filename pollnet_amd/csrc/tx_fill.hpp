@@ -75,7 +75,11 @@ constexpr int kWbPatch = -2;
 // MODE: PN_TX_TCP, PN_TX_UDP_EFVI or PN_TX_UDP.
 // PADK (tuning): KiB of LDS padding per workgroup (caps workgroups per CU, as the RX
 // kernel's 2-KiB pad does: 10 KiB = 4 waves/SIMD).
-template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false>
+// SABL: the stream phase's options.  Every stream load is issued (kExactRange): TX batches are
+// mostly full-size frames, where skipping empty loads measured 1.8 % slower at frame_off 2 and
+// equal at 14 (tuning variant 42 = with kSkipEmptyLoads, profiles/r02/s3/tx_skip_ab_off*.json).
+template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false,
+          int SABL = kExactRange>
 __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   const int lane = threadIdx.x;
   const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * a.fpw;
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
     const int end_rel = ok ? (int)(even_end | (tot & 1)) : 0;
     uint32_t t_all = window_part<MIS>(h, end_rel & ~1, stream_start((uint64_t)(ip - MIS)));
     uint32_t pad = kPadUnknown;
-    stream_phase<kExactRange | kSkipEmptyLoads, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
+    stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
     if (ok && (tot & 1) && pad == kPadUnknown) pad = ip[tot]; // pad byte inside the window
     const uint32_t tcp_chk_old = h.template u16<MIS + 36>(); // TcpHeader.checksum at tcp+16 (Core.h:84)
     const uint32_t s_seg = t_all - s_ip_stored - tcp_chk_old - ((tot & 1) ? (pad << 8) : 0u);

@@ -71,6 +71,14 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
       case 19: hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, 128, 16, 0>), grid, block, 0, s, a); return 0;
       // the product's launch shape (frames_per_wave(n) per wave, XCD order): 40 = pn_tx_fill's
       // two phases, 41 = one launch writing the fields in place (small batches: one launch fewer)
+      case 42: { // pn_tx_fill's two phases with empty stream loads skipped (kSkipEmptyLoads, measured, not adopted)
+        TArgs b = a;
+        b.fpw = frames_per_wave(n);
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kExactRange | kSkipEmptyLoads>), dim3((n + b.fpw - 1) / b.fpw), block,
+                           0, s, b);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
+        return 0;
+      }
       case 40: case 41: {
         TArgs b = a;
         b.fpw = frames_per_wave(n);
