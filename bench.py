@@ -336,10 +336,19 @@ def golden_digest(cfg):
         return None
 
 
-def time_launches(torch, fn, bufs, steps, stream, warmup=2):
-    """Average ms per launch of fn(buf) rotating over bufs, HIP events on `stream`."""
-    for k in range(warmup):
+def time_launches(torch, fn, bufs, steps, stream, warmup=2, settle_s=0.04):
+    """Average ms per launch of fn(buf) rotating over bufs, HIP events on `stream`.  Before
+    timing, back-to-back launches run for at least `settle_s` of wall time: after an idle
+    stretch (the host generating the next workload) a mixed-size workload such as C3 runs up
+    to 15 % slow for its first ~100 launches (~16 ms) while the device's power state settles
+    (scripts/warmup_probe.py, profiles/r02/s3/warmup_probe_c{2,3}.json; C2 shows no ramp)."""
+    t0 = time.perf_counter()
+    k = 0
+    while k < warmup or time.perf_counter() - t0 < settle_s:
         fn(bufs[k % len(bufs)])
+        k += 1
+        if k % 8 == 0:
+            torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for k in range(steps):
