@@ -47,14 +47,6 @@ enum : int { kAblContigStream = 512 };
 // extent.  Mixed-size frames (most end inside the first KiB) skip up to half their load
 // instructions; records are identical (the skipped loads' values were zero).
 enum : int { kSkipEmptyLoads = 1024 };
-// Tuning (with kSkipEmptyLoads): each stream load is also issued only on the lanes whose 16-B chunk
-// starts inside the extent (EXEC-masked), the rest read as zero -- records identical.
-enum : int { kLaneMaskLoads = 2048 };
-// Tuning (with kSkipEmptyLoads): the per-load branches only in batches that have an empty load;
-// a batch of 8 frames that all need both KiBs (every C2 batch) issues its 16 loads unconditionally.
-enum : int { kSkipBatchGate = 4096 };
-// Tuning (with kSkipEmptyLoads): one branch per frame choosing both loads, the first only, or none.
-enum : int { kSkipPairBranch = 8192 };
 // With kSkipEmptyLoads: the skipping form of phase 2 only in waves that have a frame ending inside
 // its first stream KiB (one ballot per wave); a wave of full-size frames (every C2 wave) streams
 // with unconditional loads, the form without the branches.
@@ -205,39 +197,6 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
     int ends[kBatch], s0s[kBatch];
     u32x4 w0s[kBatch], w1s[kBatch];
     // issue all 2*kBatch loads of the batch before consuming any of them
-    if constexpr ((ABL & kSkipBatchGate) && (ABL & kSkipEmptyLoads) && (ABL & kExactRange)) {
-      uint32_t e16s[kBatch];
-      const uint8_t* fws[kBatch];
-      bool full = true; // wave-uniform: every frame of the batch needs both KiBs
-#pragma unroll
-      for (int j = 0; j < kBatch; ++j) {
-        const uint32_t fi = b0 + j;
-        const int end = __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1;
-        ends[j] = end;
-        e16s[j] = (uint32_t)(end + 3) & ~3u;
-        fws[j] = frame_win(fi);
-        s0s[j] = (int)stream_start((uint64_t)fws[j]);
-        full = full && e16s[j] > (uint32_t)s0s[j] + 1024;
-      }
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      if (full) {
-#pragma unroll
-        for (int j = 0; j < kBatch; ++j) {
-          const __amdgpu_buffer_rsrc_t rs = frame_rsrc(fws[j], e16s[j]);
-          w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0s[j] + lane * 16, 0, LAUX);
-          w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0s[j] + 1024 + lane * 16, 0, LAUX);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < kBatch; ++j) {
-          const __amdgpu_buffer_rsrc_t rs = frame_rsrc(fws[j], e16s[j]);
-          w0s[j] = e16s[j] > (uint32_t)s0s[j] ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0s[j] + lane * 16, 0, LAUX) : z;
-          w1s[j] = e16s[j] > (uint32_t)s0s[j] + 1024
-                       ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0s[j] + 1024 + lane * 16, 0, LAUX)
-                       : z;
-        }
-      }
-    } else {
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
       const uint32_t fi = b0 + j; // wave-uniform
@@ -252,30 +211,12 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       // out-of-range chunks of a buffer load return 0 and fetch nothing
       if constexpr ((ABL & kSkipEmptyLoads) && (ABL & kExactRange)) {
         const u32x4 z = {0u, 0u, 0u, 0u};
-        if constexpr (ABL & kLaneMaskLoads) {
-          const uint32_t o0 = (uint32_t)s0 + lane * 16;
-          w0s[j] = z;
-          w1s[j] = z;
-          if (end16 > (uint32_t)s0 && o0 < end16) w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o0, 0, LAUX);
-          if (end16 > (uint32_t)s0 + 1024 && o0 + 1024 < end16)
-            w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, o0 + 1024, 0, LAUX);
-        } else if constexpr (ABL & kSkipPairBranch) {
-          if (end16 > (uint32_t)s0 + 1024) {
-            w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX);
-            w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX);
-          } else {
-            w0s[j] = end16 > (uint32_t)s0 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX) : z;
-            w1s[j] = z;
-          }
-        } else {
-          w0s[j] = end16 > (uint32_t)s0 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX) : z;
-          w1s[j] = end16 > (uint32_t)s0 + 1024 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX) : z;
-        }
+        w0s[j] = end16 > (uint32_t)s0 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX) : z;
+        w1s[j] = end16 > (uint32_t)s0 + 1024 ? __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX) : z;
       } else {
         w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX);
         w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX);
       }
-    }
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
     auto sel = [](int e, int o) -> uint32_t {

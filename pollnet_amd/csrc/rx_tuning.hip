@@ -157,7 +157,7 @@ extern "C" {
 // A/B-timed by scripts/bench_indexed.py; not part of the public header.
 int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,
                                 uint32_t avail, void* results_dev, void* stream, int variant) {
-  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 9)
+  if (!ctx || !ctx->tbl_dev || n == 0 || eth_mod16 != 2 || variant < 0 || variant > 5)
     return set_err(ctx, PN_EINVAL, "indexed variant: bad args");
   KArgs a;
   a.frames = (const uint8_t*)base;
@@ -179,14 +179,6 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
     launch_one<0, 1, kProdAbl | kAblContigStream, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
   else if (variant == 5) // production without kSkipEmptyLoads (every stream load issued)
     launch_one<0, 1, kProdAbl & ~kSkipEmptyLoads, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
-  else if (variant == 6) // production + lane-masked stream loads
-    launch_one<0, 1, kProdAbl | kLaneMaskLoads, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
-  else if (variant == 7) // production + per-batch gate on the skip branches
-    launch_one<0, 1, kProdAbl | kSkipBatchGate, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
-  else if (variant == 8) // production + one branch per frame for both loads
-    launch_one<0, 1, kProdAbl | kSkipPairBranch, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
-  else if (variant == 9) // production + the skipping form only in waves with a short frame
-    launch_one<0, 1, kProdAbl | kSkipWaveGate, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s);
   else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
@@ -242,11 +234,9 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 34: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 0>(a, s); break;  // no LDS pad: 5 waves/SIMD
     case 35: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, kProdGopt | 8>(a, s); break;  // XCD-contiguous (production)
     case 36: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, 2 << 4>(a, s); break;  // blockIdx order
-    case 37: launch_one<0, 1, kProdAbl & ~kSkipEmptyLoads>(a, s); break;  // every stream load issued (before kSkipEmptyLoads)
-    case 38: launch_one<0, 1, kProdAbl | kLaneMaskLoads>(a, s); break;    // + lane-masked stream loads
-    case 39: launch_one<0, 1, kProdAbl | kSkipBatchGate>(a, s); break;    // + per-batch gate on the skip branches
-    case 40: launch_one<0, 1, kProdAbl | kSkipPairBranch>(a, s); break;   // + one branch per frame for both loads
-    case 41: launch_one<0, 1, kProdAbl | kSkipWaveGate>(a, s); break;     // + the skipping form only in waves with a short frame
+    case 37: launch_one<0, 1, kProdAbl & ~kSkipEmptyLoads>(a, s); break;  // every stream load issued (before kSkipEmptyLoads;
+    // the per-lane EXEC mask, per-batch gate and per-frame pair branch forms measured against it are
+    // in the history)
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;

@@ -5,10 +5,8 @@
   prod_tuning    the same production kernel launched from the tuning library (variant 35) --
                  isolates the launch path from the kernel
   every_load     every stream load issued (the form before kSkipEmptyLoads; variant 37 / indexed 5)
-  lane_masked    + each load EXEC-masked to the lanes inside the extent (variant 38 / indexed 6)
-  batch_gate     + the skip branches only in batches with an empty load (variant 39 / indexed 7)
-  pair_branch    + one branch per frame choosing both loads, the first, or none (variant 40 / indexed 8)
-  wave_gate      + the skipping form only in waves with a frame ending in its first KiB (41 / indexed 9)
+(The per-lane EXEC mask, per-batch gate and per-frame pair-branch forms this script also timed are in
+the history: commit c98da75)
 
 Strided 2-KiB slots for C2/C3/C5; packed captures (frames back to back, indexed kernel) for
 C3/C5.  Every form's records must equal the product's.  Needs `make TUNING=1`.  One JSON line."""
@@ -61,9 +59,7 @@ def main():
             return lambda: tn.classify_variant(ctx, frames, stride, off, n, res, st, v)
 
         runs = {"strided_product": lambda: ctx.classify(frames, stride, off, n, res, st),
-                "strided_prod_tuning": sv(35), "strided_every_load": sv(37), "strided_lane_masked": sv(38),
-                "strided_batch_gate": sv(39), "strided_pair_branch": sv(40),
-                "strided_wave_gate": sv(41)}
+                "strided_prod_tuning": sv(35), "strided_every_load": sv(37)}
         algo = {k: wire + 16 * n for k in runs}
         if cfg != 2:
             packed, starts, pbytes = packed_layout(np, s, n, off)
@@ -74,8 +70,7 @@ def main():
                 return lambda: tn.classify_indexed_variant(ctx, dev, offs, off, n, stride - off, res, st, v)
 
             runs.update({"packed_product": lambda: ctx.classify_indexed(dev, offs, off, n, stride - off, res, st),
-                         "packed_every_load": iv(5), "packed_lane_masked": iv(6), "packed_batch_gate": iv(7),
-                         "packed_pair_branch": iv(8), "packed_wave_gate": iv(9)})
+                         "packed_every_load": iv(5)})
             for k in runs:
                 algo.setdefault(k, pbytes + 16 * n)
         equal = {}
