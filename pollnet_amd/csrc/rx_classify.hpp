@@ -67,6 +67,14 @@ struct KArgs {
   uint32_t fpw = kFramesPerWave; // frames per wave (8..64): small batches spread over more waves (latency)
 };
 
+// Conn-table lookup carried from the home-slot load to its resolution.
+struct Probe {
+  uint64_t key;
+  uint32_t e;
+  uint64_t k;   // key of entry e (PN_EMPTY_KEY when not loaded)
+  uint32_t cid; // conn_id of entry e
+};
+
 // Per-frame state the header lane keeps from phase 1 to phase 3.
 struct FrameState {
   uint32_t flags, ihl, tot_len, src_ip, dst_ip, seq_raw, doff, tflags, s_ip20, s_opt, tcp_len, conn_id;
@@ -75,6 +83,110 @@ struct FrameState {
   uint32_t pad;   // odd tcp_len: the byte after the segment (kPadUnknown until phase 2 captured it)
   bool trunc;
 };
+
+// connHashKey (Core.h:167-172) and the load of the home slot `key & tbl_mask` (Core.h:558-559).
+__device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port, bool live, const KArgs& a) {
+  Probe p;
+  const uint32_t ip_h = __builtin_bswap32(src_ip);
+  const uint32_t port_h = bswap16(src_port);
+  p.key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
+  p.e = (uint32_t)(p.key & a.mask);
+  p.k = PN_EMPTY_KEY;
+  p.cid = 0;
+  if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
+    const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + p.e);
+    p.k = ((uint64_t)ent.y << 32) | ent.x;
+    p.cid = ent.z;
+  }
+  return p;
+}
+
+// The rest of findConnEntry's ordered walk (Core.h:560-561) and the conn / TIME_WAIT / miss
+// verdict (Core.h:510).  Every lane of the wave must call it (the cooperative walk ballots).
+template <int ABL>
+__device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KArgs& a, uint32_t& conn_id, uint32_t& flags) {
+  const uint64_t key = p.key;
+  uint32_t e = p.e;
+  uint64_t k = p.k;
+  uint32_t cid = p.cid;
+  if constexpr (ABL & kCoopProbe) {
+    // Lanes whose run continues past the home slot are served one at a time by the whole
+    // wave (all 64 lanes reach here): 64 consecutive entries per round trip, the first with
+    // key >= the lane's key (or the array end) found by a ballot -- the entry the scalar
+    // walk stops at.
+    const uint32_t lane = threadIdx.x;
+    bool srch = live && e < a.n_entries && k < key;
+    if (__ballot(srch) != 0) {
+      // short runs (the common case past the home slot): every searching lane fetches its
+      // next kAhead entries at once -- one round trip for all of them, in parallel
+      constexpr int kAhead = 2;
+      u32x4 nx[kAhead];
+#pragma unroll
+      for (int j = 0; j < kAhead; ++j) {
+        nx[j] = u32x4{0u, 0u, 0u, 0u};
+        if (srch && e + 1 + j < a.n_entries) nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + e + 1 + j);
+      }
+      uint32_t step = 0, cid2 = 0;
+      uint64_t k2 = 0;
+#pragma unroll
+      for (int j = kAhead - 1; j >= 0; --j) { // the first entry (in order) that stops the walk
+        const uint64_t kk = ((uint64_t)nx[j].y << 32) | nx[j].x;
+        if (e + 1 + j >= a.n_entries || kk >= key) {
+          step = j + 1;
+          k2 = kk;
+          cid2 = nx[j].z;
+        }
+      }
+      if (srch) {
+        if (step != 0) {
+          e += step;
+          k = k2;
+          cid = cid2;
+          srch = false;
+        } else {
+          e += kAhead; // every fetched key < key: the run goes on
+        }
+      }
+    }
+    uint64_t need = __ballot(srch);
+    while (need != 0) { // wave-uniform
+      const uint32_t L = (uint32_t)__builtin_ctzll(need);
+      need &= need - 1;
+      const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L); // readlane returns int
+      for (uint32_t base = __builtin_amdgcn_readlane(e, L) + 1;; base += kWave) {
+        const uint32_t idx = base + lane;
+        u32x4 ent = {0u, 0u, 0u, 0u};
+        if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
+        const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
+        const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
+        if (stop != 0) {
+          const uint32_t first = (uint32_t)__builtin_ctzll(stop);
+          const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
+          const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
+          if (lane == L) {
+            e = base + first;
+            k = ((uint64_t)khi << 32) | klo;
+            cid = c;
+          }
+          break;
+        }
+      }
+    }
+  } else {
+    while (live && e < a.n_entries && k < key) {
+      if (++e >= a.n_entries) break;
+      const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
+      k = ((uint64_t)ent.y << 32) | ent.x;
+      cid = ent.z;
+    }
+  }
+  if (live && e < a.n_entries && k == key) {
+    conn_id = cid;
+    flags |= PN_F_HIT;
+    if (cid >= a.max_conn) flags |= PN_F_TW;
+  }
+}
 
 // ---- phase 1: decode one frame from its header window (lane f <-> frame f) ----
 template <int MIS, int ABL>
@@ -119,98 +231,11 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   // the part of the region in the window below the stream start, summed from registers
   st.t_all = window_part<MIS>(h, st.end_rel & ~1, s0);
 
-  // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries
+  // connHashKey (Core.h:167-172) + findConnEntry (Core.h:558-562), bounded at n_entries.
+  // (Resolving the probe after phase 2 instead, so the home-slot load overlaps the stream loads,
+  // measured no faster: profiles/r02/s3/late_probe_ab.json.)
   st.conn_id = PN_MISS;
-  if constexpr (!(ABL & kAblNoProbe)) {
-    const uint32_t ip_h = __builtin_bswap32(st.src_ip);
-    const uint32_t port_h = bswap16(src_port);
-    const uint64_t key = ((uint64_t)ip_h << 15) | (port_h & 0x7fff) | ((uint64_t)(port_h & 0x8000) << 32);
-    uint32_t e = (uint32_t)(key & a.mask);
-    uint64_t k = PN_EMPTY_KEY;
-    uint32_t cid = 0;
-    if (live && e < a.n_entries) { // the home slot: almost every lookup ends here
-      const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
-      k = ((uint64_t)ent.y << 32) | ent.x;
-      cid = ent.z;
-    }
-    if constexpr (ABL & kCoopProbe) {
-      // Lanes whose run continues past the home slot are served one at a time by the whole
-      // wave (all 64 lanes reach here): 64 consecutive entries per round trip, the first with
-      // key >= the lane's key (or the array end) found by a ballot -- the entry the scalar
-      // walk stops at.
-      const uint32_t lane = threadIdx.x;
-      bool srch = live && e < a.n_entries && k < key;
-      if (__ballot(srch) != 0) {
-        // short runs (the common case past the home slot): every searching lane fetches its
-        // next kAhead entries at once -- one round trip for all of them, in parallel
-        constexpr int kAhead = 2;
-        u32x4 nx[kAhead];
-#pragma unroll
-        for (int j = 0; j < kAhead; ++j) {
-          nx[j] = u32x4{0u, 0u, 0u, 0u};
-          if (srch && e + 1 + j < a.n_entries) nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + e + 1 + j);
-        }
-        uint32_t step = 0, cid2 = 0;
-        uint64_t k2 = 0;
-#pragma unroll
-        for (int j = kAhead - 1; j >= 0; --j) { // the first entry (in order) that stops the walk
-          const uint64_t kk = ((uint64_t)nx[j].y << 32) | nx[j].x;
-          if (e + 1 + j >= a.n_entries || kk >= key) {
-            step = j + 1;
-            k2 = kk;
-            cid2 = nx[j].z;
-          }
-        }
-        if (srch) {
-          if (step != 0) {
-            e += step;
-            k = k2;
-            cid = cid2;
-            srch = false;
-          } else {
-            e += kAhead; // every fetched key < key: the run goes on
-          }
-        }
-      }
-      uint64_t need = __ballot(srch);
-      while (need != 0) { // wave-uniform
-        const uint32_t L = (uint32_t)__builtin_ctzll(need);
-        need &= need - 1;
-        const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L); // readlane returns int
-        for (uint32_t base = __builtin_amdgcn_readlane(e, L) + 1;; base += kWave) {
-          const uint32_t idx = base + lane;
-          u32x4 ent = {0u, 0u, 0u, 0u};
-          if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
-          const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
-          const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
-          if (stop != 0) {
-            const uint32_t first = (uint32_t)__builtin_ctzll(stop);
-            const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
-            const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
-            if (lane == L) {
-              e = base + first;
-              k = ((uint64_t)khi << 32) | klo;
-              cid = c;
-            }
-            break;
-          }
-        }
-      }
-    } else {
-      while (live && e < a.n_entries && k < key) {
-        if (++e >= a.n_entries) break;
-        const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + e);
-        k = ((uint64_t)ent.y << 32) | ent.x;
-        cid = ent.z;
-      }
-    }
-    if (live && e < a.n_entries && k == key) {
-      st.conn_id = cid;
-      flags |= PN_F_HIT;
-      if (cid >= a.max_conn) flags |= PN_F_TW;
-    }
-  }
+  if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
   st.flags = flags;
   return st;
 }

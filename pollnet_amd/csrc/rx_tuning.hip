@@ -171,6 +171,7 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   a.ipa_off = 0;
   a.avail = avail;
   a.offs = offsets;
+  a.fpw = frames_per_wave(n);
   hipStream_t s = (hipStream_t)stream;
   if (variant == 1) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, kXcdOrder>(a, s); // window non-temporal
   else if (variant == 2) launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, 0, 1, 0>(a, s);  // production window, blockIdx order
@@ -203,6 +204,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   a.ipa_off = (frame_off + 14) & ~15u;
   a.avail = slot_stride - frame_off;
   a.offs = nullptr;
+  a.fpw = frames_per_wave(n); // the product's launch shape
   hipStream_t s = (hipStream_t)stream;
   if ((variant & 1) && !coop_layout(a)) return set_err(ctx, PN_EINVAL, "variant: needs the cooperative layout");
   // Tuning variants of the MIS = 0 (ip at slot+16) kernel, A/B-timed in one process by
