@@ -36,7 +36,7 @@ SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
 CLISRVTEST = tests/cpp/test_tcp_client_server
 
-all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
@@ -102,6 +102,11 @@ $(SRVBENCH): bench/bench_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server
 $(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $(LIB) $(TUNING_LIB)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
+# completion by a polled word (pn_classify_notify) vs stream sync, small batches
+SIGBENCH = bench/bench_signal
+$(SIGBENCH): bench/bench_signal.cpp $(HDRS) $(LIB)
+	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+
 # zero-copy classify from host rings of each pinned-memory kind: PCIe rate and staleness
 $(PINBENCH): bench/bench_pinned.cpp $(HDRS) $(LIB)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
@@ -134,6 +139,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 .PHONY: all ref clean

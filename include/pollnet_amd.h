@@ -228,6 +228,23 @@ int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint
 int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n, const uint16_t* lens,
                uint32_t mode, void* stream);
 
+/* Small batches, latency: pn_classify / pn_tx_fill whose launch also stores `token` to
+ * *done_word (4-byte aligned, host-visible: pinned host memory) once every record / field it
+ * writes is stored and visible to the host.  A host that polls the word (an acquire load)
+ * sees a 64..1024-frame batch done ≈3-4 µs sooner than hipStreamSynchronize returns (DESIGN.md
+ * §13); the stream orders later work as usual, and pn_sync / hipStreamSynchronize still apply.
+ * The same arguments as pn_classify (strided slots) / pn_tx_fill, plus: n in
+ * [1, PN_NOTIFY_MAX_FRAMES] (every workgroup makes its stores system-visible, which only pays
+ * off for small batches).  The per-ctx counter behind the word is reused: a notify call on
+ * another stream than the previous one of the same kind first waits for the device.
+ * Replaces the completion step of the reference's poll (ef_eventq_poll's RX/TX events,
+ * Core.h:496-498): the host learns the batch is done from one memory word. */
+#define PN_NOTIFY_MAX_FRAMES 1024u
+int pn_classify_notify(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                       void* results, void* stream, uint32_t* done_word, uint32_t token);
+int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                      const uint16_t* lens, uint32_t mode, void* stream, uint32_t* done_word, uint32_t token);
+
 /* Wait for the last stream used by this ctx. */
 int pn_sync(pn_ctx* ctx);
 

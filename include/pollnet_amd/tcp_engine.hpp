@@ -280,6 +280,7 @@ class GpuBackend {
     if (tx_stream_) (void)hipStreamDestroy(tx_stream_);
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
+    if (tx_word_) (void)hipHostFree(tx_word_);
   }
 
   // rx_chunk: frames per classify launch (a poll's frames go in chunks, the next one on the
@@ -305,6 +306,9 @@ class GpuBackend {
       return "hipHostMalloc(rx ring) failed";
     if (hipHostMalloc((void**)&tx_ring_, tx_bytes, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(tx batch) failed";
+    if (!tx_word_ && hipHostMalloc((void**)&tx_word_, 64, hipHostMallocDefault) != hipSuccess)
+      return "hipHostMalloc(tx notify word) failed";
+    *tx_word_ = tx_tok_;
     std::memset(rx_ring_, 0, rx_bytes);
     std::memset(tx_ring_, 0, tx_bytes);
     return nullptr;
@@ -335,14 +339,24 @@ class GpuBackend {
     if (const char* e = fillTxLaunch(n, half)) return e;
     return fillTxWait();
   }
+  // Batches of up to PN_NOTIFY_MAX_FRAMES (a poll's ACKs) complete through a pinned word
+  // (pn_tx_fill_notify): the host sees the fill done ≈4 us before a stream sync would return.
   const char* fillTxLaunch(uint32_t n, uint32_t half) {
+    tx_word_used_ = n <= PN_NOTIFY_MAX_FRAMES;
+    if (tx_word_used_) {
+      if (pn_tx_fill_notify(rx_.ctx(), txSlots(half), kStride, kFrameOff, n, nullptr, PN_TX_TCP, tx_stream_, tx_word_,
+                            ++tx_tok_))
+        return pn_last_error(rx_.ctx());
+      return nullptr;
+    }
     if (pn_tx_fill(rx_.ctx(), txSlots(half), kStride, kFrameOff, n, nullptr, PN_TX_TCP, tx_stream_))
       return pn_last_error(rx_.ctx());
     return nullptr;
   }
   const char* fillTxWait() {
+    if (tx_word_used_ && wait_word(tx_word_, tx_tok_, tx_stream_) == nullptr) return nullptr;
     if (hipStreamSynchronize(tx_stream_) != hipSuccess) return "hipStreamSynchronize(tx_fill) failed";
-    return nullptr;
+    return tx_word_used_ ? "tx_fill notify word not written" : nullptr;
   }
 
  private:
@@ -356,6 +370,9 @@ class GpuBackend {
   hipStream_t tx_stream_ = nullptr;
   uint8_t* rx_ring_ = nullptr;
   uint8_t* tx_ring_ = nullptr;
+  uint32_t* tx_word_ = nullptr; // pinned notify word of the TX fill
+  uint32_t tx_tok_ = 0;
+  bool tx_word_used_ = false;   // the fill in flight completes through tx_word_
   uint32_t rx_cap_ = 0, tx_cap_ = 0;
 };
 

@@ -160,6 +160,24 @@ inline uint32_t frames_per_wave(uint32_t n) {
   return fpw;
 }
 
+// Completion word (pn_classify_notify / pn_tx_fill_notify): every workgroup makes its stores
+// system-visible and counts itself done; the last one resets the device counter and stores
+// `token` to the host-visible word, so a host polling the word sees the batch done without
+// waiting for the launch's completion signal.  Each workgroup's system fence writes back L2,
+// which is why the notify entry points are limited to small batches (PN_NOTIFY_MAX_FRAMES).
+// Only vector memory operations (a global atomic, vector stores).
+__device__ __forceinline__ void signal_done(uint32_t* count, uint32_t* word, uint32_t token, int lane) {
+  __threadfence_system();
+  if (lane == 0) {
+    const uint32_t prev = atomicAdd(count, 1u);
+    if (prev == gridDim.x - 1) {
+      __threadfence_system();
+      count[0] = 0u;
+      __hip_atomic_store(word, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t nwg) {
   const uint32_t per = (nwg + 7) / 8, x = b % 8, k = b / 8;
   const uint32_t full = nwg % 8 == 0 ? 8 : nwg % 8; // XCDs that own `per` groups (the rest own per - 1)

@@ -20,6 +20,9 @@ struct pn_ctx {
   void* tx_patch = nullptr;       // pn_tx_fill's per-frame patch records (8 B each)
   uint32_t tx_patch_n = 0;
   hipStream_t tx_stream = nullptr; // stream of the last pn_tx_fill (the scratch is reused)
+  void* sig_count = nullptr;       // pn_*_notify workgroup counters: [0] classify, [16] tx_fill (64-B apart)
+  hipStream_t sig_stream[2] = {nullptr, nullptr}; // stream of the last notify launch of each kind
+  bool sig_used[2] = {false, false};
   std::string err;
 };
 
@@ -44,6 +47,27 @@ inline int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
 inline int wait_table_readers(pn_ctx* ctx) {
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize(table readers)");
+  return PN_OK;
+}
+
+// The workgroup counter of a notify launch of `kind` (0 classify, 1 tx_fill), device memory,
+// zero between launches (the last workgroup resets it).  The next launch of that kind reuses it,
+// so a launch on another stream than the previous one first waits for the device (the previous
+// stream may be gone; a rare path).
+inline int notify_counter(pn_ctx* ctx, int kind, hipStream_t s, uint32_t** out) {
+  hipError_t e;
+  if (!ctx->sig_count) {
+    e = hipMalloc(&ctx->sig_count, 128);
+    if (e == hipSuccess) e = hipMemset(ctx->sig_count, 0, 128);
+    if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(notify counters)");
+  }
+  if (ctx->sig_used[kind] && ctx->sig_stream[kind] != s) {
+    e = hipDeviceSynchronize();
+    if (e != hipSuccess) return hip_err(ctx, e, "hipDeviceSynchronize(notify counter)");
+  }
+  ctx->sig_stream[kind] = s;
+  ctx->sig_used[kind] = true;
+  *out = (uint32_t*)ctx->sig_count + 16 * kind;
   return PN_OK;
 }
 

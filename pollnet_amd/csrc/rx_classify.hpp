@@ -65,6 +65,9 @@ struct KArgs {
   uint32_t avail;   // stride - frame_off: bytes from the Ethernet header to the slot end
   const uint64_t* offs; // indexed layout: frame i's Ethernet header at frames + offs[i] (nullptr: strided)
   uint32_t fpw = kFramesPerWave; // frames per wave (8..64): small batches spread over more waves (latency)
+  uint32_t* sig_count = nullptr;  // kSignalDone: workgroups finished (device memory, 0 before the launch)
+  uint32_t* sig_flag = nullptr;   // kSignalDone: host-visible word the last workgroup sets to sig_token
+  uint32_t sig_token = 0;
 };
 
 // Conn-table lookup carried from the home-slot load to its resolution.
@@ -439,6 +442,8 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
 // (profiles/r01_experiments/xcd_order_c{2,3,5}.json; records identical).
 constexpr int kXcdOrder = 8;
 constexpr int kProdGopt = (2 << 4) | kXcdOrder;
+// Bit 6: completion word (pn_classify_notify; signal_done in frame_pass.hpp).
+constexpr int kSignalDone = 64;
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
           int GRP = 1, int GOPT = kProdGopt>
 __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
@@ -451,6 +456,7 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 =
   if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
     // contiguous eighth of the batch instead of every eighth group
     classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, xcd_group(blockIdx.x, gridDim.x) * a.fpw, lane, nullptr);
+    if constexpr (GOPT & kSignalDone) signal_done(a.sig_count, a.sig_flag, a.sig_token, lane);
   } else if constexpr (GRP == 1 || (GOPT & 1)) {
 #pragma nounroll
     for (int g = 0; g < GRP; ++g)
@@ -496,9 +502,10 @@ void launch_one(const KArgs& a, hipStream_t s) {
 }
 
 
-template <int MIS>
+template <int MIS, bool SIG = false>
 void launch(const KArgs& a, hipStream_t s) {
-  if (coop_layout(a)) return launch_one<MIS, 1>(a, s);
-  launch_one<MIS, 0>(a, s);
+  constexpr int G = SIG ? (kProdGopt | kSignalDone) : kProdGopt;
+  if (coop_layout(a)) return launch_one<MIS, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, G>(a, s);
+  launch_one<MIS, 0, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, G>(a, s);
 }
 } // namespace

@@ -8,6 +8,46 @@ namespace {
 using pn_internal::g_err;
 using pn_internal::hip_err;
 using pn_internal::set_err;
+
+// Argument checks and kernel arguments shared by pn_classify and pn_classify_notify.
+int strided_args(pn_ctx* ctx, const char* fn, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off,
+                 uint32_t n, void* results_dev, KArgs& a) {
+  if (!ctx) return set_err(nullptr, PN_EINVAL, std::string(fn) + ": ctx is NULL");
+  if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, std::string(fn) + ": no conn table (call pn_set_conn_table)");
+  if (!frames_dev || !results_dev) return set_err(ctx, PN_EINVAL, std::string(fn) + ": NULL buffer");
+  if (((uintptr_t)frames_dev & 15) || ((uintptr_t)results_dev & 15))
+    return set_err(ctx, PN_EINVAL, std::string(fn) + ": frames/results must be 16-byte aligned");
+  if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || slot_stride < frame_off + 96)
+    return set_err(ctx, PN_EINVAL, std::string(fn) + ": slot_stride/frame_off violate the layout contract");
+  a.frames = (const uint8_t*)frames_dev;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.avail = slot_stride - frame_off;
+  a.offs = nullptr;
+  a.fpw = frames_per_wave(n);
+  return PN_OK;
+}
+
+template <bool SIG>
+void launch_strided(const KArgs& a, uint32_t frame_off, hipStream_t s) {
+  switch ((frame_off + 14) & 15) {
+    case 0: launch<0, SIG>(a, s); break;
+    case 2: launch<2, SIG>(a, s); break;
+    case 4: launch<4, SIG>(a, s); break;
+    case 6: launch<6, SIG>(a, s); break;
+    case 8: launch<8, SIG>(a, s); break;
+    case 10: launch<10, SIG>(a, s); break;
+    case 12: launch<12, SIG>(a, s); break;
+    default: launch<14, SIG>(a, s); break;
+  }
+}
+
 } // namespace
 
 extern "C" {
@@ -37,11 +77,12 @@ int pn_open(int device, pn_ctx** out) {
 
 void pn_close(pn_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->tbl_dev || ctx->tx_patch) {
+  if (ctx->tbl_dev || ctx->tx_patch || ctx->sig_count) {
     (void)hipSetDevice(ctx->device);
     (void)pn_internal::wait_table_readers(ctx); // also covers the last tx_fill's patch scratch
     if (ctx->tbl_dev) (void)hipFree(ctx->tbl_dev);
     if (ctx->tx_patch) (void)hipFree(ctx->tx_patch);
+    if (ctx->sig_count) (void)hipFree(ctx->sig_count);
   }
   delete ctx;
 }
@@ -80,42 +121,38 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
 
 int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                 void* results_dev, void* stream) {
-  if (!ctx) return set_err(nullptr, PN_EINVAL, "pn_classify: ctx is NULL");
-  if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, "pn_classify: no conn table (call pn_set_conn_table)");
-  if (n == 0) return PN_OK;
-  if (!frames_dev || !results_dev) return set_err(ctx, PN_EINVAL, "pn_classify: NULL buffer");
-  if (((uintptr_t)frames_dev & 15) || ((uintptr_t)results_dev & 15))
-    return set_err(ctx, PN_EINVAL, "pn_classify: frames/results must be 16-byte aligned");
-  if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || slot_stride < frame_off + 96)
-    return set_err(ctx, PN_EINVAL, "pn_classify: slot_stride/frame_off violate the layout contract");
+  if (ctx && n == 0 && ctx->tbl_dev) return PN_OK;
   KArgs a;
-  a.frames = (const uint8_t*)frames_dev;
-  a.out = (pn_result*)results_dev;
-  a.tbl = ctx->tbl_dev;
-  a.mask = ctx->mask;
-  a.n_entries = ctx->n_entries;
-  a.max_conn = ctx->max_conn;
-  a.n = n;
-  a.stride = slot_stride;
-  a.ipa_off = (frame_off + 14) & ~15u;
-  a.avail = slot_stride - frame_off;
-  a.offs = nullptr;
-  a.fpw = frames_per_wave(n);
+  int rc = strided_args(ctx, "pn_classify", frames_dev, slot_stride, frame_off, n, results_dev, a);
+  if (rc) return rc;
+  if (n == 0) return PN_OK;
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  switch ((frame_off + 14) & 15) {
-    case 0: launch<0>(a, s); break;
-    case 2: launch<2>(a, s); break;
-    case 4: launch<4>(a, s); break;
-    case 6: launch<6>(a, s); break;
-    case 8: launch<8>(a, s); break;
-    case 10: launch<10>(a, s); break;
-    case 12: launch<12>(a, s); break;
-    default: launch<14>(a, s); break;
-  }
+  launch_strided<false>(a, frame_off, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify launch");
+  ctx->last_stream = s;
+  return PN_OK;
+}
+
+int pn_classify_notify(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                       void* results, void* stream, uint32_t* done_word, uint32_t token) {
+  KArgs a;
+  int rc = strided_args(ctx, "pn_classify_notify", frames, slot_stride, frame_off, n, results, a);
+  if (rc) return rc;
+  if (n == 0 || n > PN_NOTIFY_MAX_FRAMES || !done_word || ((uintptr_t)done_word & 3))
+    return set_err(ctx, PN_EINVAL, "pn_classify_notify: n must be in [1, PN_NOTIFY_MAX_FRAMES], done_word 4-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  rc = pn_internal::notify_counter(ctx, 0, s, &a.sig_count);
+  if (rc) return rc;
+  a.sig_flag = done_word;
+  a.sig_token = token;
+  launch_strided<true>(a, frame_off, s);
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (notify) launch");
   ctx->last_stream = s;
   return PN_OK;
 }

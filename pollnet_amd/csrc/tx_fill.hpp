@@ -59,6 +59,9 @@ struct TArgs {
   uint32_t frame_off;
   uint2* patch;      // n patch records (ctx scratch)
   uint32_t fpw = kFramesPerWave; // frames per wave (8..64, frames_per_wave)
+  uint32_t* sig_count = nullptr;  // SIG (pn_tx_fill_notify): workgroups finished, device memory
+  uint32_t* sig_flag = nullptr;   // SIG: host-visible word the last workgroup sets to sig_token
+  uint32_t sig_token = 0;
 };
 
 // Patch record: x = ip checksum | (tcp checksum or udp_len) << 16, y = tot_len word | flags << 16
@@ -78,8 +81,9 @@ constexpr int kWbPatch = -2;
 // SABL: the stream phase's options.  Every stream load is issued (kExactRange): TX batches are
 // mostly full-size frames, where skipping empty loads measured 1.8 % slower at frame_off 2 and
 // equal at 14 (tuning variant 42 = with kSkipEmptyLoads, profiles/r02/s3/tx_skip_ab_off*.json).
+// SIG: completion word (pn_tx_fill_notify, signal_done in frame_pass.hpp).
 template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false,
-          int SABL = kExactRange>
+          int SABL = kExactRange, bool SIG = false>
 __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   const int lane = threadIdx.x;
   const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * a.fpw;
@@ -197,6 +201,7 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
       }
     }
   }
+  if constexpr (SIG) signal_done(a.sig_count, a.sig_flag, a.sig_token, lane);
 }
 
 // Phase 2: one lane per frame writes the fields its patch record carries.
@@ -279,28 +284,28 @@ inline bool coop_layout(const TArgs& a) {
 // (§12: the in-place writes' write-back would land in the rest of the stream).
 constexpr uint32_t kTxInPlaceMaxFrames = 65536;
 
-template <int MIS, int MODE, int WB>
+template <int MIS, int MODE, int WB, bool SIG = false>
 void launch(const TArgs& a, hipStream_t s) {
   const dim3 grid((a.n + a.fpw - 1) / a.fpw), block(kWave);
   // XCD-contiguous group order, as the RX kernel: -1.7 % (profiles/r01_experiments/tx_xcd_order_off{2,14}.json)
   if (coop_layout(a)) {
-    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, WB, 0, 0, 0, true>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, WB, 0, 0, 0, true, kExactRange, SIG>), grid, block, 0, s, a);
     return;
   }
-  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, WB, 0, 0, 0, true>), grid, block, 0, s, a);
+  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, WB, 0, 0, 0, true, kExactRange, SIG>), grid, block, 0, s, a);
 }
 
-template <int MODE, int WB>
+template <int MODE, int WB, bool SIG = false>
 void launch_mis(const TArgs& a, uint32_t mis, hipStream_t s) {
   switch (mis) {
-    case 0: launch<0, MODE, WB>(a, s); break;
-    case 2: launch<2, MODE, WB>(a, s); break;
-    case 4: launch<4, MODE, WB>(a, s); break;
-    case 6: launch<6, MODE, WB>(a, s); break;
-    case 8: launch<8, MODE, WB>(a, s); break;
-    case 10: launch<10, MODE, WB>(a, s); break;
-    case 12: launch<12, MODE, WB>(a, s); break;
-    default: launch<14, MODE, WB>(a, s); break;
+    case 0: launch<0, MODE, WB, SIG>(a, s); break;
+    case 2: launch<2, MODE, WB, SIG>(a, s); break;
+    case 4: launch<4, MODE, WB, SIG>(a, s); break;
+    case 6: launch<6, MODE, WB, SIG>(a, s); break;
+    case 8: launch<8, MODE, WB, SIG>(a, s); break;
+    case 10: launch<10, MODE, WB, SIG>(a, s); break;
+    case 12: launch<12, MODE, WB, SIG>(a, s); break;
+    default: launch<14, MODE, WB, SIG>(a, s); break;
   }
 }
 

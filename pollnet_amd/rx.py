@@ -23,6 +23,7 @@ PN_RECV_BUF_SIZE = 2048
 PN_TX_TCP = 0       # efvitcp SendBuf::setOptDataLen / sumRst / resendUna (Core.h:157-163, 385-398; TcpConn.h:771-785)
 PN_TX_UDP_EFVI = 1  # Efvi update_udp_pkt with the cached IPv4 sum (Efvi.h:405-411, 611-621), bit-exact
 PN_TX_UDP = 2       # the same fields with CSum::fold (Core.h:94-98): always a verifying header checksum
+PN_NOTIFY_MAX_FRAMES = 1024  # pn_classify_notify / pn_tx_fill_notify batch limit
 
 
 class F:
@@ -114,6 +115,8 @@ _pn_set_conn_table = _sig("pn_set_conn_table", _i32, _vp, _vp, _u32, _u64, _u32)
 _pn_classify = _sig("pn_classify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_classify_indexed = _sig("pn_classify_indexed", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
 _pn_tx_fill = _sig("pn_tx_fill", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp)
+_pn_classify_notify = _sig("pn_classify_notify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _u32)
+_pn_tx_fill_notify = _sig("pn_tx_fill_notify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp, _u32)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 _pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
@@ -257,6 +260,19 @@ class RxContext:
             self._h,
             "pn_classify",
         )
+
+    def classify_notify(self, frames, slot_stride: int, frame_off: int, n: int, results, done_word, token: int,
+                        stream=None):
+        """pn_classify_notify: as classify (n <= PN_NOTIFY_MAX_FRAMES), and the launch stores
+        `token` to the u32 at done_word (pinned host memory) once every record is visible."""
+        _check(_pn_classify_notify(self._h, _ptr(frames), slot_stride, frame_off, n, _ptr(results),
+                                   _stream_handle(stream), _ptr(done_word), token), self._h, "pn_classify_notify")
+
+    def tx_fill_notify(self, frames, slot_stride: int, frame_off: int, n: int, done_word, token: int, lens=None,
+                       mode: int = PN_TX_TCP, stream=None):
+        """pn_tx_fill_notify: as tx_fill (n <= PN_NOTIFY_MAX_FRAMES) with the completion word."""
+        _check(_pn_tx_fill_notify(self._h, _ptr(frames), slot_stride, frame_off, n, _ptr(lens), mode,
+                                  _stream_handle(stream), _ptr(done_word), token), self._h, "pn_tx_fill_notify")
 
     def classify_indexed(self, base, offsets, eth_mod16: int, n: int, avail: int, results, stream=None):
         """Frames at base + offsets[i] (u64; device or pinned host memory), all with
