@@ -303,9 +303,11 @@ def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, lens=None, reps=1
 
     out = {"note": "calib kernels in pollnet_amd/csrc/rx_tuning.hip (libpollnet_amd_tuning.so); no header work, "
                    "no arithmetic"}
+    # the plain stream read of the whole ring: a ceiling, and the known byte count that calibrates
+    # FETCH_SIZE in the PMC passes (scripts/gpu_pmc.sh, pmc_summarize.py)
+    ts = t(lambda: tn.calib_stream_read(ctx, frames, frames.numel(), sink, stream))
+    out["stream_read_gbs"] = round(frames.numel() / ts / 1e9, 1)
     if slot_pattern:
-        ts = t(lambda: tn.calib_stream_read(ctx, frames, frames.numel(), sink, stream))
-        out["stream_read_gbs"] = round(frames.numel() / ts / 1e9, 1)
         t0 = t(lambda: tn.calib_slot_read(ctx, frames, n, STRIDE, 1536, sink, stream, 0))
         t16 = t(lambda: tn.calib_slot_read(ctx, frames, n, STRIDE, 1536, res, stream, 16))
         out["slot_pattern_read_gbs"] = round(n * 1536 / t0 / 1e9, 1)
