@@ -448,6 +448,7 @@ template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX =
           int GRP = 1, int GOPT = kProdGopt>
 __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
   const int lane = threadIdx.x;
+  static_assert(!(GOPT & kSignalDone) || ((GOPT & 8) && GRP == 1), "the completion word is set on the XCD-ordered one-group path");
   if constexpr ((GOPT >> 4) > 0) {
     __shared__ uint32_t pad_lds[(GOPT >> 4) * 256];
     pad_lds[lane] = lane;
