@@ -442,15 +442,16 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
 // (profiles/r01_experiments/xcd_order_c{2,3,5}.json; records identical).
 constexpr int kXcdOrder = 8;
 constexpr int kProdGopt = (2 << 4) | kXcdOrder;
-// Bit 6: completion word (pn_classify_notify; signal_done in frame_pass.hpp).
-constexpr int kSignalDone = 64;
+// Bit 12: completion word (pn_classify_notify; signal_done in frame_pass.hpp).  Above the LDS-padding
+// field (bits 4-11).
+constexpr int kSignalDone = 1 << 12;
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
           int GRP = 1, int GOPT = kProdGopt>
 __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
   const int lane = threadIdx.x;
   static_assert(!(GOPT & kSignalDone) || ((GOPT & 8) && GRP == 1), "the completion word is set on the XCD-ordered one-group path");
-  if constexpr ((GOPT >> 4) > 0) {
-    __shared__ uint32_t pad_lds[(GOPT >> 4) * 256];
+  if constexpr (((GOPT >> 4) & 0xff) > 0) {
+    __shared__ uint32_t pad_lds[((GOPT >> 4) & 0xff) * 256];
     pad_lds[lane] = lane;
     if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
   }
