@@ -488,6 +488,25 @@ def server_poll():
         return {"error": repr(ex)}
 
 
+def small_batch_latency():
+    """Host-visible round trip of one small batch (bench/bench_signal): pn_classify +
+    stream sync against pn_classify_notify + a spin on the pinned completion word, 64 / 512 / 1024
+    C2 frames, device-resident and zero-copy; median host wall clock, records compared."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "bench", "bench_signal")
+    if not os.path.exists(exe):
+        return {"error": "bench/bench_signal not built"}
+    try:
+        r = subprocess.run([exe, "200"], capture_output=True, text=True, timeout=60)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        if r.returncode != 0:
+            line["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
+        return line
+    except Exception as ex:  # measured extra; never blocks the bench line
+        return {"error": repr(ex)}
+
+
 def secondary_tx(torch, pa, n, steps, stream):
     """TX checksum fill (pn_tx_fill, PN_TX_TCP) over C2 batches with both checksum fields
     scrambled, at the ring layout (frame_off 2) and efvitcp's SendBuf layout (frame_off 14 =
@@ -720,6 +739,7 @@ def run_rank(rank, world, local_rank, args):
         except Exception as ex:  # measured extras; never block the bench line
             sec["error"] = repr(ex)
         sec["tcp_server_poll"] = server_poll()
+        sec["small_batch_latency"] = small_batch_latency()
         sec["seconds"] = round(time.perf_counter() - t_sec, 1)
         out["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_e2e:
