@@ -29,6 +29,8 @@ LATBENCH = bench/bench_latency
 SRVBENCH = bench/bench_tcp_server
 PINBENCH = bench/bench_pinned
 TXSMALLBENCH = bench/bench_tx_small
+# (defined before `all`: make expands a rule's prerequisites where the rule is read)
+SIGBENCH = bench/bench_signal
 RINGTEST = tests/cpp/test_rx_ring
 STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
@@ -103,7 +105,6 @@ $(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # completion by a polled word (pn_classify_notify) vs stream sync, small batches
-SIGBENCH = bench/bench_signal
 $(SIGBENCH): bench/bench_signal.cpp $(HDRS) $(LIB)
 	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 

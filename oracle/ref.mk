@@ -1,7 +1,8 @@
 # Builds oracle/_ref from the reference's own sources where they lie (read-only).
-# Buildable here: TcpStream.h (header-only) and Socket.h (BSD sockets, config C1).
-# efvitcp/Core.h needs <etherfabric/*.h> (ef_vi, not installed) and stand-ins for those
-# headers are not allowed, so it is not built.
+# Buildable here: TcpStream.h (header-only), Socket.h (BSD sockets, config C1), and the
+# hot-path parts of efvitcp/Core.h that touch no ef_vi type (line ranges below).  The whole
+# Core.h needs <etherfabric/*.h> (ef_vi, not installed); stand-ins for those headers are not
+# allowed, so Core.h as a unit is not built.
 REFDIR ?= /root/reference
 all: _ref/libref_tcpstream.so _ref/ref_socket_c1 _ref/tcpserver_handler.inc _ref/tcpclient_handler.inc _ref/libref_core.so
 

@@ -49,6 +49,21 @@ def test_tuning_library_is_separate():
     assert "tuning" not in src  # the product package never loads the tuning library
 
 
+def test_default_build_covers_every_native_binary():
+    """`make` (what build() runs) builds every executable that bench.py and the tests start:
+    the GPU box only gets what was built here."""
+    out = subprocess.run(["make", "-C", ROOT, "-pn", "all"], capture_output=True, text=True).stdout
+    all_line = next(ln for ln in out.splitlines() if ln.startswith("all:") and "libpollnet_amd.so" in ln)
+    prereqs = set(all_line.split(":", 1)[1].split())
+    used = set()
+    for f in ["bench.py"] + [os.path.join("tests", t) for t in os.listdir(os.path.join(ROOT, "tests")) if t.endswith(".py")]:
+        src = open(os.path.join(ROOT, f)).read()
+        used |= {f"bench/{m}" for m in re.findall(r'"bench", "(bench_[a-z_]+)"', src)}
+        used |= {f"tests/cpp/{m}" for m in re.findall(r'"cpp", "(test_[a-z_]+)"', src)}
+    assert {"bench/bench_signal", "bench/bench_tcp_server", "tests/cpp/test_gpu_rx"} <= used
+    assert used <= prereqs, sorted(used - prereqs)
+
+
 def test_result_layout():
     assert pa.RESULT_DTYPE.itemsize == 16
     assert [pa.RESULT_DTYPE.fields[k][1] for k in ("conn_id", "seq", "payload_off", "payload_len", "flags", "tcp_fold")] == [
