@@ -304,3 +304,35 @@ def test_gpu_full_size_c2_round_trip():
     assert bool(same[~corrupted].all())
     assert not bool(same[corrupted].any())
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_fill_argument_contract():
+    """n = 0 is a no-op; an unknown mode, a misaligned buffer or a layout outside the contract
+    (odd frame_off, stride not a 16-B multiple or too short) fails with PN_EINVAL and a message,
+    before any launch: the frames are left as they were."""
+    torch, pa = _gpu()
+    ctx = pa.RxContext(0)
+    slots, _, _ = orc.tx_build_batch(0xA11, 64, frame_off=14, mode=orc.TX_TCP)
+    s = scramble(slots, 14, orc.TX_TCP, False)
+    d = torch.from_numpy(s.reshape(-1).copy()).cuda()
+    ctx.tx_fill(d, 2048, 14, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), s.reshape(-1))
+    bad_calls = [
+        dict(frames=d, stride=2048, off=14, mode=7),          # unknown mode
+        dict(frames=d[2:], stride=2048, off=14, mode=0),      # frames not 16-B aligned
+        dict(frames=d, stride=2040, off=14, mode=0),          # stride not a 16-B multiple
+        dict(frames=d, stride=2048, off=13, mode=0),          # odd frame_off
+        dict(frames=d, stride=96, off=14, mode=0),            # stride < frame_off + 96
+        dict(frames=d, stride=65552, off=14, mode=0),         # stride > 65536
+    ]
+    for c in bad_calls:
+        with pytest.raises(pa.PollnetError, match=r"\(-?\d+\)"):
+            ctx.tx_fill(c["frames"], c["stride"], c["off"], 16, None, c["mode"])
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), s.reshape(-1))
+    ctx.tx_fill(d, 2048, 14, 64)  # the ctx still works after the refused calls
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy().reshape(s.shape), slots)
+    ctx.close()
