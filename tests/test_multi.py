@@ -150,3 +150,30 @@ def test_bench_spawns_ranks_itself():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
     assert line["config"]["global_frames"] == 2 * 65536
+
+
+@pytest.mark.gpu
+def test_bench_under_the_drivers_torchrun_command():
+    """The driver's own N>1 launch (`python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+    --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...`), N = 2 on this box's GPU:
+    rank 0 alone prints one JSON line, n_gpus 2, the aggregate over both ranks."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--frames", "65536", "--batches", "2", "--no-cpu-baseline", "--no-e2e", "--no-secondary"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
+    assert line["config"]["global_frames"] == 2 * 65536
+    assert line["value"] > 0 and line["scaling"] == "weak"
