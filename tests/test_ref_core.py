@@ -229,3 +229,50 @@ def test_gpu_records_digest_equals_reference_batch():
         ctx.close()
     digest, _ = orc.RefBench(entries).batch(slots, 2048, 2, n, 4)
     assert digest == orc.records_digest(rec)
+
+
+@pytest.mark.parametrize("frame_off", [2, 10, 18])
+def test_random_bytes_match_reference(frame_off):
+    """Arbitrary bytes (random header fields, random IHL / data offset / flags, tot_len
+    anywhere from 0 to past the slot, odd and even; half of them with checksums that verify):
+    every record field the reference's own
+    Core::checksum and onPack head compute equals the oracle's, wherever the reference's reads
+    stay inside the slot (elsewhere the oracle flags TRUNC, as the GPU does)."""
+    import ctypes
+
+    rng = np.random.default_rng(0xF022 + frame_off)
+    n, stride = 6000, 2048
+    slots = rng.integers(0, 256, (n, stride), dtype=np.uint8)
+    tot = rng.integers(0, stride - frame_off + 64, n)
+    sane = rng.random(n) < 0.6
+    tot[sane] = rng.integers(20, 1501, int(sane.sum()))
+    eth = frame_off
+    slots[:, eth + 16] = (tot >> 8) & 0xFF
+    slots[:, eth + 17] = tot & 0xFF
+    filled = slots.copy()  # half the frames with checksums that verify (the TX fill's recomputation)
+    orc.tx_fill_batch(filled, stride, frame_off, n, None, orc.TX_TCP)
+    pick = rng.random(n) < 0.5
+    slots[pick] = filled[pick]
+    ent = np.zeros(16, pa.ENTRY_DTYPE)
+    ent["key"] = pa.PN_EMPTY_KEY
+    rec = orc.classify_batch(slots, stride, frame_off, n, ent, 15, 1)
+    ipf, tcpf = ctypes.c_uint32(), ctypes.c_uint32()
+    off_, len_, seq_ = ctypes.c_uint32(), ctypes.c_int32(), ctypes.c_uint32()
+    checked = ok_both = 0
+    for i in range(n):
+        e = np.ascontiguousarray(slots[i, frame_off:])
+        t = int(tot[i])
+        f = int(rec["flags"][i])
+        ref.ref_onpack_head(e.ctypes.data, ctypes.byref(off_), ctypes.byref(len_), ctypes.byref(seq_))
+        assert int(rec["payload_off"][i]) == off_.value and int(rec["payload_len"][i]) == len_.value, i
+        assert int(rec["seq"][i]) == seq_.value, i
+        if t < 20 or 14 + t + (t & 1) > stride - frame_off:
+            assert f & pa.F.TRUNC or t < 20, i
+            continue
+        v = ref.ref_checksum_folds(e.ctypes.data, ctypes.byref(ipf), ctypes.byref(tcpf))
+        assert bool(v & 1) == bool(f & pa.F.IP_OK), i
+        assert bool(v & 2) == bool(f & pa.F.TCP_OK), i
+        assert int(rec["tcp_fold"][i]) == tcpf.value, i
+        checked += 1
+        ok_both += (v == 3)
+    assert checked > 3000 and ok_both > 500  # both verdicts occur
