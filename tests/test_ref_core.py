@@ -235,9 +235,9 @@ def test_gpu_records_digest_equals_reference_batch():
 def test_random_bytes_match_reference(frame_off):
     """Arbitrary bytes (random header fields, random IHL / data offset / flags, tot_len
     anywhere from 0 to past the slot, odd and even; half of them with checksums that verify):
-    every record field the reference's own
-    Core::checksum and onPack head compute equals the oracle's, wherever the reference's reads
-    stay inside the slot (elsewhere the oracle flags TRUNC, as the GPU does)."""
+    every record field the reference's own Core::checksum and onPack head compute equals the
+    oracle's, wherever the reference's reads stay inside the slot (elsewhere the oracle flags
+    TRUNC, as the GPU does)."""
     import ctypes
 
     rng = np.random.default_rng(0xF022 + frame_off)
