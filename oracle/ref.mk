@@ -58,5 +58,16 @@ _ref/onpack_head.inc: $(REFDIR)/efvitcp/TcpConn.h
 	mkdir -p _ref
 	sed -n '468p' $< | grep -q 'void onPack' && sed -n '473p' $< | grep -q 'seq_num' && sed -n '474p' $< | grep -q got_ts
 	sed -n '469,473p' $< > $@
-_ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc _ref/onpack_head.inc
+# The send path's byte work (TX checksum fill parity): TcpConn::copyAndSum (TcpConn.h:257-299)
+# and SendBuf::setOptDataLen (Core.h:157-163)
+_ref/tx_copyandsum.inc: $(REFDIR)/efvitcp/TcpConn.h
+	mkdir -p _ref
+	sed -n '257p' $< | grep -q 'CSum copyAndSum' && sed -n '299p' $< | grep -q '^  }$$' && sed -n '300p' $< | grep -q '^$$'
+	sed -n '257,299p' $< > $@
+_ref/tx_setoptdatalen.inc: $(CORE)
+	mkdir -p _ref
+	sed -n '157p' $< | grep -q 'void setOptDataLen' && sed -n '163p' $< | grep -q '^  }$$'
+	sed -n '157,163p' $< > $@
+_ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc _ref/onpack_head.inc \
+  _ref/tx_copyandsum.inc _ref/tx_setoptdatalen.inc
 	g++ -O3 -march=x86-64-v3 -std=c++17 -fPIC -shared -pthread -Wno-unused-result -o $@ ref_core.cc

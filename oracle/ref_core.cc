@@ -8,6 +8,8 @@
 //                                             delConnEntry, printTbl, tryExpandConnTbl
 //   core_checksum.inc Core.h:448-472          Core::checksum (EFVITCP_DEBUG)
 //   onpack_head.inc   TcpConn.h:469-473       TcpConn::onPack's payload extent and seq
+//   tx_copyandsum.inc TcpConn.h:257-299       TcpConn::copyAndSum (send path: append + sum)
+//   tx_setoptdatalen.inc Core.h:157-163       SendBuf::setOptDataLen (tot_len, both folds)
 // Those member functions are pasted, unchanged, into RefCore below, which supplies only
 // the data members they read (conn_tbl, tbl_mask, conn_cnt, conns, tw_cnt, tw_ids) and
 // takes the debug build's `cout` / `exit(1)` as members, so a failed check is recorded
@@ -78,6 +80,20 @@ struct RefCore {
 
 #include "_ref/core_table.inc"
 #include "_ref/core_checksum.inc"
+};
+// The send path's byte work.  SendBuf's header part (Core.h:147-156 without post_addr, send_ts,
+// avail and pad, which setOptDataLen does not touch) with setOptDataLen pasted unchanged, and
+// TcpConn's copyAndSum pasted unchanged into a holder (it reads no TcpConn member).
+#pragma pack(push, 1)
+struct RefSendHdr {
+  EtherHeader eth_hdr;
+  IpHeader ip_hdr;
+  TcpHeader tcp_hdr;
+#include "_ref/tx_setoptdatalen.inc"
+};
+#pragma pack(pop)
+struct RefCopyAndSum {
+#include "_ref/tx_copyandsum.inc"
 };
 } // namespace efvitcp
 
@@ -153,6 +169,47 @@ void ref_onpack_head(uint8_t* eth, uint32_t* payload_off, int32_t* payload_len, 
   *payload_off = (uint32_t)(data - eth);
   *payload_len = (int32_t)(data_end - data);
   *seq = seq_num;
+}
+
+// One data segment of an established connection without timestamps, built as TcpConn builds
+// it, on a frame whose Ethernet / IP / TCP headers (data_offset 5, urgent pointer 0) are in
+// place at eth: reset (TcpConn.h:149-168) caches ipsum over the IP header with tot_len and
+// checksum zeroed and tcpsum = src + dst + ntohs(6) + both ports; onEstablished (:422-428)
+// adds offset_flags; sendPartial (:232-256) appends the payload in the given pieces with
+// copyAndSum, each piece at its real address (odd ones too), into data_sum; sendBuf
+// (:310-323) adds seq, ack and window, then tcpsum, and setOptDataLen writes tot_len and the
+// two checksums.  The glue is restated; copyAndSum, CSum and setOptDataLen are the reference's.
+void ref_tx_data_segment(uint8_t* eth, const uint8_t* payload, uint32_t len, const uint32_t* pieces,
+                         uint32_t n_pieces) {
+  using namespace efvitcp;
+  RefSendHdr* b = reinterpret_cast<RefSendHdr*>(eth);
+  b->ip_hdr.tot_len = 0;
+  b->ip_hdr.checksum = 0;
+  CSum ipsum = 0;
+  ipsum.add<sizeof(IpHeader)>(&b->ip_hdr);
+  CSum tcpsum = 0;
+  tcpsum.add(b->ip_hdr.src_ip);
+  tcpsum.add(b->ip_hdr.dst_ip);
+  tcpsum.add(ntohs(0x6));
+  tcpsum.add(b->tcp_hdr.src_port);
+  tcpsum.add(b->tcp_hdr.dst_port);
+  tcpsum.add(b->tcp_hdr.offset_flags);
+  CSum data_sum = 0;
+  RefCopyAndSum c;
+  uint8_t* data = eth + sizeof(RefSendHdr);
+  uint32_t off = 0;
+  for (uint32_t i = 0; i < n_pieces && off < len; i++) {
+    const uint32_t m = std::min(pieces[i], len - off);
+    data_sum.add(c.copyAndSum(data + off, payload + off, m));
+    off += m;
+  }
+  if (off < len) data_sum.add(c.copyAndSum(data + off, payload + off, len - off));
+  CSum sum = data_sum;
+  sum.add(b->tcp_hdr.seq_num);
+  sum.add(b->tcp_hdr.ack_num);
+  sum.add(b->tcp_hdr.window_size);
+  sum.add(tcpsum);
+  b->setOptDataLen((uint16_t)len, ipsum, sum);
 }
 
 // ---- the conn table, driven the way the reference's callers drive it ----

@@ -9,6 +9,10 @@ sumRst for RST / TIME_WAIT ACKs (Core.h:385-446), and Efvi's cached IPv4 sum
 frames a reference sender puts on the wire; pn_tx_fill, which recomputes the checksums
 from the frame bytes in one HBM pass, must reproduce them byte for byte.
 
+The reference's own send-path byte work (TcpConn::copyAndSum, SendBuf::setOptDataLen and
+CSum, compiled verbatim into oracle/_ref/libref_core.so) builds data segments too; the
+recomputation, and pn_tx_fill on the GPU, reproduce those byte for byte.
+
 CPU: the incremental path equals the byte recomputation (orc_tx_fill_batch) on every
 frame kind; every TCP frame passes the reference's own debug self-check (Core::checksum,
 Core.h:448-472, applied by Core::send :478); RFC 1071 known answer; Efvi's cache carry
@@ -335,4 +339,67 @@ def test_gpu_fill_argument_contract():
     ctx.tx_fill(d, 2048, 14, 64)  # the ctx still works after the refused calls
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy().reshape(s.shape), slots)
+    ctx.close()
+
+
+def _ref_built_segments(seed, n, frame_off=14, stride=2048):
+    """n data segments built by the reference's own send-path code (oracle/_ref/libref_core.so:
+    TcpConn::copyAndSum and SendBuf::setOptDataLen compiled verbatim, the connection's cached
+    sums restated around them): random addresses, ports, seq/ack/window, payloads of 0..1460
+    bytes appended in 1..4 random pieces (odd sizes put later pieces at odd addresses)."""
+    ref = orc.ref_core()
+    if ref is None:
+        pytest.skip("oracle/_ref/libref_core.so not built (needs /root/reference)")
+    rng = np.random.default_rng(seed)
+    slots = np.zeros((n, stride), np.uint8)
+    for i in range(n):
+        e = slots[i, frame_off:]
+        e[0:12] = rng.integers(0, 256, 12)
+        e[12:14] = (0x08, 0x00)
+        e[14:34] = rng.integers(0, 256, 20)  # IpHeader: any tos/id/frag/ttl/addresses
+        e[14] = 0x45
+        e[23] = 6
+        e[34:54] = rng.integers(0, 256, 20)  # TcpHeader: any ports/seq/ack/flags/window
+        e[46] = 0x50 | (e[46] & 0x0F)  # data_offset 5
+        e[52:54] = 0  # urgent pointer
+        ln = int(rng.integers(0, 1461))
+        payload = rng.integers(0, 256, ln, dtype=np.uint8)
+        pieces = np.array(rng.integers(1, 700, int(rng.integers(1, 5))), np.uint32)
+        buf = np.ascontiguousarray(slots[i])
+        ref.ref_tx_data_segment(buf.ctypes.data + frame_off, payload.ctypes.data, ln, pieces.ctypes.data, len(pieces))
+        slots[i] = buf
+        assert np.array_equal(slots[i, frame_off + 54:frame_off + 54 + ln], payload)
+    return slots
+
+
+def test_byte_recompute_equals_reference_send_path():
+    """The oracle's one-pass recomputation (the GPU kernel's contract) reproduces segments the
+    reference's own copyAndSum + setOptDataLen built, byte for byte, in the SendBuf layout
+    (frame_off 14) and the RX-ring layout (2); every one passes the reference's Core::checksum
+    when its segment is even (odd ones: the debug check reads the byte after the segment)."""
+    for off in (14, 2):
+        slots = _ref_built_segments(0x5E0D + off, 3000, off)
+        s = scramble(slots, off, orc.TX_TCP, False)
+        orc.tx_fill_batch(s, 2048, off, len(s), None, orc.TX_TCP)
+        assert np.array_equal(s, slots)
+        rec = orc.classify_batch(slots, 2048, off, len(slots), E_EMPTY, 1, 1)
+        tot = (slots[:, off + 16].astype(int) << 8) | slots[:, off + 17]
+        even = (tot & 1) == 0
+        assert ((rec["flags"][even] & 3) == 3).all() and even.sum() > 1000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame_off", [14, 2])
+def test_gpu_fill_equals_reference_send_path(frame_off):
+    """pn_tx_fill on segments the reference's own copyAndSum + setOptDataLen built (checksums
+    scrambled first) gives back those segments byte for byte, in both launch forms."""
+    torch, pa = _gpu()
+    ctx = pa.RxContext(0)
+    slots = _ref_built_segments(0x6E0D + frame_off, 3000, frame_off)
+    s = scramble(slots, frame_off, orc.TX_TCP, False)
+    got = _fill_gpu(ctx, torch, s, 2048, frame_off, len(s), None, 0)
+    assert np.array_equal(got, slots)
+    big = np.tile(s, (23, 1))[:66000]  # > kTxInPlaceMaxFrames: the two-phase form
+    got = _fill_gpu(ctx, torch, big, 2048, frame_off, len(big), None, 0)
+    assert np.array_equal(got, np.tile(slots, (23, 1))[:66000])
     ctx.close()
