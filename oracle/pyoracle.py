@@ -220,6 +220,7 @@ def ref_core():
             ("ref_onpack_head", None, [_vp, _vp, _vp, _vp]),
             ("ref_checksum_folds", _i32, [_vp, _vp, _vp]),
             ("ref_tx_data_segment", None, [_vp, _vp, _u32, _vp, _u32]),
+            ("ref_efvi_udp_datagram", None, [_vp, _u32]),
             ("ref_table_new", _vp, []),
             ("ref_table_free", None, [_vp]),
             ("ref_table_add", _i32, [_vp, _u64, _u32]),

@@ -68,6 +68,21 @@ _ref/tx_setoptdatalen.inc: $(CORE)
 	mkdir -p _ref
 	sed -n '157p' $< | grep -q 'void setOptDataLen' && sed -n '163p' $< | grep -q '^  }$$'
 	sed -n '157,163p' $< > $@
+# Efvi's UDP send path (the PN_TX_UDP_EFVI contract): its header structs (Efvi.h:557-586, up to
+# the ef_addr-holding pkt_buf), the cached IPv4 header sum (:406-411) and update_udp_pkt (:611-621)
+EFVI = $(REFDIR)/Efvi.h
+_ref/efvi_hdrs.inc: $(EFVI)
+	mkdir -p _ref
+	sed -n '557p' $< | grep -q 'pragma pack(push, 1)' && sed -n '558p' $< | grep -q ci_ether_hdr && sed -n '580p' $< | grep -q ci_udp_hdr && sed -n '586p' $< | grep -q '^  };$$'
+	sed -n '557,586p' $< > $@
+_ref/efvi_ipsum_cache.inc: $(EFVI)
+	mkdir -p _ref
+	sed -n '405p' $< | grep -q 'uint16_t\* ip4' && sed -n '406p' $< | grep -q 'ipsum_cache = 0;' && sed -n '411p' $< | grep -q 'ipsum_cache += (ipsum_cache >> 16u);'
+	sed -n '406,411p' $< > $@
+_ref/efvi_update_udp_pkt.inc: $(EFVI)
+	mkdir -p _ref
+	sed -n '611p' $< | grep -q 'void update_udp_pkt' && sed -n '621p' $< | grep -q '^  }$$'
+	sed -n '611,621p' $< > $@
 _ref/libref_core.so: ref_core.cc _ref/core_defs.inc _ref/core_sizes.inc _ref/core_table.inc _ref/core_checksum.inc _ref/onpack_head.inc \
-  _ref/tx_copyandsum.inc _ref/tx_setoptdatalen.inc
+  _ref/tx_copyandsum.inc _ref/tx_setoptdatalen.inc _ref/efvi_hdrs.inc _ref/efvi_ipsum_cache.inc _ref/efvi_update_udp_pkt.inc
 	g++ -O3 -march=x86-64-v3 -std=c++17 -fPIC -shared -pthread -Wno-unused-result -o $@ ref_core.cc

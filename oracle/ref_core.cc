@@ -10,6 +10,9 @@
 //   onpack_head.inc   TcpConn.h:469-473       TcpConn::onPack's payload extent and seq
 //   tx_copyandsum.inc TcpConn.h:257-299       TcpConn::copyAndSum (send path: append + sum)
 //   tx_setoptdatalen.inc Core.h:157-163       SendBuf::setOptDataLen (tot_len, both folds)
+//   efvi_hdrs.inc     Efvi.h:557-586          ci_ether_hdr / ci_ip4_hdr / ci_udp_hdr
+//   efvi_ipsum_cache.inc Efvi.h:406-411       Efvi's cached IPv4 header sum
+//   efvi_update_udp_pkt.inc Efvi.h:611-621    Efvi::update_udp_pkt (tot_len, checksum, udp_len)
 // Those member functions are pasted, unchanged, into RefCore below, which supplies only
 // the data members they read (conn_tbl, tbl_mask, conn_cnt, conns, tw_cnt, tw_ids) and
 // takes the debug build's `cout` / `exit(1)` as members, so a failed check is recorded
@@ -210,6 +213,29 @@ void ref_tx_data_segment(uint8_t* eth, const uint8_t* payload, uint32_t len, con
   sum.add(b->tcp_hdr.window_size);
   sum.add(tcpsum);
   b->setOptDataLen((uint16_t)len, ipsum, sum);
+}
+
+// Efvi's UDP sender (Efvi.h): the header structs, the cached IPv4 header sum and update_udp_pkt
+// pasted unchanged; the cache is taken over the frame's own IPv4 header with tot_len and checksum
+// zeroed, as init_udp_pkt's ci_ip4_hdr_init leaves them (Efvi.h:403-411, 625-640).
+struct RefEfviUdp {
+#include "_ref/efvi_hdrs.inc"
+#pragma pack(pop)
+  uint32_t ipsum_cache = 0;
+  void cache(uint8_t* eth) {
+    uint16_t* ip4 = (uint16_t*)(eth + 14);
+#include "_ref/efvi_ipsum_cache.inc"
+  }
+#include "_ref/efvi_update_udp_pkt.inc"
+};
+
+// One Efvi datagram: header cached with tot_len = checksum = 0, then update_udp_pkt(paylen).
+void ref_efvi_udp_datagram(uint8_t* eth, uint32_t paylen) {
+  RefEfviUdp u;
+  eth[16] = eth[17] = 0; // ip_tot_len_be16
+  eth[24] = eth[25] = 0; // ip_check_be16
+  u.cache(eth);
+  u.update_udp_pkt(eth, paylen);
 }
 
 // ---- the conn table, driven the way the reference's callers drive it ----

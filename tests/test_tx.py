@@ -10,8 +10,9 @@ frames a reference sender puts on the wire; pn_tx_fill, which recomputes the che
 from the frame bytes in one HBM pass, must reproduce them byte for byte.
 
 The reference's own send-path byte work (TcpConn::copyAndSum, SendBuf::setOptDataLen and
-CSum, compiled verbatim into oracle/_ref/libref_core.so) builds data segments too; the
-recomputation, and pn_tx_fill on the GPU, reproduce those byte for byte.
+CSum; Efvi's cached IPv4 sum and update_udp_pkt — compiled verbatim into
+oracle/_ref/libref_core.so) builds data segments and datagrams too; the recomputation, and
+pn_tx_fill on the GPU, reproduce those byte for byte.
 
 CPU: the incremental path equals the byte recomputation (orc_tx_fill_batch) on every
 frame kind; every TCP frame passes the reference's own debug self-check (Core::checksum,
@@ -402,4 +403,65 @@ def test_gpu_fill_equals_reference_send_path(frame_off):
     big = np.tile(s, (23, 1))[:66000]  # > kTxInPlaceMaxFrames: the two-phase form
     got = _fill_gpu(ctx, torch, big, 2048, frame_off, len(big), None, 0)
     assert np.array_equal(got, np.tile(slots, (23, 1))[:66000])
+    ctx.close()
+
+
+def _ref_efvi_datagrams(seed, n, frame_off=2, stride=2048):
+    """n UDP datagrams through Efvi's own code (oracle/_ref/libref_core.so: the cached IPv4 sum,
+    Efvi.h:406-411, and update_udp_pkt, :611-621, compiled verbatim): random addresses and
+    header words, random payload lengths, and every 8th header chosen so that the cache's first
+    end-around step carries (the defect).  Returns (slots, paylens, defect rows)."""
+    ref = orc.ref_core()
+    if ref is None:
+        pytest.skip("oracle/_ref/libref_core.so not built (needs /root/reference)")
+    rng = np.random.default_rng(seed)
+    slots = np.zeros((n, stride), np.uint8)
+    paylens = rng.integers(0, stride - frame_off - 42 + 1, n).astype(np.uint16)
+    defect = np.zeros(n, bool)
+    need = 0x1FFFF - 0x11C5  # craft_udp_header's other words sum to 0x11C5
+    for i in range(n):
+        e = slots[i, frame_off:]
+        e[0:12] = rng.integers(0, 256, 12)
+        e[12:14] = (0x08, 0x00)
+        if i % 8 == 0:
+            e[14:34] = np.frombuffer(craft_udp_header([0xFFFF, need - 0xFFFF], [0, 0], 0), np.uint8)
+        else:
+            e[14:34] = rng.integers(0, 256, 20)
+            e[14], e[23] = 0x45, 17
+        e[34:42] = rng.integers(0, 256, 8)
+        e[42:42 + int(paylens[i])] = rng.integers(0, 256, int(paylens[i]))
+        words = e[14:34].view("<u2").astype(np.int64)
+        c = int(words.sum()) - int(words[1]) - int(words[5])
+        defect[i] = (c >> 16) + (c & 0xFFFF) >= 0x10000
+        buf = np.ascontiguousarray(slots[i])
+        ref.ref_efvi_udp_datagram(buf.ctypes.data + frame_off, int(paylens[i]))
+        slots[i] = buf
+    assert defect.sum() >= n // 8
+    return slots, paylens, defect
+
+
+def test_efvi_mode_equals_reference_update_udp_pkt():
+    """PN_TX_UDP_EFVI's recomputation (with lens = paylen) reproduces Efvi's own
+    update_udp_pkt output byte for byte, the carry defect included; PN_TX_UDP agrees wherever
+    Efvi's checksum verifies and differs exactly on the defect rows."""
+    for off in (2, 14):
+        slots, paylens, defect = _ref_efvi_datagrams(0xEF1 + off, 2000, off)
+        s = scramble(slots, off, orc.TX_UDP_EFVI, True)
+        orc.tx_fill_batch(s, 2048, off, len(s), paylens, orc.TX_UDP_EFVI)
+        assert np.array_equal(s, slots)
+        u = scramble(slots, off, orc.TX_UDP_EFVI, True)
+        orc.tx_fill_batch(u, 2048, off, len(u), paylens, orc.TX_UDP)
+        differs = (u != slots).any(1)
+        assert np.array_equal(differs, defect)
+
+
+@pytest.mark.gpu
+def test_gpu_efvi_mode_equals_reference_update_udp_pkt():
+    torch, pa = _gpu()
+    ctx = pa.RxContext(0)
+    for off in (2, 14):
+        slots, paylens, _ = _ref_efvi_datagrams(0xEF9 + off, 3000, off)
+        s = scramble(slots, off, orc.TX_UDP_EFVI, True)
+        got = _fill_gpu(ctx, torch, s, 2048, off, len(s), paylens, 1)
+        assert np.array_equal(got, slots)
     ctx.close()
