@@ -38,84 +38,93 @@ SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
 CLISRVTEST = tests/cpp/test_tcp_client_server
 
-all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+# Host programs that include HIP headers: compiled by hipcc with the device pass pinned to gfx950
+# (without --offload-arch hipcc would add a default-arch device pass for nothing)
+HOSTHIP = $(HIPCC) --offload-arch=$(ARCH)
+
+# The two example-handler tests compile text the ref recipe extracts from /root/reference
+# (oracle/_ref/*.inc, never committed, never sent to the GPU box).  Where neither that text nor
+# the reference is present (a fresh GPU box), they are not rebuilt: their prebuilt binaries are used.
+REF_INCS = oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
+HAVE_REF_TEXT = $(or $(wildcard $(REFDIR)/example/tcpserver.cc),$(and $(wildcard oracle/_ref/tcpserver_handler.inc),$(wildcard oracle/_ref/tcpclient_handler.inc)))
+REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST))
+
+all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
 $(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp include/pollnet_amd/rx_ring.hpp $(HDRS) $(LIB) $(ORACLE) \
   oracle/_ref/tcpserver_handler.inc
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
-oracle/_ref/tcpserver_handler.inc:
-	$(MAKE) ref
+$(REF_INCS):
+	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR) $(@:oracle/%=%); \
+	else echo "$@: no $(REFDIR) to extract it from" >&2; exit 1; fi
 
 # GpuTcpClient <-> GpuTcpServer running both reference example handlers over a lossy in-memory wire
 $(CLISRVTEST): tests/cpp/test_tcp_client_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
   include/pollnet_amd/tcp_client.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) \
   oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
-	$(HIPCC) -O2 -std=c++17 -Wall -Wno-unused-function -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -Wno-unused-function -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
-
-oracle/_ref/tcpclient_handler.inc:
-	$(MAKE) ref
 
 # GpuTcpServer against reactive in-memory TCP peers (loss, timers, windows), GPU vs twin
 $(PEERTEST): tests/cpp/test_tcp_server_peer.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
   include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # TcpStream reassembly restated vs the reference's own TcpStream (4 instantiations)
 $(STREAMTEST): tests/cpp/test_tcp_stream.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_stream.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle -ldl \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle -ldl \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # pn_match_streams + GpuTcpStreams vs the reference filterPacket / TcpStream (GPU)
 $(GPUSTREAMTEST): tests/cpp/test_gpu_tcp_stream.cpp tests/cpp/segframes.hpp include/pollnet_amd/tcp_stream.hpp \
   include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle -ldl \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle -ldl \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # RX-ring ingestion: socket batcher (+ loopback capture when permitted), ef_vi event rings on the GPU
 $(RINGTEST): tests/cpp/test_rx_ring.cpp include/pollnet_amd/rx_ring.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # batch size vs throughput and latency of pn_classify (resident, host ring in/records out, hipGraph)
 $(LATBENCH): bench/bench_latency.cpp $(HDRS) $(LIB)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # poll() throughput (GPU-classified) vs the same host loop over the CPU release path
 $(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
 # GpuTcpServer::poll throughput (handshake, RX, ACKs) on the GPU vs the same server on the sequential backend
 $(SRVBENCH): bench/bench_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp \
   include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
 # TX fill at small batch sizes, one in-place launch vs two phases (variant 41: make TUNING=1; not in `all`)
 $(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $(LIB) $(TUNING_LIB)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # completion by a polled word (pn_classify_notify) vs stream sync, small batches
 $(SIGBENCH): bench/bench_signal.cpp $(HDRS) $(LIB)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # zero-copy classify from host rings of each pinned-memory kind: PCIe rate and staleness
 $(PINBENCH): bench/bench_pinned.cpp $(HDRS) $(LIB)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # receive-side server loop on the GPU vs a sequential twin with reference semantics
 $(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # receive-side state machine (host only): scenarios + differential vs the reference TcpStream
@@ -124,7 +133,7 @@ $(RXCONNTEST): tests/cpp/test_rx_conn.cpp tests/cpp/segframes.hpp include/pollne
 
 # standalone C++ adapter test (no torch): links the product library and, as the checker, the oracle
 $(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HIPCC) -O2 -std=c++17 -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O2 -std=c++17 -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 $(LIB): $(SRCS) $(HDRS) $(KHDRS)

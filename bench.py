@@ -3,12 +3,15 @@
 
 One step = one pn_classify launch over this rank's batch of RX-ring slots already
 resident in HBM (parse + IP/TCP checksum verification + conn-table probe +
-payload off/len, one 16-B record per frame).  Default workload = BASELINE config
-C2 (1 Mi x 1514-B IPv4/TCP frames, 1 flow) per GPU; N GPUs = N independent
-contiguous index shards of one global batch (weak scaling, no collective on the
-data path: the frames shard by index and nothing is exchanged).
-torch.distributed over gloo (host-side, no RCCL) carries only the start/stop
-barriers and the max-over-ranks / sum-over-ranks reductions of the timing.
+payload off/len, one 16-B record per frame).  Default workload at one GPU = BASELINE
+configs[1] (C2: 1 Mi x 1514-B IPv4/TCP frames, 1 flow); at N>1 GPUs = configs[3]
+(C4: 16 Mi x 1514-B frames over 1024 flows sharded by index across 8 GPUs, i.e.
+2 Mi frames per GPU, rank r owning global frames [r*2Mi, (r+1)*2Mi)): weak scaling,
+no collective on the data path (the frames shard by index and nothing is exchanged,
+SURVEY §8e).  Every rank sha256-gates its own shard against the committed oracle
+digest.  torch.distributed over gloo (host-side, no RCCL) carries only the start/stop
+barriers, the reductions of the timing and the gathered gates; the aggregate is timed
+over one common barrier-to-barrier window.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--frames N]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -54,7 +57,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5],
+                    help="workload (default: C2 at one GPU, C4 = BASELINE configs[3] at N>1)")
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: 1 Mi; C4: 2 Mi)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -330,12 +334,20 @@ def load_pmc(workload_key):
         return None
 
 
-def golden_digest(cfg):
+def golden_digest(cfg, first=0, n=None):
+    """The committed oracle digest over config cfg's global frames [first, first+n) (tests/golden/
+    make_golden.py): C2/C3/C5 [0, 1 Mi) and C4's 8 shards of 2 Mi; None when none covers that range."""
     try:
         with open(os.path.join(ROOT, "tests", "golden", "full_digests.json")) as f:
-            return json.load(f).get(f"c{cfg}")
+            full = json.load(f)
     except (OSError, ValueError):
         return None
+    cands = [dict(full[f"c{cfg}"], first_index=0)] if f"c{cfg}" in full else []
+    cands += full.get(f"c{cfg}_shards", [])
+    for d in cands:
+        if d.get("first_index", 0) == first and (n is None or d["n"] == n):
+            return d
+    return None
 
 
 def time_launches(torch, fn, bufs, steps, stream, warmup=2, settle_s=0.04):
@@ -577,7 +589,7 @@ def run_rank(rank, world, local_rank, args):
     import torch.distributed as dist
 
     import pollnet_amd as pa
-    from pollnet_amd.shard import shard_range
+    from pollnet_amd.shard import common_window, shard_range
 
     ndev = max(1, torch.cuda.device_count())
     dev = local_rank % ndev
@@ -585,7 +597,9 @@ def run_rank(rank, world, local_rank, args):
     if world > 1:  # host-side coordination only: barriers and two scalar reductions (no RCCL)
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    cfg = args.config
+    # N=1: BASELINE configs[1] (C2, 1 Mi single-flow frames).  N>1: configs[3] (C4, 16 Mi frames over
+    # 1024 flows sharded by index across 8 GPUs = 2 Mi per GPU; rank r owns global [r*2Mi, (r+1)*2Mi)).
+    cfg = args.config or (2 if world == 1 else 4)
     n = args.frames or ((1 << 21) if cfg == 4 else (1 << 20))
     params = pa.rx.GenParams.for_config(cfg)
     lo, _ = shard_range(rank, world, n)
@@ -597,31 +611,42 @@ def run_rank(rank, world, local_rank, args):
     entries, mask = table.snapshot()
     ctx = pa.RxContext(dev)
     ctx.set_conn_table(table)
-    # R distinct batches per rank; batch b of rank r holds global frames [(b*world + r)*n, +n)
+    # R resident batches per rank, rotated over by the timed steps.  N=1: batch b holds global frames
+    # [b*n, (b+1)*n) (distinct content).  N>1: batch 0 is this rank's index shard, generated on the
+    # host; batches 1.. are device copies of it at other HBM addresses (a 4-GiB batch is ~16x the
+    # memory-side cache, so a copy is as cold as new content), so every timed batch is the rank's own
+    # shard and is gated against that shard's committed digest.
+    firsts = [b * n if world == 1 else lo for b in range(R)]
     frames_b, wires = [], []
     host = np.empty((n, STRIDE), dtype=np.uint8)
     slots = None
     for b in range(R):
-        first = (b * world + rank) * n if R > 1 else lo
-        pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=first, threads=gen_threads, out=host)
+        if world > 1 and b > 0:
+            frames_b.append(frames_b[0].clone())
+            wires.append(wires[0])
+            continue
+        pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=firsts[b], threads=gen_threads, out=host)
         wires.append(pa.wire_bytes(host, STRIDE, FRAME_OFF, n))
         frames_b.append(torch.from_numpy(host.reshape(-1)).to(f"cuda:{dev}"))
         if b == 0:
-            slots = host.copy()  # batch 0 stays on the host: oracle check, CPU baseline, e2e leg
+            # N=1 keeps batch 0 on the host (CPU baseline, e2e legs); N>1 ranks keep only the rows
+            # the in-run oracle check reads
+            slots = host.copy() if world == 1 else host[: min(n, 4096)].copy()
     del host
     frames = frames_b[0]
-    log(f"[rank {rank}] device {dev}: generated {R} x {n} frames ({sum(wires) / 1e9:.2f} GB wire) in "
-        f"{time.perf_counter() - t0:.1f}s")
+    log(f"[rank {rank}] device {dev}: C{cfg} shard [{lo}, {lo + n}), {R} x {n} frames "
+        f"({sum(wires) / 1e9:.2f} GB wire) in {time.perf_counter() - t0:.1f}s")
 
     res = torch.empty(n * 16, dtype=torch.uint8, device=f"cuda:{dev}")
     stream = torch.cuda.current_stream()
 
-    # correctness gate on the measured configuration, every batch: rank 0's batch 0 holds global
-    # frames [0, n) — its records' sha256 must equal the committed full-size digest (made by the
-    # oracle); every batch on every rank must satisfy the workload's invariants; and the first 4096
-    # records of batch 0 are re-checked against the oracle in this run
+    # correctness gate on the measured configuration, on every rank: each batch's records must satisfy
+    # the workload's invariants; each batch whose global frame range has a committed digest (made by the
+    # oracle: C2/C3/C5 [0, 1 Mi), each of C4's 8 shards) must hash to it; the first 4096 records of
+    # batch 0 are re-checked against the oracle in this run
     inv_ok = True
     got0 = None
+    sha_ok, sha_gated = True, 0
     for b in range(R):
         ctx.classify(frames_b[b], STRIDE, FRAME_OFF, n, res, stream)
         torch.cuda.synchronize()
@@ -632,50 +657,54 @@ def run_rank(rank, world, local_rank, args):
             inv_ok &= bool(torch.all((flags & 0x5) == 0x5)) and bool(torch.all(off_len == (54 | (1460 << 16))))
         else:
             inv_ok &= bool(torch.all((flags & 0x4000) == 0))
+        host_rec = res.cpu().numpy()
+        gd = golden_digest(cfg, firsts[b], n)
+        if gd is not None:
+            sha_gated += 1
+            sha_ok &= hashlib.sha256(host_rec.tobytes()).hexdigest() == gd["records_sha256"]
         if b == 0:
-            got0 = res.cpu().numpy()
-    gate = {"all_batches_invariants": inv_ok}
-    if rank == 0:
-        from oracle import pyoracle as orc
+            got0 = host_rec
+    from oracle import pyoracle as orc
 
-        gd = golden_digest(cfg)
-        if gd is not None and gd["n"] == n and (R > 1 or lo == 0):
-            gate["batch0_records_sha256_matches_golden"] = hashlib.sha256(got0.tobytes()).hexdigest() == gd[
-                "records_sha256"]
-        k = min(n, 4096)
-        exp = orc.classify_batch(slots, STRIDE, FRAME_OFF, k, entries, mask, table.max_conn_cnt, threads=8)
-        gate["batch0_first_4096_vs_oracle"] = bool(np.array_equal(got0[: k * 16].view(pa.RESULT_DTYPE), exp))
-    verified = all(v for v in gate.values())
+    k = min(n, 4096)
+    exp = orc.classify_batch(slots, STRIDE, FRAME_OFF, k, entries, mask, table.max_conn_cnt, threads=8)
+    gate = {"all_batches_invariants": inv_ok, "batches_sha256_gated": f"{sha_gated}/{R}",
+            "gated_batches_sha256_match_golden": bool(sha_ok and sha_gated > 0),
+            "batch0_first_4096_vs_oracle": bool(np.array_equal(got0[: k * 16].view(pa.RESULT_DTYPE), exp))}
+    verified = all(v for v in gate.values() if isinstance(v, bool))
     if not verified:
         log(f"ERROR [rank {rank}]: correctness gate failed: {gate}")
 
     for w in range(args.warmup):
         ctx.classify(frames_b[w % R], STRIDE, FRAME_OFF, n, res, stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    # one common window (pollnet_amd.shard.common_window): every rank opens it when the start barrier
+    # releases and closes it after the end barrier, so each rank's window covers the slowest rank's last
+    # launch; value = all ranks' bytes / the max over ranks of that window
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(args.steps):
-        ctx.classify(frames_b[k % R], STRIDE, FRAME_OFF, n, res, stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    wall = t1 - t0
+
+    def timed_steps():
+        ev0.record(stream)
+        for k in range(args.steps):
+            ctx.classify(frames_b[k % R], STRIDE, FRAME_OFF, n, res, stream)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+
+    wall_max, own_max = common_window(timed_steps, dist if world > 1 else None)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     step_wire = float(sum(wires[k % R] for k in range(args.steps)))  # this rank's wire bytes over the K steps
-    total_wire, wall_max, kern_ms_max, all_verified = step_wire, wall, kern_ms, verified
+    total_wire, kern_ms_max, all_verified = step_wire, kern_ms, verified
+    gates = [gate]
     if world > 1:
-        t = torch.tensor([wall, kern_ms, 0.0 if verified else 1.0], dtype=torch.float64)
+        t = torch.tensor([kern_ms, 0.0 if verified else 1.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall_max, kern_ms_max, all_verified = float(t[0]), float(t[1]), float(t[2]) == 0.0
+        kern_ms_max, all_verified = float(t[0]), float(t[1]) == 0.0
         w = torch.tensor([step_wire], dtype=torch.float64)
         dist.all_reduce(w, op=dist.ReduceOp.SUM)
         total_wire = float(w[0])
+        gates = [None] * world
+        dist.all_gather_object(gates, {"shard": [lo, lo + n], **gate})
     total_frames = n * world * args.steps
     gbit = total_wire * 8 / wall_max / 1e9
     mfps = total_frames / wall_max / 1e6
@@ -707,7 +736,11 @@ def run_rank(rank, world, local_rank, args):
                        "coordination": "gloo (host): start/stop barrier, max/sum of the timing" if world > 1 else
                        "single process"},
             "verified_vs_oracle": bool(all_verified),
-            "correctness_gate": gate,
+            "correctness_gate": gate if world == 1 else {"every_rank_verified": bool(all_verified),
+                                                        "ranks": gates},
+            "timing": ("one common window: max over ranks of start barrier -> end barrier (the end barrier inside "
+                       "the window)" if world > 1 else "wall clock around the K launches + device sync"),
+            "rank_own_wall_ms_max": round(own_max * 1e3, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
@@ -756,7 +789,7 @@ def run_rank(rank, world, local_rank, args):
             out["e2e_pinned_host"] = {"error": str(ex)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(slots, n, entries, mask, table.max_conn_cnt, args.cpu_seconds,
-                                           gpu_records=got0 if (R > 1 or lo == 0) else None)
+                                           gpu_records=got0)
     if rank == 0:
         if "WORLD_SIZE" not in os.environ or os.environ.get("PN_BENCH_SPAWNED") == "1":
             assert out["n_gpus"] == args.gpus, (out["n_gpus"], args.gpus)

@@ -126,7 +126,10 @@ uint32_t pn_table_size(const pn_conn_table* t); /* getTblSize() (Core.h:564) */
 uint32_t pn_table_repairs(const pn_conn_table* t);
 
 /* ======================= device context =======================
- * One ctx per (host thread, device).  Owns the device copy of the conn table. */
+ * One ctx per (host thread, device).  Owns the device copy of the conn table.
+ * Streams: every launch call takes the caller's stream; the ctx keeps that handle until its
+ * next pn_set_conn_table or pn_sync returns, so a stream passed to a launch call must stay
+ * valid until then (pn_close touches no stream handle). */
 typedef struct pn_ctx pn_ctx;
 
 int pn_open(int device, pn_ctx** out);
@@ -134,11 +137,14 @@ void pn_close(pn_ctx* ctx);
 const char* pn_last_error(const pn_ctx* ctx); /* ctx may be NULL: last global error */
 int pn_device_count(int* n);
 
-/* Snapshot the conn table into device memory (synchronous H2D, ≤160 KiB for
- * 1024+1024 conns).  `entries` is host memory laid out as pn_conn_entry[n].
- * Waits first for the device's work in flight (hipDeviceSynchronize; classify
- * launches may be on any stream), so a launch in flight always sees the snapshot it
- * was issued against.  A control-plane call: the launch path records nothing. */
+/* Snapshot the conn table into device memory (H2D on the ctx's own stream, <=160 KiB for
+ * 1024+1024 conns; returns when the copy is done).  `entries` is host memory laid out as
+ * pn_conn_entry[n].  Double-buffered: the snapshot goes to the buffer no launch is reading
+ * now, so launches already issued (on any stream, running or queued) keep the snapshot they
+ * were issued against, and launches issued after this returns see the new one.  It waits
+ * only for the launches issued before the PREVIOUS set (by events recorded then; normally long
+ * done) — never for the device, other streams or other contexts.  The launch path records
+ * nothing. */
 int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entries, uint64_t tbl_mask,
                       uint32_t max_conn_cnt);
 
@@ -221,7 +227,8 @@ int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint
  * Layout as pn_classify (frames in device memory or pinned host memory read and patched in
  * place, 16-byte aligned; SendBuf slots: frame_off = 14, slot_stride = SendBufSize,
  * Core.h:147-156, 232).  Asynchronous.  Up to 65,536 frames one launch; above, two (the
- * fields through ctx scratch). */
+ * fields through ctx scratch; a two-launch call on another stream than the
+ * previous one is ordered after it on the device). */
 #define PN_TX_TCP 0u
 #define PN_TX_UDP_EFVI 1u
 #define PN_TX_UDP 2u
@@ -236,7 +243,8 @@ int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_o
  * The same arguments as pn_classify (strided slots) / pn_tx_fill, plus: n in
  * [1, PN_NOTIFY_MAX_FRAMES] (every workgroup makes its stores system-visible, which only pays
  * off for small batches).  The per-ctx counter behind the word is reused: a notify call on
- * another stream than the previous one of the same kind first waits for the device.
+ * another stream than the previous one of the same kind is ordered after it on the device
+ * (an event and hipStreamWaitEvent; the host does not wait).
  * Replaces the completion step of the reference's poll (ef_eventq_poll's RX/TX events,
  * Core.h:496-498): the host learns the batch is done from one memory word. */
 #define PN_NOTIFY_MAX_FRAMES 1024u
@@ -245,7 +253,9 @@ int pn_classify_notify(pn_ctx* ctx, const void* frames, uint32_t slot_stride, ui
 int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                       const uint16_t* lens, uint32_t mode, void* stream, uint32_t* done_word, uint32_t token);
 
-/* Wait for the last stream used by this ctx. */
+/* Wait until every launch this ctx issued (on any stream) has finished: synchronizes each
+ * stream launched on since the last pn_set_conn_table, and the events that set recorded
+ * for the launches before it.  Not a device-wide wait. */
 int pn_sync(pn_ctx* ctx);
 
 /* ======================= synthetic frame generator =======================

@@ -31,6 +31,11 @@ int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint3
 int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
                            int store_bytes, void* sink_dev, void* stream);
 
+/* Test helper (no ctx): holds `stream` with one lane until the host stores non-zero to *go_host
+ * or max_ms (<= 10000) pass, then stores 1 (released) / 2 (timed out) to *done_host; both in
+ * pinned host memory.  Unrelated work in flight on a foreign stream (tests/test_gpu_notify.py). */
+int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max_ms, void* stream);
+
 /* ---- A/B variants (make TUNING=1; ids documented at their definitions) ---- */
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                         void* results_dev, void* stream, int variant);

@@ -77,13 +77,19 @@ int pn_open(int device, pn_ctx** out) {
 
 void pn_close(pn_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->tbl_dev || ctx->tx_patch || ctx->sig_count) {
-    (void)hipSetDevice(ctx->device);
-    (void)pn_internal::wait_table_readers(ctx); // also covers the last tx_fill's patch scratch
-    if (ctx->tbl_dev) (void)hipFree(ctx->tbl_dev);
-    if (ctx->tx_patch) (void)hipFree(ctx->tx_patch);
-    if (ctx->sig_count) (void)hipFree(ctx->sig_count);
-  }
+  (void)hipSetDevice(ctx->device);
+  // teardown: every launch that may still read ctx memory has finished.  A device-wide wait, so
+  // that no stream handle is touched (the caller may have destroyed its streams already)
+  if (ctx->tbl_buf[0] || ctx->tbl_buf[1] || ctx->tx_patch || ctx->sig_count) (void)hipDeviceSynchronize();
+  for (pn_conn_entry* b : ctx->tbl_buf)
+    if (b) (void)hipFree(b);
+  if (ctx->tx_patch) (void)hipFree(ctx->tx_patch);
+  if (ctx->sig_count) (void)hipFree(ctx->sig_count);
+  for (hipEvent_t ev : ctx->retired)
+    if (ev) (void)hipEventDestroy(ev);
+  for (pn_fence* f : {&ctx->sig[0], &ctx->sig[1], &ctx->tx})
+    if (f->ev) (void)hipEventDestroy(f->ev);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   delete ctx;
 }
 
@@ -96,22 +102,33 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
     return set_err(ctx, PN_EINVAL, "pn_set_conn_table: tbl_mask must be 2^k-1 < n_entries");
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  // classify launches on this ctx (any stream) may still be reading the table: let them
-  // finish before the snapshot is replaced (the copy below is not ordered against them).
-  // Waiting here, not recording an event per launch, keeps the launch path free
-  if (ctx->tbl_dev) {
-    const int rc = pn_internal::wait_table_readers(ctx);
-    if (rc) return rc;
-  }
-  if (n_entries > ctx->n_entries) {
-    if (ctx->tbl_dev) (void)hipFree(ctx->tbl_dev);
-    ctx->tbl_dev = nullptr;
-    ctx->n_entries = 0;
-    e = hipMalloc(&ctx->tbl_dev, (size_t)n_entries * sizeof(pn_conn_entry));
+  // the snapshot goes to the buffer launches are NOT reading now; its own readers (launches
+  // issued before the previous set) are waited for by event — normally long done — and the
+  // launches reading the current buffer, on any stream, keep running untouched
+  int rc = pn_internal::wait_retired(ctx);
+  if (rc) return rc;
+  const int nxt = ctx->tbl_dev ? ctx->cur ^ 1 : ctx->cur;
+  if (n_entries > ctx->tbl_cap[nxt]) {
+    if (ctx->tbl_buf[nxt]) (void)hipFree(ctx->tbl_buf[nxt]);
+    ctx->tbl_buf[nxt] = nullptr;
+    ctx->tbl_cap[nxt] = 0;
+    e = hipMalloc(&ctx->tbl_buf[nxt], (size_t)n_entries * sizeof(pn_conn_entry));
     if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(conn table)");
+    ctx->tbl_cap[nxt] = n_entries;
   }
-  e = hipMemcpy(ctx->tbl_dev, entries, (size_t)n_entries * sizeof(pn_conn_entry), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpy(conn table)");
+  if (!ctx->copy_stream) {
+    e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamCreate(table uploads)");
+  }
+  e = hipMemcpyAsync(ctx->tbl_buf[nxt], entries, (size_t)n_entries * sizeof(pn_conn_entry), hipMemcpyHostToDevice,
+                     ctx->copy_stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->copy_stream);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpyAsync(conn table)");
+  // everything launched so far reads (at most) the buffer being retired: mark its end
+  rc = pn_internal::retire_streams(ctx);
+  if (rc) return rc;
+  ctx->cur = nxt;
+  ctx->tbl_dev = ctx->tbl_buf[nxt];
   ctx->n_entries = n_entries;
   ctx->mask = tbl_mask;
   ctx->max_conn = max_conn_cnt;
@@ -132,7 +149,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   launch_strided<false>(a, frame_off, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
@@ -153,7 +170,7 @@ int pn_classify_notify(pn_ctx* ctx, const void* frames, uint32_t slot_stride, ui
   launch_strided<true>(a, frame_off, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (notify) launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
@@ -196,15 +213,23 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
 int pn_sync(pn_ctx* ctx) {
   if (!ctx) return set_err(nullptr, PN_EINVAL, "pn_sync: ctx is NULL");
   hipError_t e = hipSetDevice(ctx->device);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->last_stream);
-  if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize");
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  // every stream launched on since the last set, and (by event) everything before it
+  for (hipStream_t s : ctx->streams) {
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize");
+  }
+  ctx->streams.clear();
+  int rc = pn_internal::wait_retired(ctx);
+  if (rc) return rc;
+  for (pn_fence* f : {&ctx->sig[0], &ctx->sig[1], &ctx->tx}) f->state = 0;
   return PN_OK;
 }
 

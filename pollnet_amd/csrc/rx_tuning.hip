@@ -20,6 +20,23 @@ __global__ __launch_bounds__(256) void calib_stream_read_kernel(const u32x4* src
   if (acc == 0x9E3779B9u) sink[blockIdx.x] = acc; // keeps the loads live; practically never stores
 }
 
+// Test helper: one lane holds its stream until the host stores non-zero to *go (pinned host
+// memory) or max_ticks of the device wall clock pass (always exits), then stores 1 (released)
+// or 2 (timed out) to *done.  Stands for unrelated work in flight on a foreign stream.
+__global__ __launch_bounds__(64) void spin_wait_kernel(const uint32_t* go, uint32_t* done, uint64_t max_ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  uint32_t r = 2;
+  while (wall_clock64() - t0 < max_ticks) {
+    if (__hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+      r = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(8);
+  }
+  __hip_atomic_store(done, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Read-only ceilings for the slot layout (no header work, no arithmetic): each wave
 // streams the first `bytes` of each of its 64 slots with the RX kernel's 1-KiB
 // buffer loads, 8 slots per batch.  STORE = 16 / 8: plus a per-slot record store
@@ -183,7 +200,7 @@ int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* o
   else launch_one<0, 0, kProdAbl, kLoadAux, kStoreAux, 1, kLoadAux, 1, 0>(a, s);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "indexed variant launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
@@ -247,7 +264,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "variant launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
@@ -275,7 +292,7 @@ int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint3
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "calib slot launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
@@ -298,10 +315,23 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
     hipLaunchKernelGGL((calib_slot_read_var_kernel<0>), dim3(waves), dim3(64), 0, s, src, n_slots, stride, lens, sink);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "calib slot var launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
+
+int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max_ms, void* stream) {
+  if (!go_host || !done_host || max_ms == 0 || max_ms > 10000)
+    return set_err(nullptr, PN_EINVAL, "pn_test_spin_wait: go/done must be set, max_ms in [1, 10000]");
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess || khz <= 0) return hip_err(nullptr, e, "wall clock rate");
+  hipLaunchKernelGGL(spin_wait_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, go_host, done_host,
+                     (uint64_t)khz * max_ms);
+  e = hipGetLastError();
+  return e == hipSuccess ? PN_OK : hip_err(nullptr, e, "spin_wait launch");
+}
 
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream) {
   if (!ctx || !src_dev || !sink_dev || (bytes & 15) || ((uintptr_t)src_dev & 15))
@@ -312,7 +342,7 @@ int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void*
                      bytes / 16, (uint32_t*)sink_dev);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "calib launch");
-  ctx->last_stream = (hipStream_t)stream;
+  pn_internal::note_stream(ctx, (hipStream_t)stream);
   return PN_OK;
 }
 

@@ -106,6 +106,6 @@ extern "C" int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_s
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "match_streams launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }

@@ -328,29 +328,24 @@ inline int check_args(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
   return PN_OK;
 }
 
-// ctx-owned patch scratch, grown on demand.  A call on a different stream than the last
-// TX call first waits for that one (the scratch is reused).
+// ctx-owned patch scratch, grown on demand.  A call on another stream than the previous
+// scratch user is ordered after it on the device (pn_fence: no per-launch event, no host wait);
+// growing it waits on the host for that user before the old scratch is freed.
 inline int ensure_patch(pn_ctx* ctx, uint32_t n, hipStream_t s) {
-  hipError_t e;
-  if (ctx->tx_patch && ctx->tx_stream != s) {
-    e = hipStreamSynchronize(ctx->tx_stream);
-    if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(last tx_fill)");
-  }
   if (n > ctx->tx_patch_n) {
     if (ctx->tx_patch) {
-      e = hipStreamSynchronize(ctx->tx_stream);
-      if (e != hipSuccess) return hip_err(ctx, e, "hipStreamSynchronize(last tx_fill)");
+      const int rc = pn_internal::fence_host_wait(ctx, ctx->tx);
+      if (rc) return rc;
       (void)hipFree(ctx->tx_patch);
       ctx->tx_patch = nullptr;
       ctx->tx_patch_n = 0;
     }
     const uint32_t cap = n < (1u << 16) ? (1u << 16) : n;
-    e = hipMalloc(&ctx->tx_patch, (size_t)cap * sizeof(uint2));
+    hipError_t e = hipMalloc(&ctx->tx_patch, (size_t)cap * sizeof(uint2));
     if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(tx patch scratch)");
     ctx->tx_patch_n = cap;
   }
-  ctx->tx_stream = s;
-  return PN_OK;
+  return pn_internal::fence_use(ctx, ctx->tx, s);
 }
 
 } // namespace

@@ -40,7 +40,7 @@ extern "C" int pn_tx_fill(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint3
   else launch_mode<PN_TX_UDP>(a, mis, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "tx_fill launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 
@@ -69,6 +69,6 @@ extern "C" int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride
   else launch_mis<PN_TX_UDP, 0, true>(a, mis, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "tx_fill (notify) launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }

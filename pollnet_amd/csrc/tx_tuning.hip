@@ -98,7 +98,7 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
   if (rc) return set_err(ctx, PN_EINVAL, "tx variant: unknown");
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "tx variant launch");
-  ctx->last_stream = s;
+  pn_internal::note_stream(ctx, s);
   return PN_OK;
 }
 #endif // PN_TUNING_VARIANTS

@@ -217,6 +217,15 @@ def _ptr(x):
     raise TypeError(f"cannot take the address of {type(x)}")
 
 
+def _hold(ctx, stream):
+    """Keep a torch stream alive while the ctx may still use its handle (include/pollnet_amd.h:
+    until the next pn_set_conn_table / pn_sync)."""
+    h = _stream_handle(stream)
+    if h is not None and not isinstance(stream, int) and h not in ctx._held:
+        ctx._held[h] = stream
+    return h
+
+
 def _stream_handle(stream):
     if stream is None:
         return None
@@ -234,6 +243,9 @@ class RxContext:
         self._h = h
         self.device = device
         self.max_conn_cnt = 0
+        # handle -> stream object of the streams launched on since the last set / sync: the C-ABI
+        # keeps those handles until then
+        self._held = {}
 
     def close(self):
         if getattr(self, "_h", None):
@@ -252,11 +264,12 @@ class RxContext:
             _pn_set_conn_table(self._h, entries.ctypes.data, len(entries), mask, max_conn_cnt), self._h, "pn_set_conn_table"
         )
         self.max_conn_cnt = max_conn_cnt
+        self._held.clear()
 
     def classify(self, frames_dev, slot_stride: int, frame_off: int, n: int, results_dev, stream=None):
         """Asynchronous launch on `stream` (torch.cuda.Stream, raw handle, or None = null stream)."""
         _check(
-            _pn_classify(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(results_dev), _stream_handle(stream)),
+            _pn_classify(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(results_dev), _hold(self, stream)),
             self._h,
             "pn_classify",
         )
@@ -266,20 +279,20 @@ class RxContext:
         """pn_classify_notify: as classify (n <= PN_NOTIFY_MAX_FRAMES), and the launch stores
         `token` to the u32 at done_word (pinned host memory) once every record is visible."""
         _check(_pn_classify_notify(self._h, _ptr(frames), slot_stride, frame_off, n, _ptr(results),
-                                   _stream_handle(stream), _ptr(done_word), token), self._h, "pn_classify_notify")
+                                   _hold(self, stream), _ptr(done_word), token), self._h, "pn_classify_notify")
 
     def tx_fill_notify(self, frames, slot_stride: int, frame_off: int, n: int, done_word, token: int, lens=None,
                        mode: int = PN_TX_TCP, stream=None):
         """pn_tx_fill_notify: as tx_fill (n <= PN_NOTIFY_MAX_FRAMES) with the completion word."""
         _check(_pn_tx_fill_notify(self._h, _ptr(frames), slot_stride, frame_off, n, _ptr(lens), mode,
-                                  _stream_handle(stream), _ptr(done_word), token), self._h, "pn_tx_fill_notify")
+                                  _hold(self, stream), _ptr(done_word), token), self._h, "pn_tx_fill_notify")
 
     def classify_indexed(self, base, offsets, eth_mod16: int, n: int, avail: int, results, stream=None):
         """Frames at base + offsets[i] (u64; device or pinned host memory), all with
         offsets[i] % 16 == eth_mod16; asynchronous on `stream`."""
         _check(
             _pn_classify_indexed(self._h, _ptr(base), _ptr(offsets), eth_mod16, n, avail, _ptr(results),
-                                 _stream_handle(stream)),
+                                 _hold(self, stream)),
             self._h,
             "pn_classify_indexed",
         )
@@ -292,7 +305,7 @@ class RxContext:
         frame, optional) sets tot_len first, as setOptDataLen / update_udp_pkt do.
         Asynchronous on `stream`."""
         _check(_pn_tx_fill(self._h, _ptr(frames_dev), slot_stride, frame_off, n, _ptr(lens), mode,
-                           _stream_handle(stream)), self._h, "pn_tx_fill")
+                           _hold(self, stream)), self._h, "pn_tx_fill")
 
     def match_streams(self, frames, slot_stride: int, frame_off: int, n: int, filters: np.ndarray, stream_ids,
                       stream=None):
@@ -300,10 +313,12 @@ class RxContext:
         (STREAM_FILTER_DTYPE, host array) frame i passes, PN_NO_STREAM if none."""
         flt = np.ascontiguousarray(filters, dtype=STREAM_FILTER_DTYPE)
         _check(_pn_match_streams(self._h, _ptr(frames), slot_stride, frame_off, n, flt.ctypes.data, len(flt),
-                                 _ptr(stream_ids), _stream_handle(stream)), self._h, "pn_match_streams")
+                                 _ptr(stream_ids), _hold(self, stream)), self._h, "pn_match_streams")
 
     def sync(self):
+        """pn_sync: every stream this ctx launched on has drained."""
         _check(_pn_sync(self._h), self._h, "pn_sync")
+        self._held.clear()
 
 
 @dataclass

@@ -32,6 +32,7 @@ def _sig(name, res, *args):
 _calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
 _calib_slot_var = _sig("pn_calib_slot_read_var", _i32, _vp, _vp, _u32, _u32, _vp, _i32, _vp, _vp)
+_spin = _sig("pn_test_spin_wait", _i32, _vp, _vp, _u32, _vp)
 _variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _tx_variant = _sig("pn_tx_fill_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _i32, _vp)
@@ -59,6 +60,13 @@ def calib_slot_read_var(ctx, src_dev, n_slots, stride, lens_dev, sink_dev, strea
     """The same over each frame's own lines (lens_dev: u32 per slot)."""
     rx._check(_calib_slot_var(ctx._h, rx._ptr(src_dev), n_slots, stride, rx._ptr(lens_dev), store_bytes,
                               rx._ptr(sink_dev), rx._stream_handle(stream)), ctx._h, "pn_calib_slot_read_var")
+
+
+def spin_wait(go_host, done_host, max_ms: int, stream=None):
+    """Test helper: hold `stream` until go_host[0] != 0 (pinned u32) or max_ms pass; then
+    done_host[0] = 1 (released) or 2 (timed out).  Uses no ctx."""
+    rx._check(_spin(rx._ptr(go_host), rx._ptr(done_host), max_ms, rx._stream_handle(stream)), None,
+              "pn_test_spin_wait")
 
 
 def classify_variant(ctx, frames_dev, slot_stride, frame_off, n, results_dev, stream, variant):

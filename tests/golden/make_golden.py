@@ -8,7 +8,13 @@
   config_slices.npz per BASELINE config C2..C5: sha256 of the first 4096 generated
                     slots and of the conn table, and the oracle's records for them.
   full_digests.json sha256 of the oracle's records over the full BASELINE batch
-                    (C2, C3, C5: 1,048,576 frames; C4 shard 0 of 8: 2,097,152).
+                    (C2, C3, C5: 1,048,576 frames; C4 shard 0 of 8: 2,097,152),
+                    and "c4_shards": each of C4's 8 index shards (2,097,152 frames
+                    each, global frames [r*2Mi, (r+1)*2Mi)), so every rank of an
+                    N<=8 bench run gates its own shard.
+                    "c2_shards": C2's frames [1Mi, 4Mi) in 3 batches (the N=1 bench's
+                    rotating batches 1-3).  `python make_golden.py shards` refreshes
+                    only these two keys.
 
 The oracle is pinned by known_answers.json, loopback_frames.npz and oracle/_ref
 (tests/test_oracle.py); these fixtures then pin the product against it.
@@ -115,8 +121,64 @@ def digest(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def records_digest(cfg, first, n, threads):
+    """sha256 of the oracle's records over global frames [first, first+n) of config cfg,
+    generated in 256K-frame chunks; also the wire bytes and the per-flag-bit counts."""
+    p = pa.rx.GenParams.for_config(cfg)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    chunk = min(n, 1 << 18)
+    h = hashlib.sha256()
+    wire = 0
+    flags_hist = np.zeros(16, np.int64)
+    buf = np.empty((chunk, STRIDE), np.uint8)
+    for lo in range(0, n, chunk):
+        pa.gen_frames(p, chunk, STRIDE, FRAME_OFF, first_index=first + lo, threads=threads, out=buf)
+        rr = orc.classify_batch(buf, STRIDE, FRAME_OFF, chunk, e, m, t.max_conn_cnt, threads=threads)
+        h.update(rr.tobytes())
+        wire += pa.wire_bytes(buf, STRIDE, FRAME_OFF, chunk)
+        for bit in range(14):
+            flags_hist[bit] += int(((rr["flags"] >> bit) & 1).sum())
+    return {"n": n, "records_sha256": h.hexdigest(), "wire_bytes": wire, "flag_bit_counts": flags_hist[:14].tolist(),
+            "seed": p.seed}
+
+
+C4_SHARDS, C4_SHARD_N = 8, 1 << 21  # BASELINE configs[3]: 16 Mi frames over 8 GPUs
+
+
+def c4_shards(threads):
+    out = []
+    for r in range(C4_SHARDS):
+        d = records_digest(4, r * C4_SHARD_N, C4_SHARD_N, threads)
+        d["first_index"] = r * C4_SHARD_N
+        out.append(d)
+        print(f"c4 shard {r}: {d['records_sha256'][:16]} wire={d['wire_bytes']}")
+    return out
+
+
+def c2_batches(threads):
+    """C2 global frames [b*1Mi, (b+1)*1Mi), b = 1..3: the bench's N=1 rotating batches 1-3
+    (batch 0 is the "c2" entry), so every timed batch is gated."""
+    out = []
+    for b in range(1, 4):
+        d = records_digest(2, b << 20, 1 << 20, threads)
+        d["first_index"] = b << 20
+        out.append(d)
+        print(f"c2 batch {b}: {d['records_sha256'][:16]}")
+    return out
+
+
 def main():
     threads = min(16, os.cpu_count() or 1)
+    if sys.argv[1:] == ["shards"]:
+        path = os.path.join(HERE, "full_digests.json")
+        with open(path) as f:
+            full = json.load(f)
+        full["c4_shards"] = c4_shards(threads)
+        full["c2_shards"] = c2_batches(threads)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1)
+        return
     # ---- edge frames, classified against the C5 table (1024 conns, 32 TW, adversarial run) ----
     p5 = pa.rx.GenParams.for_config(5)
     table = pa.gen_conn_table(p5)
@@ -151,21 +213,10 @@ def main():
         slices[f"c{cfg}_mask"] = m
         slices[f"c{cfg}_expected"] = r
         # full-size digest, generated in 256K-frame chunks
-        n, chunk = FULL[cfg], 1 << 18
-        h = hashlib.sha256()
-        wire = 0
-        flags_hist = np.zeros(16, np.int64)
-        buf = np.empty((chunk, STRIDE), np.uint8)
-        for lo in range(0, n, chunk):
-            pa.gen_frames(p, chunk, STRIDE, FRAME_OFF, first_index=lo, threads=threads, out=buf)
-            rr = orc.classify_batch(buf, STRIDE, FRAME_OFF, chunk, e, m, t.max_conn_cnt, threads=threads)
-            h.update(rr.tobytes())
-            wire += pa.wire_bytes(buf, STRIDE, FRAME_OFF, chunk)
-            for bit in range(14):
-                flags_hist[bit] += int(((rr["flags"] >> bit) & 1).sum())
-        full[f"c{cfg}"] = {"n": n, "records_sha256": h.hexdigest(), "wire_bytes": wire,
-                           "flag_bit_counts": flags_hist[:14].tolist(), "seed": p.seed}
-        print(f"c{cfg}: n={n} wire={wire} flags={flags_hist[:14].tolist()}")
+        full[f"c{cfg}"] = records_digest(cfg, 0, FULL[cfg], threads)
+        print(f"c{cfg}: {full[f'c{cfg}']}")
+    full["c4_shards"] = c4_shards(threads)
+    full["c2_shards"] = c2_batches(threads)
     np.savez_compressed(os.path.join(HERE, "config_slices.npz"), **slices)
     with open(os.path.join(HERE, "full_digests.json"), "w") as f:
         json.dump(full, f, indent=1)

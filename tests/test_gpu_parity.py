@@ -324,8 +324,8 @@ def test_side_stream_and_sync(torch_cuda, ctx):
 
 def test_table_replaced_while_classify_in_flight(torch_cuda):
     """pn_set_conn_table right after classify launches on two side streams (and a TX fill on
-    a third, which becomes the ctx's last stream): every launch still sees the snapshot it
-    was issued against -- the replacement waits for the device, the launches record nothing."""
+    a third): every launch still sees the snapshot it was issued against -- the replacement
+    goes to the other table buffer, the launches record nothing."""
     torch = torch_cuda
     c = pa.RxContext(0)
     p = pa.rx.GenParams.for_config(3)

@@ -77,6 +77,89 @@ def test_two_rank_shards_match_single_process(tmp_path, cfg):
     assert wire == float(pa.wire_bytes(full, 2048, 2, world * n))
 
 
+def _window_worker(rank, world, port, flag, out_dir):
+    """Rank 1's work cannot start until rank 0's is done (a file flag): the two ran one after the
+    other, so the common window must cover both (>= 0.4 s), while each rank's own body is ~0.2 s
+    of work plus, on rank 1, the wait."""
+    import time
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from pollnet_amd.shard import common_window
+
+    def body():
+        if rank == 1:
+            while not os.path.exists(flag):
+                time.sleep(0.005)
+        time.sleep(0.2)
+        if rank == 0:
+            open(flag, "w").close()
+
+    wall, own = common_window(body, dist)
+    with open(os.path.join(out_dir, f"win{rank}.txt"), "w") as f:
+        f.write(f"{wall} {own}")
+    dist.destroy_process_group()
+
+
+def test_common_window_covers_serialised_ranks(tmp_path):
+    """bench.py's aggregate timing (shard.common_window): ranks that ran one after another cannot
+    look parallel — every rank reports the same max window, and it spans both ranks' work."""
+    world = 2
+    mp.spawn(_window_worker, args=(world, _free_port(), str(tmp_path / "flag"), str(tmp_path)), nprocs=world,
+             join=True)
+    res = [tuple(map(float, open(tmp_path / f"win{r}.txt").read().split())) for r in range(world)]
+    assert res[0] == res[1]  # max over ranks, identical everywhere
+    wall, own = res[0]
+    assert wall >= 0.4 and own >= 0.4 and wall >= own
+
+
+def test_common_window_single_process():
+    import time
+
+    from pollnet_amd.shard import common_window
+
+    wall, own = common_window(lambda: time.sleep(0.05), None)
+    assert 0.05 <= own <= wall < 1.0
+
+
+def test_bench_golden_covers_every_c4_shard_and_c2_batch():
+    """The N>1 bench gates each rank's C4 shard (8 shards of 2 Mi = BASELINE configs[3]) and the N=1
+    bench every rotating C2 batch against a committed oracle digest (tests/golden/make_golden.py)."""
+    import importlib.util
+    import sys
+
+    sys.path.insert(0, ROOT)
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for r in range(8):
+        d = bench.golden_digest(4, r << 21, 1 << 21)
+        assert d is not None and d["wire_bytes"] == (1 << 21) * 1514
+    assert bench.golden_digest(4, 0, 1 << 21)["records_sha256"] == bench.golden_digest(4)["records_sha256"]
+    for b in range(4):
+        assert bench.golden_digest(2, b << 20, 1 << 20) is not None
+    assert bench.golden_digest(4, 8 << 21, 1 << 21) is None and bench.golden_digest(4, 0, 4096) is None
+
+
+def test_c4_shard_digest_regenerates():
+    """One C4 shard (shard 5) recomputed here by generator + oracle equals the committed digest."""
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    sys.path.insert(0, ROOT)
+    import make_golden
+
+    with open(os.path.join(ROOT, "tests", "golden", "full_digests.json")) as f:
+        ref = json.load(f)["c4_shards"][5]
+    got = make_golden.records_digest(4, ref["first_index"], ref["n"], threads=min(8, os.cpu_count() or 1))
+    assert got["records_sha256"] == ref["records_sha256"] and got["wire_bytes"] == ref["wire_bytes"]
+
+
 def test_shard_ranges():
     from pollnet_amd.shard import shard_range, split_range
 
@@ -150,13 +233,16 @@ def test_bench_spawns_ranks_itself():
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
     assert line["config"]["global_frames"] == 2 * 65536
+    assert line["config"]["workload"].startswith("C4")  # N>1 defaults to BASELINE configs[3]
 
 
 @pytest.mark.gpu
 def test_bench_under_the_drivers_torchrun_command():
     """The driver's own N>1 launch (`python -m torch.distributed.run --nnodes=1 --nproc-per-node N
     --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...`), N = 2 on this box's GPU:
-    rank 0 alone prints one JSON line, n_gpus 2, the aggregate over both ranks."""
+    rank 0 alone prints one JSON line, n_gpus 2, the aggregate over both ranks.  Full C4 shards
+    (2 Mi frames per rank, BASELINE configs[3]): each rank sha256-gates both of its batches against
+    its own shard's committed digest."""
     import json
     import socket
     import subprocess
@@ -167,7 +253,7 @@ def test_bench_under_the_drivers_torchrun_command():
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
-           "--warmup", "1", "--frames", "65536", "--batches", "2", "--no-cpu-baseline", "--no-e2e", "--no-secondary"]
+           "--warmup", "1", "--batches", "2", "--no-cpu-baseline", "--no-e2e", "--no-secondary"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -175,5 +261,10 @@ def test_bench_under_the_drivers_torchrun_command():
     assert len(lines) == 1, p.stdout[-2000:]
     line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["verified_vs_oracle"] is True
-    assert line["config"]["global_frames"] == 2 * 65536
+    assert line["config"]["workload"].startswith("C4") and line["config"]["global_frames"] == 2 * (1 << 21)
+    ranks = line["correctness_gate"]["ranks"]
+    assert [g["shard"] for g in ranks] == [[0, 1 << 21], [1 << 21, 2 << 21]]
+    for g in ranks:
+        assert g["batches_sha256_gated"] == "2/2" and g["gated_batches_sha256_match_golden"] is True
+        assert g["all_batches_invariants"] is True and g["batch0_first_4096_vs_oracle"] is True
     assert line["value"] > 0 and line["scaling"] == "weak"
