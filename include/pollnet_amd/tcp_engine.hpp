@@ -13,8 +13,9 @@
 //     flows and unestablished connections (Derived::onMiss / Derived::onHandshake: a server's
 //     SYN accept and SYN-RECEIVED, a client's SYN-SENT), then onPack — its receive half is
 //     RxConn (rx_conn.hpp), its ACK-field / send half is here;
-//   - every frame the poll built gets its IP and TCP checksums from ONE pn_tx_fill launch
-//     over the pinned TX batch and leaves through the link in generation order.
+//   - every frame the poll built gets its IP and TCP checksums — from ONE pn_tx_fill launch
+//     over the pinned TX batch when it carries enough payload (TxGpuMinDataFrames), else on the
+//     host (header-only ACKs: nanoseconds each) — and leaves through the link in generation order.
 // The table snapshot on the device is refreshed before each classify; records after a table
 // change within the same batch are re-resolved on the host (one ordered probe), so every
 // frame sees the table the reference's sequential loop would have shown it.
@@ -67,6 +68,12 @@ PN_CONF_OPT(ConnSendBufCnt, uint32_t, 1024) // EfviTcp.h:181
 PN_CONF_OPT(RxBatch, uint32_t, 512)         // frames per poll (RecvBufCnt = 512, EfviTcp.h:186)
 PN_CONF_OPT(RxLatencyBudgetUs, uint32_t, 0) // hold received frames up to this long for a fuller batch
 PN_CONF_OPT(TxBatch, uint32_t, 1024)        // frames per pn_tx_fill launch
+PN_CONF_OPT(TxGpuMinDataFrames, uint32_t, 64) // a TX batch goes to pn_tx_fill when it holds at least this many
+                                            // payload-bearing frames; below, every frame of it is
+                                            // checksummed on the host (0 = always the GPU)
+PN_CONF_OPT(UseAllowNewConnection, bool, false) // consult the handler's allowNewConnection on a SYN, as
+                                            // efvitcp::TcpServer does (TcpServer.h:84); pollnet's
+                                            // EfviTcpServer wrapper never does (EfviTcp.h:270)
 PN_CONF_OPT(RxChunk, uint32_t, 0)           // frames per classify launch within a poll (0 = RxBatch): chunk
                                             // k+1 is on the GPU while chunk k is dispatched
 PN_CONF_OPT(RxPipeline, bool, false)        // throughput mode: a poll's frames are classified while the
@@ -108,6 +115,55 @@ inline void wr16(uint8_t* p, uint16_t v) {
 inline void wr32(uint8_t* p, uint32_t v) {
   wr16(p, (uint16_t)(v >> 16));
   wr16(p + 2, (uint16_t)v);
+}
+
+// One's-complement sum of n bytes taken as big-endian 16-bit words (an odd tail byte padded
+// with zero, as copyAndSum pads it, TcpConn.h:291-295), accumulated from native-order loads: the
+// folded result is the byte-swapped sum (RFC 1071 §2(B)), stored back with a native store.
+inline uint64_t csum_add(const uint8_t* p, uint32_t n, uint64_t s) {
+  for (; n >= 8; p += 8, n -= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    s += (v & 0xffffffffu) + (v >> 32);
+  }
+  if (n >= 4) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    s += v;
+    p += 4;
+    n -= 4;
+  }
+  if (n >= 2) {
+    uint16_t v;
+    std::memcpy(&v, p, 2);
+    s += v;
+    p += 2;
+    n -= 2;
+  }
+  if (n) s += p[0];
+  return s;
+}
+inline uint16_t csum_fold(uint64_t s) { // CSum::fold (Core.h:94-98), carries folded back until none
+  while (s >> 16) s = (s & 0xffff) + (s >> 16);
+  return (uint16_t)~s;
+}
+// Both checksums of a built TCP/IPv4 frame (eth = Ethernet header; 20-B IP header, as every
+// frame the engine builds): the values SendBuf::setOptDataLen folds from its cached header sums
+// (Core.h:157-163, at the end of TcpConn::sendBuf, TcpConn.h:310-323) and pn_tx_fill(PN_TX_TCP)
+// writes.  A sum over these fields is never zero (IP version, protocol 6), so the folded value
+// is unique and any correct order of summation gives the same bytes.
+inline void fill_tcp_checksums(uint8_t* eth) {
+  uint8_t* ip = eth + 14;
+  const uint32_t tot_len = rd16(ip + 2), tcp_len = tot_len - 20;
+  ip[10] = ip[11] = 0;
+  const uint16_t ip_sum = csum_fold(csum_add(ip, 20, 0));
+  std::memcpy(ip + 10, &ip_sum, 2);
+  uint8_t* tcp = ip + 20;
+  tcp[16] = tcp[17] = 0;
+  const uint16_t len_be = (uint16_t)(tcp_len >> 8 | (tcp_len & 0xff) << 8);
+  uint64_t s = csum_add(ip + 12, 8, 0x0600u + len_be); // pseudo-header: addresses, protocol 6, TCP length
+  const uint16_t tcp_sum = csum_fold(csum_add(tcp, tcp_len, s));
+  std::memcpy(tcp + 16, &tcp_sum, 2);
 }
 } // namespace srv_detail
 
@@ -401,6 +457,7 @@ class TcpEngine {
   static constexpr uint32_t kTimeWaitTimeout = 60 * 1000; // Core.h:48
   static constexpr uint32_t kRxBatch = srv_detail::opt_RxBatch<Conf>::value;
   static constexpr uint32_t kTxBatch = srv_detail::opt_TxBatch<Conf>::value;
+  static constexpr uint32_t kTxGpuMin = srv_detail::opt_TxGpuMinDataFrames<Conf>::value;
   static constexpr uint32_t kRxBudgetUs = srv_detail::opt_RxLatencyBudgetUs<Conf>::value;
   static constexpr uint32_t kRxChunk = srv_detail::opt_RxChunk<Conf>::value;
   static constexpr bool kRxPipeline = srv_detail::opt_RxPipeline<Conf>::value;
@@ -508,20 +565,29 @@ class TcpEngine {
   // Frames built since the last flush (checksums not yet filled), plus (pipelined) those whose
   // fill is still running.
   uint32_t pendingTx() const { return tx_n_ + tx_fl_n_; }
-  // Fill the pending frames' checksums (one pn_tx_fill launch) and send them in order; a
-  // pipelined batch still being filled goes first.
+  // Fill the pending frames' checksums and send them in order; a pipelined batch still being
+  // filled goes first.  A batch of at least TxGpuMinDataFrames payload-bearing frames takes one
+  // pn_tx_fill launch; a smaller one (a poll's ACKs, the odd data segment) is summed on the host,
+  // where a header-only frame costs nanoseconds and a launch ~10 us.
   const char* flushTx() {
     const char* e = completeTx();
     if (!tx_n_) return e;
-    if (const char* e2 = be_.fillTx(tx_n_, tx_cur_)) {
+    if (txOnHost()) {
+      fillTxHost(tx_cur_, tx_n_);
+    } else if (const char* e2 = be_.fillTx(tx_n_, tx_cur_)) {
       err_ = e2;
-      tx_n_ = 0;
+      tx_n_ = tx_data_n_ = 0;
       return e2;
+    } else {
+      tx_gpu_frames_ += tx_n_;
     }
     sendTx(tx_cur_, tx_n_);
-    tx_n_ = 0;
+    tx_n_ = tx_data_n_ = 0;
     return e;
   }
+  // TX frames summed on the host / filled by pn_tx_fill since init (measurement)
+  uint64_t txHostFrames() const { return tx_host_frames_; }
+  uint64_t txGpuFrames() const { return tx_gpu_frames_; }
 
  protected:
   struct Tw { // Core.h:186-197 TimeWaitConn
@@ -554,8 +620,10 @@ class TcpEngine {
       if constexpr (srv_detail::has_onRecvTimeout<Handler, Conn>::value) u.onRecvTimeout(c);
     }
     bool allow(uint32_t ip_be, uint16_t port_be) {
-      if constexpr (srv_detail::has_allowNewConnection<Handler, Conn>::value) return u.allowNewConnection(ip_be, port_be);
-      return true;
+      if constexpr (srv_detail::opt_UseAllowNewConnection<Conf>::value &&
+                    srv_detail::has_allowNewConnection<Handler, Conn>::value)
+        return u.allowNewConnection(ip_be, port_be);
+      return true; // EfviTcp.h:270: the wrapper's TmpHandler accepts every connection
     }
     uint32_t data(Conn& c, const uint8_t* d, uint32_t n) { return u.onTcpData(c, d, n); }
   };
@@ -608,7 +676,7 @@ class TcpEngine {
       c.fin_sent_ = c.fin_received_ = true;
     }
     for (uint32_t i = 0; i < kMaxTw; i++) tws_[i].timer.owner = kMaxConn + i;
-    tx_n_ = rx_pending_ = cur_ = tx_cur_ = tx_fl_n_ = 0;
+    tx_n_ = tx_data_n_ = rx_pending_ = cur_ = tx_cur_ = tx_fl_n_ = 0;
     fl_n_[0] = fl_n_[1] = 0;
     ++tver_;
     ready_ = true;
@@ -629,16 +697,27 @@ class TcpEngine {
       link_.send(f, 14 + srv_detail::rd16(f + 16));
     }
   }
+  bool txOnHost() const { return tx_data_n_ < kTxGpuMin; }
+  void fillTxHost(uint32_t half, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+      srv_detail::fill_tcp_checksums(be_.txSlots(half) + (size_t)i * Backend::kStride + Backend::kFrameOff);
+    tx_host_frames_ += n;
+  }
   // Pipelined TX: start filling the frames built so far and switch to the other batch ...
   void launchTx() {
     if (!tx_n_) return;
-    if (const char* e = be_.fillTxLaunch(tx_n_, tx_cur_)) {
+    tx_fl_host_ = txOnHost();
+    if (tx_fl_host_) {
+      fillTxHost(tx_cur_, tx_n_);
+    } else if (const char* e = be_.fillTxLaunch(tx_n_, tx_cur_)) {
       err_ = e;
-      tx_n_ = 0;
+      tx_n_ = tx_data_n_ = 0;
       return;
+    } else {
+      tx_gpu_frames_ += tx_n_;
     }
     tx_fl_n_ = tx_n_;
-    tx_n_ = 0;
+    tx_n_ = tx_data_n_ = 0;
     tx_cur_ ^= 1;
   }
   // ... and, a poll later, wait for that fill and send its frames.
@@ -646,7 +725,8 @@ class TcpEngine {
     if (!tx_fl_n_) return nullptr;
     const uint32_t n = tx_fl_n_;
     tx_fl_n_ = 0;
-    if (const char* e = be_.fillTxWait()) return err_ = e;
+    if (!tx_fl_host_)
+      if (const char* e = be_.fillTxWait()) return err_ = e;
     sendTx(tx_cur_ ^ 1, n);
     return nullptr;
   }
@@ -971,7 +1051,13 @@ class TcpEngine {
     }
   }
 
-  void sendAck(Conn& c, bool immediate) { // TcpConn.h:335-343
+  // TcpConn.h:335-343.  The reference takes the ACK's buffer from getAckBuf (TcpConn.h:851-860):
+  // a free SendBuf in [data_next, send_una + ConnSendBufCnt - 1] whose previous frame the NIC has
+  // completed (avail).  Here every frame leaves through the link at flush, so every buffer is
+  // complete, and sendPartial / sendFin keep data_next <= send_una + ConnSendBufCnt - 1: that range
+  // is never empty and getAckBuf never fails — the ACK (and close()'s RST) always goes out.  The one
+  // case the reference would drop, a buffer still in the NIC's TX queue, does not exist here.
+  void sendAck(Conn& c, bool immediate) {
     if (kDelayedAckMS == 0 || immediate) {
       emit(c, c.seg(c.send_next_).seq, kAck, nullptr, 0);
       return;
@@ -1009,16 +1095,19 @@ class TcpEngine {
     c.established_ = false;
     for (auto& t : c.timers_) t.unlink();
     if (!enter_tw || tw_cnt_ == kMaxTw) { // Core::enterTW: TIME_WAIT table full -> delete (Core.h:608-611)
-      delEntry(c.key_);
+      releaseEntry(c);
       return;
     }
     // Core::enterTW (Core.h:607-638)
-    free_conns_.push_back(c.id_);
-    --conn_cnt_;
     const uint32_t tw_id = free_tws_.back();
+    if (table_.enterTW(c.key_, tw_id) != 0) { // the key is not in the table (a reference-literal rehash
+      releaseEntry(c);                        // stranded it): no TIME_WAIT, the ids stay consistent
+      return;
+    }
     free_tws_.pop_back();
     ++tw_cnt_;
-    table_.enterTW(c.key_, tw_id);
+    free_conns_.push_back(c.id_);
+    --conn_cnt_;
     ++tver_;
     Tw& tw = tws_[tw_id];
     tw.key = c.key_;
@@ -1029,6 +1118,18 @@ class TcpEngine {
     tw.seq_num = c.seg(c.send_next_).seq;
     tw.ack_num = c.rx_.ackSeq();
     wheel_.add(kTimeWaitTimeout, &tw.timer);
+  }
+
+  // A closing connection leaves the table (delConnEntry); its id is returned even when its key
+  // cannot be found (stranded by a reference-literal rehash, PN_TABLE_REFERENCE_LITERAL).
+  void releaseEntry(Conn& c) {
+    uint32_t id = PN_MISS;
+    if (table_.find(c.key_, nullptr, &id) && id == c.id_) {
+      delEntry(c.key_);
+      return;
+    }
+    free_conns_.push_back(c.id_);
+    --conn_cnt_;
   }
 
   // Core::delConnEntry (Core.h:578-605) with its id bookkeeping.
@@ -1076,7 +1177,7 @@ class TcpEngine {
     }
   }
 
-  // ---- frame building: headers only; pn_tx_fill writes both checksums at flush ----
+  // ---- frame building: headers only; both checksums are written at flush (flushTx) ----
   enum Kind { kSyn, kSynAck, kData, kFinAck, kAck, kRstAck };
   uint8_t* txFrame() {
     if (tx_n_ == kTxBatch) flushTx();
@@ -1108,7 +1209,7 @@ class TcpEngine {
     tcp[12] = (uint8_t)(doff_words << 4);
     tcp[13] = flags;
     wr16(tcp + 14, window);
-    wr32(tcp + 16, 0); // checksum (filled on the GPU), urgent pointer
+    wr32(tcp + 16, 0); // checksum (filled at flush), urgent pointer
   }
   // A segment of connection c (TcpConn::sendBuf, TcpConn.h:310-323): ack = what was received
   // so far (updateLastAck, TcpConn.h:838-843), window = free receive buffer.
@@ -1132,7 +1233,10 @@ class TcpEngine {
       case kFinAck:
         header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, (uint8_t)(PSH | ACK | (k == kFinAck ? FIN : 0)), win,
                20 + len);
-        if (len) std::memcpy(f + 54, payload, len);
+        if (len) {
+          std::memcpy(f + 54, payload, len);
+          ++tx_data_n_;
+        }
         break;
       case kAck: header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, PSH | ACK, win, 20); break;
       case kRstAck: header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, RST | PSH | ACK, win, 20); break;
@@ -1183,6 +1287,9 @@ class TcpEngine {
   uint64_t tver_ = 1, synced_ver_ = 0, disp_ver_ = 0, fl_ver_[2] = {0, 0};
   uint32_t cur_ = 0, fl_n_[2] = {0, 0};
   uint32_t tx_cur_ = 0, tx_fl_n_ = 0; // TX batch being built; frames of the other one in its fill (pipelined)
+  uint32_t tx_data_n_ = 0;            // payload-bearing frames in the batch being built
+  bool tx_fl_host_ = false;           // the batch in its fill was summed on the host
+  uint64_t tx_host_frames_ = 0, tx_gpu_frames_ = 0;
   uint64_t re_resolved_ = 0;
   bool ready_ = false, drop_bad_ = true;
   const char* err_ = "Closed";

@@ -16,12 +16,14 @@
 //            bytes NOT consumed, re-presented with the next data (TcpConn.h:715-724)
 //   void onTcpConnected(Conn&), onTcpDisconnect(Conn&), onSendTimeout(Conn&),
 //        onRecvTimeout(Conn&)                                         optional
-//   bool allowNewConnection(uint32_t ip_be, uint16_t port_be)          optional (accept all)
+//   bool allowNewConnection(uint32_t ip_be, uint16_t port_be)          consulted only with
+//        Conf::UseAllowNewConnection = true (efvitcp::TcpServer's event, TcpServer.h:84); by
+//        default every SYN is allowed, as pollnet's EfviTcpServer wrapper does (EfviTcp.h:270)
 // so a handler written for EfviTcpServer (example/tcpserver.cc:61-91) compiles unchanged.
 //
 // The poll itself — one timer tick, one pn_classify launch over the received frames, the
-// records walked through the reference's branches, one pn_tx_fill launch over the frames it
-// sends — is TcpEngine's (tcp_engine.hpp).  The server's own branches (TcpServer.h:80-111):
+// records walked through the reference's branches, the checksums of the frames it sends (one
+// pn_tx_fill launch, or the host for a batch of header-only frames) — is TcpEngine's (tcp_engine.hpp).  The server's own branches (TcpServer.h:80-111):
 //   - unknown flow: a SYN is accepted while conn_cnt < MaxConnCnt and allowNewConnection
 //     agrees (entry added, SYN-ACK with the MSS option sent), anything else but an RST is
 //     answered with an RST;

@@ -40,6 +40,7 @@ struct PeerConf {
   static const uint32_t RxBatch = 1024;
   static const uint32_t TxBatch = 128;
   static const uint32_t DelayedAckMS = 10;
+  static const bool UseAllowNewConnection = true; // efvitcp::TcpServer's admission event (TcpServer.h:84)
   struct UserData {
     uint32_t echoed = 0;
     bool fin_asked = false;
@@ -431,11 +432,45 @@ static int check(const char* tag, R& r) {
   return fail;
 }
 
+// the same Conf with every TX batch through the backend's fill (pn_tx_fill on the GPU, the
+// oracle's fill in the twin) instead of the host for batches with few payload frames
+template <class Conf>
+struct AllTxOnBackend : Conf {
+  static const uint32_t TxGpuMinDataFrames = 0;
+};
+// ... and a mixed policy: batches with 2+ payload frames through the backend, the rest on the host
+template <class Conf>
+struct MixedTx : Conf {
+  static const uint32_t TxGpuMinDataFrames = 2;
+};
+
+template <class A, class B>
+static int same_frames(const char* what, A& a, B& b) {
+  const auto &x = a.srv->link().out, &y = b.srv->link().out;
+  const bool eq = x == y && a.log == b.log;
+  std::printf("%s: TX frames %s (%zu vs %zu), logs %s\n", what, eq ? "identical" : "DIFFERENT", x.size(), y.size(),
+              a.log == b.log ? "identical" : "DIFFERENT");
+  return eq ? 0 : 1;
+}
+
 template <class Conf>
 static int scenario(bool gpu, const std::vector<Client>& pop, const char* name) {
   int fail = 0;
   Run<OracleBackend, Conf> twin;
   if (!twin.go(pop)) return 100;
+  {
+    // TX policies: host sums for small batches (default), the oracle's fill for every batch, mixed
+    Run<OracleBackend, AllTxOnBackend<Conf>> twin_b;
+    Run<OracleBackend, MixedTx<Conf>> twin_m;
+    if (!twin_b.go(pop) || !twin_m.go(pop)) return 100;
+    std::printf("[%s] TX policies: default %llu frames summed on the host; mixed %llu host + %llu backend fill\n",
+                name, (unsigned long long)twin.srv->txHostFrames(), (unsigned long long)twin_m.srv->txHostFrames(),
+                (unsigned long long)twin_m.srv->txGpuFrames());
+    if (!twin_m.srv->txHostFrames() || !twin_m.srv->txGpuFrames() || twin_b.srv->txHostFrames())
+      fail++, std::printf("FAIL: both TX policies not exercised\n");
+    fail += same_frames("twin host-fill vs twin backend-fill", twin, twin_b);
+    fail += same_frames("twin mixed vs twin backend-fill", twin_m, twin_b);
+  }
   std::printf("[%s] twin: %llu records re-resolved against the live table\n", name,
               (unsigned long long)twin.srv->reResolved());
   fail += check("twin", twin);
@@ -454,6 +489,40 @@ static int scenario(bool gpu, const std::vector<Client>& pop, const char* name) 
     fail += !frames_eq + (g.log != twin.log);
     std::printf("gpu: handler log %s, TX frames %s (%zu)\n", g.log == twin.log ? "identical" : "DIFFERENT",
                 frames_eq ? "identical" : "DIFFERENT", a.size());
+    Run<GpuBackend, MixedTx<Conf>> g_mixed; // batches with payload through pn_tx_fill, the rest on the host
+    if (!g_mixed.go(pop)) return 100;
+    if (!g_mixed.srv->txGpuFrames() || !g_mixed.srv->txHostFrames())
+      fail++, std::printf("FAIL: gpu mixed TX policy not exercised\n");
+    fail += same_frames("gpu mixed TX policy vs twin", g_mixed, twin);
+  }
+  return fail;
+}
+
+// pollnet's EfviTcpServer wrapper never consults the handler's allowNewConnection (its TmpHandler
+// returns true, EfviTcp.h:270): without Conf::UseAllowNewConnection the same handler, which would
+// refuse every port divisible by 7, gets no refusal at all (room for every client).
+struct PeerConfWrapper : PeerConf {
+  static const bool UseAllowNewConnection = false;
+  static const uint32_t MaxConns = 128;
+};
+static int wrapper_admission(bool gpu, const std::vector<Client>& pop) {
+  auto one = [&](auto& r, const char* tag) {
+    if (!r.go(pop)) return 100;
+    uint32_t refused = 0, est = 0, by7 = 0;
+    for (auto& c : r.srv->link().clients) {
+      refused += c.refused;
+      est += c.established;
+      by7 += c.established && c.port % 7 == 0;
+    }
+    std::printf("%s (allowNewConnection not consulted): %u established (%u on ports divisible by 7), %u refused\n", tag,
+                est, by7, refused);
+    return (refused != 0 || by7 == 0) ? (std::printf("FAIL %s: wrapper admission\n", tag), 1) : 0;
+  };
+  Run<OracleBackend, PeerConfWrapper> twin;
+  int fail = one(twin, "twin");
+  if (gpu) {
+    Run<GpuBackend, PeerConfWrapper> g;
+    fail += one(g, "gpu");
   }
   return fail;
 }
@@ -469,6 +538,7 @@ int main(int argc, char** argv) {
     fail += scenario<PeerConfBudget>(gpu, pop, "3-ms RX latency budget");
     fail += scenario<PeerConfChunk>(gpu, pop, "RX chunks of 16");
     fail += scenario<PeerConfPipe>(gpu, pop, "pipelined RX (dispatch one poll later)");
+    if (g_seed == 0) fail += wrapper_admission(gpu, pop);
   }
   std::printf("%s\n", fail ? "FAIL" : "PASS");
   return fail ? 1 : 0;
