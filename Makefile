@@ -9,7 +9,7 @@ LIB = pollnet_amd/libpollnet_amd.so
 SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
 HDRS = include/pollnet_amd.h
 KHDRS = pollnet_amd/csrc/frame_pass.hpp pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp \
-  pollnet_amd/csrc/rx_classify.hpp pollnet_amd/csrc/tx_fill.hpp
+  pollnet_amd/csrc/rx_classify.hpp pollnet_amd/csrc/tx_fill.hpp pollnet_amd/csrc/stream_match.hpp
 # measurement-only library (bench ceilings; A/B variants with TUNING=1): never loaded by the product
 TUNING_LIB = pollnet_amd/libpollnet_amd_tuning.so
 TUNING_SRCS = pollnet_amd/csrc/rx_tuning.hip pollnet_amd/csrc/tx_tuning.hip

@@ -279,50 +279,37 @@ def e2e_zero_copy(torch, ctx, slots, n, passes=3):
             "note": "pn_classify on pinned host 2048-B slots (zero copy), records to pinned host memory"}, host_res
 
 
-def frame_lines(slots):
-    """u32 per slot: slot start to the frame's pad byte (the lines a frame occupies)."""
-    tl = slots[:, FRAME_OFF + 16].astype(np.uint32) << 8 | slots[:, FRAME_OFF + 17]  # ip tot_len (BE)
-    return (FRAME_OFF + 14 + tl + (tl & 1)).astype(np.uint32)
-
-
-def ceilings(torch, ctx, frames, n, res, stream, slot_pattern, lens=None, reps=10):
-    """Same-run bandwidth ceilings (no arithmetic; kernels of the measurement-only tuning
-    library): a front-to-back stream read of the whole ring, and the RX kernel's own load
-    pattern over the first 1536 B of each slot with and without its 16-B/frame record
-    writes.  With `lens`, the same pattern over each frame's own lines, in the RX kernel's
-    workgroup order and occupancy: the ceiling for mixed-size rings (C3/C5)."""
+def ceilings(torch, ctx, bufs, n, res, stream, steps=20, rounds=3):
+    """Same-run ceilings (kernels of the measurement-only tuning library, never the product path):
+    the plain front-to-back stream read of one resident batch, and the tight one -- the production
+    kernel with the conn-table probe and the lane reduction ablated (same window and stream loads,
+    record stores, occupancy and workgroup order; pn_calib_classify_ablated).  The product and the
+    ablated kernel are timed alternately over the same rotating batches (time_launches, HIP events);
+    kernel_vs_ablated_ceiling = ablated / product <= 1 measures what the arithmetic and the probe cost."""
     from pollnet_amd import tuning as tn  # measurement-only library, never the product path
 
-    sink = torch.zeros(4096, dtype=torch.int32, device=frames.device)
+    sink = torch.zeros(4096, dtype=torch.int32, device=bufs[0].device)
+    scratch = torch.empty_like(res)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-
-    def t(fn):
-        fn()
-        ev[0].record(stream)
-        for _ in range(reps):
-            fn()
-        ev[1].record(stream)
-        torch.cuda.synchronize()
-        return ev[0].elapsed_time(ev[1]) / reps * 1e-3
-
-    out = {"note": "calib kernels in pollnet_amd/csrc/rx_tuning.hip (libpollnet_amd_tuning.so); no header work, "
-                   "no arithmetic"}
-    # the plain stream read of the whole ring: a ceiling, and the known byte count that calibrates
-    # FETCH_SIZE in the PMC passes (scripts/gpu_pmc.sh, pmc_summarize.py)
-    ts = t(lambda: tn.calib_stream_read(ctx, frames, frames.numel(), sink, stream))
-    out["stream_read_gbs"] = round(frames.numel() / ts / 1e9, 1)
-    if slot_pattern:
-        t0 = t(lambda: tn.calib_slot_read(ctx, frames, n, STRIDE, 1536, sink, stream, 0))
-        t16 = t(lambda: tn.calib_slot_read(ctx, frames, n, STRIDE, 1536, res, stream, 16))
-        out["slot_pattern_read_gbs"] = round(n * 1536 / t0 / 1e9, 1)
-        out["slot_pattern_read_plus_16B_records_ms"] = round(t16 * 1e3, 5)
-    if lens is not None:
-        lens_dev = torch.from_numpy(lens).to(frames.device)
-        tv0 = t(lambda: tn.calib_slot_read_var(ctx, frames, n, STRIDE, lens_dev, sink, stream, 0))
-        tv16 = t(lambda: tn.calib_slot_read_var(ctx, frames, n, STRIDE, lens_dev, res, stream, 16))
-        out["frame_lines_read_ms"] = round(tv0 * 1e3, 5)
-        out["frame_lines_read_plus_16B_records_ms"] = round(tv16 * 1e3, 5)
-    return out
+    tn.calib_stream_read(ctx, bufs[0], bufs[0].numel(), sink, stream)
+    ev[0].record(stream)
+    for _ in range(10):
+        tn.calib_stream_read(ctx, bufs[0], bufs[0].numel(), sink, stream)
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    ts = ev[0].elapsed_time(ev[1]) / 10 * 1e-3
+    prod, abl = [], []
+    for _ in range(rounds):
+        prod.append(time_launches(torch, lambda d: ctx.classify(d, STRIDE, FRAME_OFF, n, res, stream), bufs, steps,
+                                  stream))
+        abl.append(time_launches(torch, lambda d: tn.calib_classify_ablated(ctx, d, STRIDE, FRAME_OFF, n, scratch, stream),
+                                 bufs, steps, stream))
+    p_ms, a_ms = statistics.median(prod), statistics.median(abl)
+    return {"note": "tuning-library kernels (libpollnet_amd_tuning.so): stream read of one batch; the production "
+                    "kernel with probe + lane reduction ablated, timed alternately with the product",
+            "stream_read_gbs": round(bufs[0].numel() / ts / 1e9, 1),
+            "product_ms_alternating": round(p_ms, 5), "ablated_kernel_ms": round(a_ms, 5),
+            "kernel_vs_ablated_ceiling": round(a_ms / p_ms, 4)}
 
 
 def load_pmc(workload_key):
@@ -397,16 +384,15 @@ def secondary_rx(torch, pa, cfg, n, steps, stream, packed=False):
     sha_ok = gd is not None and gd["n"] == n and hashlib.sha256(ref.tobytes()).hexdigest() == gd["records_sha256"]
     kern = time_launches(torch, lambda d: ctx.classify(d, STRIDE, FRAME_OFF, n, res, stream), bufs, steps, stream)
     algo = int(sum(wires) / 2) + 16 * n
-    lens = frame_lines(slots0)
-    c = ceilings(torch, ctx, bufs[0], n, res, stream, slot_pattern=False, lens=lens)
+    c = ceilings(torch, ctx, bufs, n, res, stream, steps=steps)
     pmc = load_pmc(f"c{cfg}_n{n}")
     out = {"workload": WORKLOADS[cfg], "frames": n, "resident_batches": 2, "kernel_ms": round(kern, 5),
            "gbit_per_s": round(8 * sum(wires) / 2 / (kern * 1e-3) / 1e9, 1),
            "mframes_per_s": round(n / (kern * 1e-3) / 1e6, 1),
            "algorithmic_bytes_per_launch": algo, "achieved_gbs": round(algo / (kern * 1e-3) / 1e9, 1),
            "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "frame_lines_read_plus_records_ms": c["frame_lines_read_plus_16B_records_ms"],
-           "frac_vs_frame_lines_ceiling": round(c["frame_lines_read_plus_16B_records_ms"] / kern, 4),
+           "ablated_kernel_ms": c["ablated_kernel_ms"], "kernel_vs_ablated_ceiling": c["kernel_vs_ablated_ceiling"],
+           "stream_read_gbs": c["stream_read_gbs"],
            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
            "traffic_over_algorithmic": None if pmc is None else pmc.get("traffic_over_algorithmic"),
            "records_sha256_matches_golden": bool(sha_ok)}
@@ -553,8 +539,16 @@ def secondary_tx(torch, pa, n, steps, stream):
         exp[:, off + 24:off + 26] = 0x5A
         exp[:, off + 50:off + 52] = 0xA5
         orc.tx_fill_batch(exp, STRIDE, off, 4096, None, orc.TX_TCP)
-        kern = time_launches(torch, lambda d: ctx.tx_fill(d, STRIDE, off, n, None, pa.PN_TX_TCP, stream), bufs, steps,
-                             stream)
+        from pollnet_amd import tuning as tn  # measurement-only library
+
+        ks, abl = [], []
+        for _ in range(3):  # product and ablated ceiling alternately (the ceiling's fields are garbage;
+            # the fill recomputes both from the frame bytes, so the product's timing is unaffected)
+            ks.append(time_launches(torch, lambda d: ctx.tx_fill(d, STRIDE, off, n, None, pa.PN_TX_TCP, stream), bufs,
+                                    steps, stream))
+            abl.append(time_launches(torch, lambda d: tn.calib_tx_ablated(ctx, d, STRIDE, off, n, stream), bufs, steps,
+                                     stream))
+        kern, kabl = statistics.median(ks), statistics.median(abl)
         algo = 1504 * n
         tr = None if not pmc else pmc.get(f"frame_off_{off}", {})
         out[f"frame_off_{off}"] = {
@@ -562,6 +556,7 @@ def secondary_tx(torch, pa, n, steps, stream):
             "kernel_ms": round(kern, 5), "gbit_per_s": round(8 * 1514 * n / (kern * 1e-3) / 1e9, 1),
             "algorithmic_bytes_per_launch": algo, "achieved_gbs": round(algo / (kern * 1e-3) / 1e9, 1),
             "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "ablated_kernel_ms": round(kabl, 5), "kernel_vs_ablated_ceiling": round(kabl / kern, 4),
             "traffic": None if not tr else tr.get("hbm_bytes_per_launch"),
             "traffic_over_algorithmic": None if not tr else tr.get("traffic_over_algorithmic"),
             "first_4096_vs_oracle": bool(np.array_equal(got, exp)),
@@ -669,7 +664,8 @@ def run_rank(rank, world, local_rank, args):
     k = min(n, 4096)
     exp = orc.classify_batch(slots, STRIDE, FRAME_OFF, k, entries, mask, table.max_conn_cnt, threads=8)
     gate = {"all_batches_invariants": inv_ok, "batches_sha256_gated": f"{sha_gated}/{R}",
-            "gated_batches_sha256_match_golden": bool(sha_ok and sha_gated > 0),
+            # None: no committed digest covers this frame range (e.g. a --frames override)
+            "gated_batches_sha256_match_golden": bool(sha_ok) if sha_gated else None,
             "batch0_first_4096_vs_oracle": bool(np.array_equal(got0[: k * 16].view(pa.RESULT_DTYPE), exp))}
     verified = all(v for v in gate.values() if isinstance(v, bool))
     if not verified:
@@ -750,12 +746,8 @@ def run_rank(rank, world, local_rank, args):
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
-    if rank == 0 and world == 1:  # the slot-pattern ceilings are for 1514-B frames (1536 B of lines per slot)
-        c = ceilings(torch, ctx, frames, n, res, stream, slot_pattern=cfg in (2, 4), lens=frame_lines(slots))
-        if cfg in (2, 4):
-            c["kernel_vs_read_plus_records_ceiling"] = round(c["slot_pattern_read_plus_16B_records_ms"] / kern_ms, 4)
-        c["kernel_vs_frame_lines_ceiling"] = round(c["frame_lines_read_plus_16B_records_ms"] / kern_ms, 4)
-        out["roofline"]["same_run_ceilings"] = c
+    if rank == 0 and world == 1:
+        out["roofline"]["same_run_ceilings"] = ceilings(torch, ctx, frames_b, n, res, stream)
     if rank == 0 and world == 1 and not args.no_secondary and cfg == 2 and n == 1 << 20:
         t_sec = time.perf_counter()
         sec = {}

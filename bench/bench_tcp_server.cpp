@@ -226,8 +226,16 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
   for (uint32_t p = 0; p < polls; p++)
     if (be.classify(n, srv->table(), [](uint64_t, const pn_result&, const uint8_t*) {})) break;
   const auto c1 = Clock::now();
-  for (uint32_t p = 0; p < polls && acks; p++)
-    if (be.fillTx(acks)) break;
+  // the TX leg as the engine runs it for a poll's ACKs: header-only frames summed on the host
+  // (below TxGpuMinDataFrames payload frames), else one pn_tx_fill launch
+  for (uint32_t p = 0; p < polls && acks; p++) {
+    if (Server::kTxGpuMin > 0) {
+      for (uint32_t i = 0; i < acks; i++)
+        srv_detail::fill_tcp_checksums(be.txSlots(0) + (size_t)i * Backend::kStride + Backend::kFrameOff);
+    } else if (be.fillTx(acks)) {
+      break;
+    }
+  }
   out.classify_share = secs(c0, c1) / t;
   out.tx_share = secs(c1, Clock::now()) / t;
   out.ok = timed_bytes == frames * kPayload && h.bytes == (uint64_t)link.poll_no * (kBatch / n_flows) * n_flows * kPayload &&

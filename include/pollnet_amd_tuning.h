@@ -31,6 +31,21 @@ int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint3
 int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, const void* lens_dev,
                            int store_bytes, void* sink_dev, void* stream);
 
+/* Same-run ceilings that the product kernels cannot beat (bench.py): the production RX kernel
+ * with the conn-table probe and the stream-phase lane reduction ablated (same loads, record
+ * stores, occupancy and order; frame_off 2 or 18), and the production two-launch TX fill
+ * (n > 65,536; frame_off 2 or 14) with its lane reduction ablated.  Timing only: their
+ * records / fields are wrong. */
+int pn_calib_classify_ablated(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                              void* results_dev, void* stream);
+int pn_calib_tx_ablated(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n, void* stream);
+
+/* pn_match_streams in either kernel form: variant 1 = 4 lanes per frame load its header chunks
+ * through LDS (production), 0 = one lane per frame loads its own (scripts/bench_streams.py). */
+int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                             const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
+                             int variant);
+
 /* Test helper (no ctx): holds `stream` with one lane until the host stores non-zero to *go_host
  * or max_ms (<= 10000) pass, then stores 1 (released) / 2 (timed out) to *done_host; both in
  * pinned host memory.  Unrelated work in flight on a foreign stream (tests/test_gpu_notify.py). */

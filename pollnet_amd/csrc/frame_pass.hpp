@@ -51,8 +51,14 @@ enum : int { kSkipEmptyLoads = 1024 };
 // its first stream KiB (one ballot per wave); a wave of full-size frames (every C2 wave) streams
 // with unconditional loads, the form without the branches.
 enum : int { kSkipWaveGate = 16384 };
+// With kCoopProbe: the wave walks each distinct run position once for every lane standing at it
+// (in C5's adversarial cluster, every cluster lane of a wave shares one home slot): one 64-entry
+// round trip resolves all of them, each against its own key, instead of one round trip per lane.
+// C5 -3.9 % (0.1660 -> 0.1596 ms; the probe's share over the no-probe ablation 13.6 -> 7.2 us),
+// C3 equal (profiles/r03/probe_group_c{3,5}.json).
+enum : int { kGroupProbe = 32768 };
 // The production RX configuration.
-constexpr int kProdAbl = kExactRange | kCoopProbe | kSkipEmptyLoads | kSkipWaveGate;
+constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the

@@ -152,27 +152,60 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
       }
     }
     uint64_t need = __ballot(srch);
-    while (need != 0) { // wave-uniform
-      const uint32_t L = (uint32_t)__builtin_ctzll(need);
-      need &= need - 1;
-      const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L); // readlane returns int
-      for (uint32_t base = __builtin_amdgcn_readlane(e, L) + 1;; base += kWave) {
-        const uint32_t idx = base + lane;
-        u32x4 ent = {0u, 0u, 0u, 0u};
-        if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
-        const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
-        const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
-        if (stop != 0) {
-          const uint32_t first = (uint32_t)__builtin_ctzll(stop);
-          const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
-          const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
-          if (lane == L) {
-            e = base + first;
-            k = ((uint64_t)khi << 32) | klo;
-            cid = c;
+    if constexpr (ABL & kGroupProbe) {
+      while (need != 0) { // wave-uniform
+        // the lanes at the first searching lane's run position: one fetch serves them all
+        const uint32_t e0 = __builtin_amdgcn_readlane(e, (uint32_t)__builtin_ctzll(need));
+        uint64_t group = __ballot(srch && e == e0);
+        for (uint32_t base = e0 + 1; group != 0; base += kWave) {
+          const uint32_t idx = base + lane;
+          u32x4 ent = {0u, 0u, 0u, 0u};
+          if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
+          const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
+          for (uint64_t pend = group; pend != 0; pend &= pend - 1) {
+            const uint32_t L = (uint32_t)__builtin_ctzll(pend);
+            const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L);
+            const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
+            if (stop != 0) { // the entry lane L's scalar walk stops at
+              const uint32_t first = (uint32_t)__builtin_ctzll(stop);
+              const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
+              const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
+              if (lane == L) {
+                e = base + first;
+                k = ((uint64_t)khi << 32) | klo;
+                cid = c;
+                srch = false;
+              }
+              group &= ~(1ull << L);
+            }
           }
-          break;
+        }
+        need = __ballot(srch);
+      }
+    } else {
+      while (need != 0) { // wave-uniform
+        const uint32_t L = (uint32_t)__builtin_ctzll(need);
+        need &= need - 1;
+        const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L); // readlane returns int
+        for (uint32_t base = __builtin_amdgcn_readlane(e, L) + 1;; base += kWave) {
+          const uint32_t idx = base + lane;
+          u32x4 ent = {0u, 0u, 0u, 0u};
+          if (idx < a.n_entries) ent = *reinterpret_cast<const u32x4*>(a.tbl + idx);
+          const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
+          const uint64_t stop = __ballot(idx >= a.n_entries || kk >= kl);
+          if (stop != 0) {
+            const uint32_t first = (uint32_t)__builtin_ctzll(stop);
+            const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
+            const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
+            if (lane == L) {
+              e = base + first;
+              k = ((uint64_t)khi << 32) | klo;
+              cid = c;
+            }
+            break;
+          }
         }
       }
     }

@@ -4,6 +4,7 @@
 // linked into or loaded by the product path; the variants are compiled only with
 // `make TUNING=1` (-DPN_TUNING_VARIANTS).
 #include "rx_classify.hpp"
+#include "stream_match.hpp"
 
 namespace {
 using pn_internal::g_err;
@@ -164,6 +165,28 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_grouped_kernel(const ui
     __builtin_amdgcn_raw_buffer_store_b128(recs[g * kFramesPerWave + lane], ro, (g * kFramesPerWave + lane) * 16, 0, kStoreAux);
 }
 
+// The production launch's arguments (rx_kernel.hip strided_args) for the ceilings below.
+int strided_args_calib(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                       void* results_dev, KArgs& a) {
+  if (((uintptr_t)frames_dev & 15) || ((uintptr_t)results_dev & 15) || (slot_stride & 15) || slot_stride > 65536 ||
+      slot_stride < frame_off + 96)
+    return set_err(ctx, PN_EINVAL, "ceiling: layout contract");
+  a.frames = (const uint8_t*)frames_dev;
+  a.out = (pn_result*)results_dev;
+  a.tbl = ctx->tbl_dev;
+  a.mask = ctx->mask;
+  a.n_entries = ctx->n_entries;
+  a.max_conn = ctx->max_conn;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.avail = slot_stride - frame_off;
+  a.offs = nullptr;
+  a.fpw = frames_per_wave(n);
+  if (!coop_layout(a)) return set_err(ctx, PN_EINVAL, "ceiling: needs the cooperative layout");
+  return PN_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -256,6 +279,8 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 37: launch_one<0, 1, kProdAbl & ~kSkipEmptyLoads>(a, s); break;  // every stream load issued (before kSkipEmptyLoads;
     // the per-lane EXEC mask, per-batch gate and per-frame pair branch forms measured against it are
     // in the history)
+    case 38: launch_one<0, 1, kProdAbl | kGroupProbe>(a, s); break;  // cluster lanes resolved per run position
+    case 39: launch_one<0, 1, kProdAbl & ~kGroupProbe>(a, s); break; // one lane per round trip past kAhead
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
@@ -270,6 +295,25 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
 
 
 #endif // PN_TUNING_VARIANTS
+
+// Same-run ceiling for pn_classify (bench.py): the production kernel -- its window loads, stream
+// loads, record stores, occupancy and workgroup order -- with the conn-table probe and the stream
+// phase's lane reduction ablated.  Timing only: the records are wrong.  frame_off 2 or 18 (the
+// MIS = 0 class, the bench's layout), cooperative layout.
+int pn_calib_classify_ablated(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                              void* results_dev, void* stream) {
+  if (!ctx || !ctx->tbl_dev || !frames_dev || !results_dev || n == 0 || (frame_off + 14) % 16 != 0)
+    return set_err(ctx, PN_EINVAL, "pn_calib_classify_ablated: bad arguments");
+  KArgs a;
+  int rc = strided_args_calib(ctx, frames_dev, slot_stride, frame_off, n, results_dev, a);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  launch_one<0, 1, kProdAbl | kAblNoProbe | kAblNoReduce>(a, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "pn_calib_classify_ablated launch");
+  pn_internal::note_stream(ctx, s);
+  return PN_OK;
+}
 
 int pn_calib_slot_read(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, uint32_t stride, uint32_t bytes,
                        int store_bytes, void* sink_dev, void* stream) {
@@ -319,6 +363,24 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
   return PN_OK;
 }
 
+
+// pn_match_streams in either form (stream_match.hpp): V = 1 cooperative chunks through LDS,
+// V = 0 one lane per frame.  A/B by scripts/bench_streams.py.
+int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                             const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
+                             int variant) {
+  if (n == 0 || (variant != 0 && variant != 1)) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  MatchArgs a;
+  int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (variant == 1) launch_match<1>(a, frame_off, s);
+  else launch_match<0>(a, frame_off, s);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "match variant launch");
+  pn_internal::note_stream(ctx, s);
+  return PN_OK;
+}
 
 int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max_ms, void* stream) {
   if (!go_host || !done_host || max_ms == 0 || max_ms > 10000)

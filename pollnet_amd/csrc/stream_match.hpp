@@ -1,0 +1,157 @@
+// stream_match.hpp — the TcpStream filter kernel (device code + launch helper), shared by the
+// product library (stream_kernel.hip: pn_match_streams) and the tuning library (rx_tuning.hip:
+// the A/B variant).  Internal linkage; one including translation unit per library.
+#pragma once
+// TcpStream's packet filter for a whole batch, many streams at once (SURVEY §8(f)
+// rank 3).  Reference, per frame and per stream (TcpStream.h:39-52):
+//   etherType == 0x0008 (0x0800 read little-endian) && ip.protocol == 6 &&
+//   (filter_src_ip == 0 || == ip.ipSrc) && (filter_dst_ip == 0 || == ip.ipDst) &&
+//   (filter_src_port == 0 || == tcp.portSrc) && (filter_dst_port == 0 || == tcp.portDst)
+// with the IP header assumed 20 bytes (TcpHeaderPos = 14 + 20, TcpStream.h:213-214).
+//
+// Each frame's header bytes (ethertype .. TCP ports) are read once -- one 64-B segment of
+// its slot, a gather at the slot stride -- and the frame's lane compares them against every
+// filter in the kernel-argument segment (scalar loads, wave-uniform) and writes the index of
+// the first stream the frame belongs to.  V = 1 (production): 4 lanes per frame load its
+// segment's 16-B chunks with one instruction for 16 frames (one 64-B request per frame per
+// instruction, only the chunks the fields touch) into an LDS tile each frame's lane reads back.
+// V = 0 (tuning): each lane loads its own frame's 4 chunks, 4 instructions each touching 64
+// slots.
+#include <hip/hip_runtime.h>
+
+#include "../../include/pollnet_amd.h"
+#include "device_common.hpp"
+#include "pn_internal.hpp"
+
+namespace {
+
+using namespace pn_dev;
+using pn_internal::hip_err;
+using pn_internal::set_err;
+
+struct MatchArgs {
+  const uint8_t* frames;
+  uint32_t* out;
+  uint32_t n;
+  uint32_t stride;
+  uint32_t ipa_off; // (frame_off + 14) & ~15
+  uint32_t n_filters;
+  pn_stream_filter f[PN_MAX_STREAM_FILTERS];
+};
+
+// MIS = (frame_off + 14) % 16: the IP header's offset in its 16-B chunk.  The window
+// is the chunk before it (ethertype when MIS < 2) and the 3 chunks from it.
+constexpr int kPre = 16; // window starts one chunk before the IP header's chunk
+// whether window chunk c holds any byte of ethertype .. the TCP ports ([IP - 2, IP + 24))
+template <int MIS>
+__device__ __host__ constexpr bool chunk_needed(int c) {
+  return 16 * c < kPre + MIS + 24 && 16 * c + 16 > kPre + MIS - 2;
+}
+
+template <int MIS, int V>
+__global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
+  const uint32_t f = blockIdx.x * 256 + threadIdx.x;
+  Win<16> h;
+  if constexpr (V == 1) {
+    // wave w of the workgroup: frames f0 .. f0 + 63; instruction i: lane l loads chunk l & 3 of
+    // frame f0 + 16 i + (l >> 2)
+    __shared__ u32x4 tile[256 * 4];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t f0 = blockIdx.x * 256 + w * 64;
+    u32x4* wt = tile + w * 256;
+    const uint32_t c = lane & 3;
+    const uint32_t n_here = f0 < a.n ? min(64u, a.n - f0) : 0u;
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.frames + (uint64_t)f0 * a.stride + a.ipa_off - kPre,
+                                                 n_here ? (n_here - 1) * a.stride + 64 : 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = 16 * i + (lane >> 2);
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if ((c == 0 && chunk_needed<MIS>(0)) || (c == 1 && chunk_needed<MIS>(1)) || (c == 2 && chunk_needed<MIS>(2)) ||
+          (c == 3 && chunk_needed<MIS>(3)))
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + 16 * c, 0, 0); // past n: zeros, no fetch
+      wt[r * 4 + (c ^ (r & 3))] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32x4 v = wt[lane * 4 + (q ^ (lane & 3))];
+      h.d[4 * q + 0] = v.x;
+      h.d[4 * q + 1] = v.y;
+      h.d[4 * q + 2] = v.z;
+      h.d[4 * q + 3] = v.w;
+    }
+    if (f >= a.n) return;
+  } else {
+    if (f >= a.n) return;
+    const __amdgpu_buffer_rsrc_t rs =
+        frame_rsrc(a.frames + (uint64_t)f * a.stride + a.ipa_off - kPre, kPre + 48);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * c, 0, 0);
+      h.d[4 * c + 0] = v.x;
+      h.d[4 * c + 1] = v.y;
+      h.d[4 * c + 2] = v.z;
+      h.d[4 * c + 3] = v.w;
+    }
+  }
+  constexpr int IP = kPre + MIS;
+  const uint32_t ether_type = h.template u16<IP - 2>(); // as stored: 0x0008 for IPv4
+  const uint32_t proto = h.template b8<IP + 9>();
+  const uint32_t src_ip = h.template u32<IP + 12>(), dst_ip = h.template u32<IP + 16>();
+  const uint32_t src_port = h.template u16<IP + 20>(), dst_port = h.template u16<IP + 22>();
+  uint32_t id = PN_NO_STREAM;
+  if (ether_type == 0x0008 && proto == 6) {
+    for (uint32_t k = 0; k < a.n_filters; ++k) {
+      const pn_stream_filter& q = a.f[k];
+      if ((q.src_ip == 0 || q.src_ip == src_ip) && (q.dst_ip == 0 || q.dst_ip == dst_ip) &&
+          (q.src_port == 0 || q.src_port == src_port) && (q.dst_port == 0 || q.dst_port == dst_port)) {
+        id = k;
+        break;
+      }
+    }
+  }
+  a.out[f] = id;
+}
+
+// The production form (A/B: scripts/bench_streams.py, tuning variant pn_match_streams_variant).
+constexpr int kMatchProd = 1;
+
+template <int V>
+void launch_match(const MatchArgs& a, uint32_t frame_off, hipStream_t s) {
+  const dim3 grid((a.n + 255) / 256), block(256);
+  switch ((frame_off + 14) & 15) {
+    case 0: hipLaunchKernelGGL((match_streams_kernel<0, V>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((match_streams_kernel<2, V>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((match_streams_kernel<4, V>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((match_streams_kernel<6, V>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((match_streams_kernel<8, V>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((match_streams_kernel<10, V>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((match_streams_kernel<12, V>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((match_streams_kernel<14, V>), grid, block, 0, s, a); break;
+  }
+}
+
+// Argument checks and kernel arguments of pn_match_streams.
+inline int match_args(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                      const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, MatchArgs& a) {
+  if (!ctx) return set_err(nullptr, PN_EINVAL, "pn_match_streams: ctx is NULL");
+  if (!frames || !stream_ids || (n_filters && !filters)) return set_err(ctx, PN_EINVAL, "pn_match_streams: NULL buffer");
+  if (n_filters > PN_MAX_STREAM_FILTERS)
+    return set_err(ctx, PN_EINVAL, "pn_match_streams: at most PN_MAX_STREAM_FILTERS filters");
+  if (((uintptr_t)frames & 15) || ((uintptr_t)stream_ids & 3))
+    return set_err(ctx, PN_EINVAL, "pn_match_streams: frames must be 16-byte, ids 4-byte aligned");
+  if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || frame_off < 2 || slot_stride < frame_off + 96)
+    return set_err(ctx, PN_EINVAL, "pn_match_streams: slot_stride/frame_off violate the layout contract");
+  a.frames = (const uint8_t*)frames;
+  a.out = stream_ids;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.n_filters = n_filters;
+  for (uint32_t k = 0; k < n_filters; ++k) a.f[k] = filters[k]; // host memory: copied into the kernel arguments
+  return PN_OK;
+}
+
+} // namespace
+

@@ -2,6 +2,43 @@
 // `make TUNING=1`.  Never part of the product library.
 #include "tx_fill.hpp"
 
+// Same-run ceiling for pn_tx_fill (bench.py): the production launches (the fill kernel with
+// its header window and stream loads, the patch records, the patch kernel's 2-byte stores) with
+// the stream phase's lane reduction ablated -- the same loads and stores, next to no arithmetic.
+// Timing only: the fields it writes are wrong.  Batches above kTxInPlaceMaxFrames (two launches),
+// frame_off 2 or 14, cooperative layout.
+extern "C" int pn_calib_tx_ablated(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                                   void* stream) {
+  if (!ctx || !frames || n <= kTxInPlaceMaxFrames || (frame_off != 2 && frame_off != 14))
+    return set_err(ctx, PN_EINVAL, "pn_calib_tx_ablated: bad arguments");
+  TArgs a;
+  a.frames = (uint8_t*)frames;
+  a.lens = nullptr;
+  a.n = n;
+  a.stride = slot_stride;
+  a.ipa_off = (frame_off + 14) & ~15u;
+  a.avail = slot_stride - frame_off;
+  a.frame_off = frame_off;
+  a.fpw = frames_per_wave(n);
+  if (!coop_layout(a) || slot_stride < frame_off + 96 || (slot_stride & 15))
+    return set_err(ctx, PN_EINVAL, "pn_calib_tx_ablated: needs the cooperative layout");
+  hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_patch(ctx, n, s);
+  if (rc) return rc;
+  a.patch = (uint2*)ctx->tx_patch;
+  const dim3 grid((n + a.fpw - 1) / a.fpw), block(kWave);
+  constexpr int SABL = kExactRange | kAblNoReduce;
+  if (frame_off == 2)
+    hipLaunchKernelGGL((tx_fill_kernel<0, 1, PN_TX_TCP, kWbPatch, 0, 0, 0, true, SABL>), grid, block, 0, s, a);
+  else
+    hipLaunchKernelGGL((tx_fill_kernel<12, 1, PN_TX_TCP, kWbPatch, 0, 0, 0, true, SABL>), grid, block, 0, s, a);
+  hipLaunchKernelGGL((tx_patch_kernel<PN_TX_TCP>), dim3((n + 255) / 256), dim3(256), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "pn_calib_tx_ablated launch");
+  pn_internal::note_stream(ctx, s);
+  return PN_OK;
+}
+
 #ifdef PN_TUNING_VARIANTS
 
 // Tuning variants (TCP mode, cooperative layouts, no lens), A/B-timed by

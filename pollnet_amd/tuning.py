@@ -32,6 +32,9 @@ def _sig(name, res, *args):
 _calib = _sig("pn_calib_stream_read", _i32, _vp, _vp, _u64, _vp, _vp)
 _calib_slot = _sig("pn_calib_slot_read", _i32, _vp, _vp, _u32, _u32, _u32, _i32, _vp, _vp)
 _calib_slot_var = _sig("pn_calib_slot_read_var", _i32, _vp, _vp, _u32, _u32, _vp, _i32, _vp, _vp)
+_calib_rx_abl = _sig("pn_calib_classify_ablated", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp)
+_calib_tx_abl = _sig("pn_calib_tx_ablated", _i32, _vp, _vp, _u32, _u32, _u32, _vp)
+_match_variant = _sig("pn_match_streams_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp, _i32)
 _spin = _sig("pn_test_spin_wait", _i32, _vp, _vp, _u32, _vp)
 _variant = _sig("pn_classify_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
 _idx_variant = _sig("pn_classify_indexed_variant", _i32, _vp, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _i32)
@@ -60,6 +63,27 @@ def calib_slot_read_var(ctx, src_dev, n_slots, stride, lens_dev, sink_dev, strea
     """The same over each frame's own lines (lens_dev: u32 per slot)."""
     rx._check(_calib_slot_var(ctx._h, rx._ptr(src_dev), n_slots, stride, rx._ptr(lens_dev), store_bytes,
                               rx._ptr(sink_dev), rx._stream_handle(stream)), ctx._h, "pn_calib_slot_read_var")
+
+
+def calib_classify_ablated(ctx, frames_dev, slot_stride, frame_off, n, results_dev, stream=None):
+    """The production RX kernel with the probe and lane reduction ablated (timing-only ceiling)."""
+    rx._check(_calib_rx_abl(ctx._h, rx._ptr(frames_dev), slot_stride, frame_off, n, rx._ptr(results_dev),
+                            rx._stream_handle(stream)), ctx._h, "pn_calib_classify_ablated")
+
+
+def calib_tx_ablated(ctx, frames_dev, slot_stride, frame_off, n, stream=None):
+    """The production two-launch TX fill with its lane reduction ablated (timing-only ceiling)."""
+    rx._check(_calib_tx_abl(ctx._h, rx._ptr(frames_dev), slot_stride, frame_off, n, rx._stream_handle(stream)), ctx._h,
+              "pn_calib_tx_ablated")
+
+
+def match_streams_variant(ctx, frames, slot_stride, frame_off, n, filters, stream_ids, variant, stream=None):
+    """pn_match_streams' kernel in form `variant` (1 cooperative, 0 per lane)."""
+    import numpy as np
+
+    flt = np.ascontiguousarray(filters, dtype=rx.STREAM_FILTER_DTYPE)
+    rx._check(_match_variant(ctx._h, rx._ptr(frames), slot_stride, frame_off, n, flt.ctypes.data, len(flt),
+                             rx._ptr(stream_ids), rx._stream_handle(stream), variant), ctx._h, "pn_match_streams_variant")
 
 
 def spin_wait(go_host, done_host, max_ms: int, stream=None):

@@ -14,6 +14,12 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3")
+    ap.add_argument("--rounds", type=int, default=10)
+    args = ap.parse_args()
     import numpy as np
     import torch
 
@@ -23,7 +29,7 @@ def main():
 
     n, off = 1 << 20, 2
     out = {}
-    for cfg in (2, 3):
+    for cfg in [int(c) for c in args.configs.split(",")]:
         p = pa.rx.GenParams.for_config(cfg)
         host = [pa.gen_frames(p, n, 2048, off, first_index=b * n) for b in range(4)]
         dev = [torch.from_numpy(h.reshape(-1)).cuda() for h in host]
@@ -38,23 +44,33 @@ def main():
         ctx.match_streams(dev[0], 2048, off, n, flt, ids, st)
         torch.cuda.synchronize()
         ok = np.array_equal(ids.cpu().numpy().view(np.uint32), match_streams_np(host[0], off, flt))
-        ts = []
+        # the per-lane form (tuning variant 0) gives the same ids
+        ids0 = torch.empty_like(ids)
+        tn.match_streams_variant(ctx, dev[0], 2048, off, n, flt, ids0, 0, st)
+        torch.cuda.synchronize()
+        ok = ok and bool(torch.equal(ids0, ids))
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-        for _ in range(10):
+
+        def timed(fn, reps=20):
             ev[0].record(st)
-            for r in range(20):
-                ctx.match_streams(dev[r % 4], 2048, off, n, flt, ids, st)
+            for r in range(reps):
+                fn(dev[r % 4])
             ev[1].record(st)
             torch.cuda.synchronize()
-            ts.append(ev[0].elapsed_time(ev[1]) / 20)
-        ms = statistics.median(ts)
+            return ev[0].elapsed_time(ev[1]) / reps
+
+        ts, ts0 = [], []
+        for _ in range(args.rounds):  # interleaved: production, per-lane form
+            ts.append(timed(lambda d: ctx.match_streams(d, 2048, off, n, flt, ids, st)))
+            ts0.append(timed(lambda d: tn.match_streams_variant(ctx, d, 2048, off, n, flt, ids0, 0, st)))
+        ms, ms0 = statistics.median(ts), statistics.median(ts0)
         # same-run ceiling for this access pattern: the first 64 / 128 B of every 2-KiB slot,
         # the RX kernel's load pattern, no arithmetic, nothing written
         sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
         ceil = {}
         for nb in (64, 128):
             cs = []
-            for _ in range(5):
+            for _ in range(max(3, args.rounds // 2)):
                 ev[0].record(st)
                 for r in range(20):
                     tn.calib_slot_read(ctx, dev[r % 4], n, 2048, nb, sink, st, 0)
@@ -63,7 +79,8 @@ def main():
                 cs.append(ev[0].elapsed_time(ev[1]) / 20)
             ceil[f"slot_read_first_{nb}B_ms"] = round(statistics.median(cs), 5)
         algo = n * (64 + 4)
-        out[f"c{cfg}"] = {"ids_equal_numpy": ok, "ms_median": round(ms, 5), "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
+        out[f"c{cfg}"] = {"ids_equal_numpy": ok, "ms_median": round(ms, 5), "per_lane_form_ms_median": round(ms0, 5),
+                          "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
                           "algo_gbs": round(algo / (ms * 1e-3) / 1e9, 1),
                           "line_gbs": round(n * (128 + 4) / (ms * 1e-3) / 1e9, 1),
                           "same_run_ceilings": ceil,

@@ -82,6 +82,7 @@ def test_set_conn_table_does_not_wait_for_a_foreign_stream(torch_cuda):
             t0 = time.perf_counter()
             c.set_conn_entries(tbl, m, t.max_conn_cnt)
             lat.append(time.perf_counter() - t0)
+        c.classify(frames, STRIDE, FRAME_OFF, n, res, mine)  # against e, the last table set
         mine.synchronize()
         still_running = spin.done() == 0
     finally:
@@ -90,7 +91,7 @@ def test_set_conn_table_does_not_wait_for_a_foreign_stream(torch_cuda):
     assert max(lat) < 0.5, f"pn_set_conn_table waited: {lat}"
     assert released == 1  # released by the host, not by its time limit
     got = res.cpu().numpy().view(pa.RESULT_DTYPE)
-    assert np.array_equal(got, exp)  # the last classify ran against table e (set before it)
+    assert np.array_equal(got, exp)
     c.close()
 
 
