@@ -6,7 +6,9 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CFLAGS_ORACLE = -O3 -march=x86-64-v3 -fPIC -Wall -std=c11
 
 LIB = pollnet_amd/libpollnet_amd.so
-SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip pollnet_amd/csrc/conn_table.cpp pollnet_amd/csrc/framegen.cpp
+SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip pollnet_amd/csrc/conn_table.cpp
+# the seeded workload generator (tests, bench): its own library, outside the product ABI
+GEN_LIB = pollnet_amd/libpollnet_amd_gen.so
 HDRS = include/pollnet_amd.h
 KHDRS = pollnet_amd/csrc/frame_pass.hpp pollnet_amd/csrc/device_common.hpp pollnet_amd/csrc/pn_internal.hpp \
   pollnet_amd/csrc/rx_classify.hpp pollnet_amd/csrc/tx_fill.hpp pollnet_amd/csrc/stream_match.hpp
@@ -49,7 +51,7 @@ REF_INCS = oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
 HAVE_REF_TEXT = $(or $(wildcard $(REFDIR)/example/tcpserver.cc),$(and $(wildcard oracle/_ref/tcpserver_handler.inc),$(wildcard oracle/_ref/tcpclient_handler.inc)))
 REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST))
 
-all: $(LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST)
+all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
@@ -89,13 +91,13 @@ $(GPUSTREAMTEST): tests/cpp/test_gpu_tcp_stream.cpp tests/cpp/segframes.hpp incl
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # RX-ring ingestion: socket batcher (+ loopback capture when permitted), ef_vi event rings on the GPU
-$(RINGTEST): tests/cpp/test_rx_ring.cpp include/pollnet_amd/rx_ring.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+$(RINGTEST): tests/cpp/test_rx_ring.cpp include/pollnet_amd/rx_ring.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # batch size vs throughput and latency of pn_classify (resident, host ring in/records out, hipGraph)
-$(LATBENCH): bench/bench_latency.cpp $(HDRS) $(LIB)
-	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+$(LATBENCH): bench/bench_latency.cpp $(HDRS) $(LIB) $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # poll() throughput (GPU-classified) vs the same host loop over the CPU release path
 $(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
@@ -110,16 +112,16 @@ $(SRVBENCH): bench/bench_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server
 	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
 # TX fill at small batch sizes, one in-place launch vs two phases (variant 41: make TUNING=1; not in `all`)
-$(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $(LIB) $(TUNING_LIB)
-	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+$(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $(LIB) $(TUNING_LIB) $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # completion by a polled word (pn_classify_notify) vs stream sync, small batches
-$(SIGBENCH): bench/bench_signal.cpp $(HDRS) $(LIB)
-	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+$(SIGBENCH): bench/bench_signal.cpp $(HDRS) $(LIB) $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # zero-copy classify from host rings of each pinned-memory kind: PCIe rate and staleness
-$(PINBENCH): bench/bench_pinned.cpp $(HDRS) $(LIB)
-	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+$(PINBENCH): bench/bench_pinned.cpp $(HDRS) $(LIB) $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
 # receive-side server loop on the GPU vs a sequential twin with reference semantics
 $(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_amd/gpu_tcp_rx.hpp \
@@ -132,12 +134,19 @@ $(RXCONNTEST): tests/cpp/test_rx_conn.cpp tests/cpp/segframes.hpp include/pollne
 	g++ -O2 -std=c++17 -Wall -o $@ $< -Loracle -loracle -ldl -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # standalone C++ adapter test (no torch): links the product library and, as the checker, the oracle
-$(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
-	$(HOSTHIP) -O2 -std=c++17 -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+$(CPPTEST): tests/cpp/test_gpu_rx.cpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 $(LIB): $(SRCS) $(HDRS) $(KHDRS)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS) -lpthread
+
+# clang (as hipcc): the generator's call arguments draw from one RNG, and the committed goldens
+# were made with clang's left-to-right argument evaluation (g++ evaluates right to left)
+CLANGXX ?= /opt/rocm/lib/llvm/bin/clang++
+$(GEN_LIB): pollnet_amd/csrc/framegen.cpp include/pollnet_amd_gen.h $(HDRS) $(LIB)
+	$(CLANGXX) -O3 -std=c++17 -fPIC -Wall -shared -o $@ pollnet_amd/csrc/framegen.cpp -Lpollnet_amd -lpollnet_amd -lpthread \
+	  -Wl,-rpath,'$$ORIGIN'
 
 $(TUNING_LIB): $(TUNING_SRCS) $(HDRS) include/pollnet_amd_tuning.h $(KHDRS)
 	$(HIPCC) $(HIPFLAGS) $(TUNING_FLAGS) -shared -o $@ $(TUNING_SRCS)
@@ -149,6 +158,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
 
 .PHONY: all ref clean

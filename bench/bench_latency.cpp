@@ -17,7 +17,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../include/pollnet_amd.h"
+#include "../include/pollnet_amd_gen.h"
 
 using Clock = std::chrono::steady_clock;
 

@@ -16,7 +16,7 @@
 #include <string>
 #include <vector>
 
-#include "../include/pollnet_amd.h"
+#include "../include/pollnet_amd_gen.h"
 #include "../include/pollnet_amd/gpu_rx.hpp"
 
 using Clock = std::chrono::steady_clock;

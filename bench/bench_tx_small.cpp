@@ -14,7 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "../include/pollnet_amd.h"
+#include "../include/pollnet_amd_gen.h"
 #include "../include/pollnet_amd_tuning.h"
 
 using Clock = std::chrono::steady_clock;

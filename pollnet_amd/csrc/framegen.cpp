@@ -1,4 +1,5 @@
-// Deterministic synthetic RX-ring generator for the BASELINE configs
+// Deterministic synthetic RX-ring generator for the BASELINE configs (libpollnet_amd_gen.so,
+// include/pollnet_amd_gen.h: workload tooling, not the product ABI)
 // (SURVEY.md §8d C2-C5).  Every frame is a pure function of (seed, global frame
 // index), so threads and ranks can generate disjoint shards of one batch.
 //
@@ -13,7 +14,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/pollnet_amd.h"
+#include "../../include/pollnet_amd_gen.h"
 
 namespace {
 

@@ -119,9 +119,22 @@ _pn_classify_notify = _sig("pn_classify_notify", _i32, _vp, _vp, _u32, _u32, _u3
 _pn_tx_fill_notify = _sig("pn_tx_fill_notify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp, _u32)
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
-_pn_gen_frames = _sig("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
-_pn_gen_conn_table = _sig("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)
-_pn_wire_bytes = _sig("pn_wire_bytes", _u64, _vp, _u32, _u32, _u32)
+
+# The seeded workload generator lives in its own library (include/pollnet_amd_gen.h), outside
+# the product ABI; loaded on first use.
+GEN_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpollnet_amd_gen.so")
+_gen = {}
+
+
+def _gen_fn(name, res, *args):
+    if not _gen:
+        if not os.path.exists(GEN_LIB_PATH):
+            raise ImportError(f"{GEN_LIB_PATH} not built: run `make`")
+        _gen["lib"] = ctypes.CDLL(GEN_LIB_PATH)
+    fn = getattr(_gen["lib"], name)
+    fn.restype = res
+    fn.argtypes = list(args)
+    return fn
 
 
 def _check(rc, ctx=None, what=""):
@@ -351,17 +364,19 @@ def gen_frames(params: GenParams, n: int, slot_stride: int = PN_RECV_BUF_SIZE, f
     assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= n * slot_stride
     threads = threads or min(16, os.cpu_count() or 1)
     p = params._c()
-    _check(_pn_gen_frames(_c.byref(p), first_index, n, out.ctypes.data, slot_stride, frame_off, threads), None, "pn_gen_frames")
+    gen = _gen_fn("pn_gen_frames", _i32, _c.POINTER(_GenParams), _u64, _u32, _vp, _u32, _u32, _i32)
+    _check(gen(_c.byref(p), first_index, n, out.ctypes.data, slot_stride, frame_off, threads), None, "pn_gen_frames")
     return out
 
 
 def gen_conn_table(params: GenParams, max_tw_cnt: int | None = None) -> ConnTable:
     t = ConnTable(params.max_conn_cnt, params.max_conn_cnt if max_tw_cnt is None else max_tw_cnt)
     p = params._c()
-    _check(_pn_gen_conn_table(_c.byref(p), t.handle), None, "pn_gen_conn_table")
+    _check(_gen_fn("pn_gen_conn_table", _i32, _c.POINTER(_GenParams), _vp)(_c.byref(p), t.handle), None,
+           "pn_gen_conn_table")
     return t
 
 
 def wire_bytes(slots: np.ndarray, slot_stride: int, frame_off: int, n: int) -> int:
     """Σ(14 + tot_len): the metric's numerator (wire frame bytes without FCS)."""
-    return int(_pn_wire_bytes(slots.ctypes.data, slot_stride, frame_off, n))
+    return int(_gen_fn("pn_wire_bytes", _u64, _vp, _u32, _u32, _u32)(slots.ctypes.data, slot_stride, frame_off, n))

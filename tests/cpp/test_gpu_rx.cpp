@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/pollnet_amd/gpu_rx.hpp"
+#include "../../include/pollnet_amd_gen.h"
 #include "../../oracle/pn_oracle.h"
 
 static int run(uint32_t cfg, uint32_t n, pollnet_amd::GpuRx::Mode mode, uint32_t chunk) {

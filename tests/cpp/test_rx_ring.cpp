@@ -27,6 +27,7 @@
 
 #include "../../include/pollnet_amd/gpu_rx.hpp"
 #include "../../include/pollnet_amd/rx_ring.hpp"
+#include "../../include/pollnet_amd_gen.h"
 #include "../../oracle/pn_oracle.h"
 
 using namespace pollnet_amd;

@@ -38,6 +38,14 @@ def test_product_exports_exactly_the_header():
     assert exported_functions(pa.LIB_PATH) == declared_functions()
 
 
+def test_generator_library_is_separate():
+    """The seeded workload generator is its own library (include/pollnet_amd_gen.h), outside the
+    product ABI."""
+    gen = set(exported_functions(pa.rx.GEN_LIB_PATH))
+    assert gen == set(declared_functions("pollnet_amd_gen.h")) == {"pn_gen_frames", "pn_gen_conn_table", "pn_wire_bytes"}
+    assert not gen & set(exported_functions(pa.LIB_PATH))
+
+
 def test_tuning_library_is_separate():
     from pollnet_amd import tuning
 
