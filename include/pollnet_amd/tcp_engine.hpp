@@ -152,9 +152,11 @@ inline uint16_t csum_fold(uint64_t s) { // CSum::fold (Core.h:94-98), carries fo
 // (Core.h:157-163, at the end of TcpConn::sendBuf, TcpConn.h:310-323) and pn_tx_fill(PN_TX_TCP)
 // writes.  A sum over these fields is never zero (IP version, protocol 6), so the folded value
 // is unique and any correct order of summation gives the same bytes.
+// A frame whose tot_len is below the bare headers (40) is left untouched, as pn_tx_fill leaves it.
 inline void fill_tcp_checksums(uint8_t* eth) {
   uint8_t* ip = eth + 14;
   const uint32_t tot_len = rd16(ip + 2), tcp_len = tot_len - 20;
+  if (tot_len < 40) return;
   ip[10] = ip[11] = 0;
   const uint16_t ip_sum = csum_fold(csum_add(ip, 20, 0));
   std::memcpy(ip + 10, &ip_sum, 2);

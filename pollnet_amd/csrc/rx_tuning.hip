@@ -364,18 +364,23 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
 }
 
 
-// pn_match_streams in either form (stream_match.hpp): V = 1 cooperative chunks through LDS,
-// V = 0 one lane per frame.  A/B by scripts/bench_streams.py.
+// pn_match_streams in either form (stream_match.hpp): 1 cooperative chunks through LDS, 0 one lane
+// per frame; 2-4 the cooperative form with nt / sc0 / sc1 loads.  A/B by scripts/bench_streams.py.
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant) {
-  if (n == 0 || (variant != 0 && variant != 1)) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  if (n == 0 || variant < 0 || variant > 4) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
   MatchArgs a;
   int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  if (variant == 1) launch_match<1>(a, frame_off, s);
-  else launch_match<0>(a, frame_off, s);
+  switch (variant) {
+    case 1: launch_match<1>(a, frame_off, s); break;
+    case 2: launch_match<1, 2>(a, frame_off, s); break;  // cooperative, nt loads
+    case 3: launch_match<1, 1>(a, frame_off, s); break;  // cooperative, sc0 loads
+    case 4: launch_match<1, 16>(a, frame_off, s); break; // cooperative, sc1 loads
+    default: launch_match<0>(a, frame_off, s);
+  }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "match variant launch");
   pn_internal::note_stream(ctx, s);

@@ -48,7 +48,8 @@ __device__ __host__ constexpr bool chunk_needed(int c) {
   return 16 * c < kPre + MIS + 24 && 16 * c + 16 > kPre + MIS - 2;
 }
 
-template <int MIS, int V>
+// LAUX: the cooperative loads' cache policy (tuning: whether L2 then fetches 64-B sectors, not lines).
+template <int MIS, int V, int LAUX = 0>
 __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
   Win<16> h;
@@ -69,7 +70,7 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
       u32x4 v = {0u, 0u, 0u, 0u};
       if ((c == 0 && chunk_needed<MIS>(0)) || (c == 1 && chunk_needed<MIS>(1)) || (c == 2 && chunk_needed<MIS>(2)) ||
           (c == 3 && chunk_needed<MIS>(3)))
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + 16 * c, 0, 0); // past n: zeros, no fetch
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + 16 * c, 0, LAUX); // past n: zeros, no fetch
       wt[r * 4 + (c ^ (r & 3))] = v;
     }
     __syncthreads();
@@ -117,18 +118,18 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 // The production form (A/B: scripts/bench_streams.py, tuning variant pn_match_streams_variant).
 constexpr int kMatchProd = 1;
 
-template <int V>
+template <int V, int LAUX = 0>
 void launch_match(const MatchArgs& a, uint32_t frame_off, hipStream_t s) {
   const dim3 grid((a.n + 255) / 256), block(256);
   switch ((frame_off + 14) & 15) {
-    case 0: hipLaunchKernelGGL((match_streams_kernel<0, V>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((match_streams_kernel<2, V>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((match_streams_kernel<4, V>), grid, block, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((match_streams_kernel<6, V>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((match_streams_kernel<8, V>), grid, block, 0, s, a); break;
-    case 10: hipLaunchKernelGGL((match_streams_kernel<10, V>), grid, block, 0, s, a); break;
-    case 12: hipLaunchKernelGGL((match_streams_kernel<12, V>), grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL((match_streams_kernel<14, V>), grid, block, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((match_streams_kernel<0, V, LAUX>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((match_streams_kernel<2, V, LAUX>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((match_streams_kernel<4, V, LAUX>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((match_streams_kernel<6, V, LAUX>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((match_streams_kernel<8, V, LAUX>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((match_streams_kernel<10, V, LAUX>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((match_streams_kernel<12, V, LAUX>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((match_streams_kernel<14, V, LAUX>), grid, block, 0, s, a); break;
   }
 }
 

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,3")
     ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--policies", action="store_true", help="also time the cooperative form's nt / sc0 / sc1 loads")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -64,6 +65,15 @@ def main():
             ts.append(timed(lambda d: ctx.match_streams(d, 2048, off, n, flt, ids, st)))
             ts0.append(timed(lambda d: tn.match_streams_variant(ctx, d, 2048, off, n, flt, ids0, 0, st)))
         ms, ms0 = statistics.median(ts), statistics.median(ts0)
+        pol = {}
+        if args.policies:
+            for v, name in ((2, "nt"), (3, "sc0"), (4, "sc1")):
+                ids_v = torch.empty_like(ids)
+                tn.match_streams_variant(ctx, dev[0], 2048, off, n, flt, ids_v, v, st)
+                torch.cuda.synchronize()
+                assert torch.equal(ids_v, ids)
+                pol[name] = round(statistics.median(
+                    timed(lambda d: tn.match_streams_variant(ctx, d, 2048, off, n, flt, ids_v, v, st)) for _ in range(args.rounds)), 5)
         # same-run ceiling for this access pattern: the first 64 / 128 B of every 2-KiB slot,
         # the RX kernel's load pattern, no arithmetic, nothing written
         sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
@@ -80,6 +90,7 @@ def main():
             ceil[f"slot_read_first_{nb}B_ms"] = round(statistics.median(cs), 5)
         algo = n * (64 + 4)
         out[f"c{cfg}"] = {"ids_equal_numpy": ok, "ms_median": round(ms, 5), "per_lane_form_ms_median": round(ms0, 5),
+                          "cooperative_load_policies_ms": pol,
                           "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
                           "algo_gbs": round(algo / (ms * 1e-3) / 1e9, 1),
                           "line_gbs": round(n * (128 + 4) / (ms * 1e-3) / 1e9, 1),

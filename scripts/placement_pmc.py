@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""C2 kernel time and counters by where the batch sits in HBM.
+
+K hipMalloc'd 2-GiB buffers get the same C2 frames; each is timed in interleaved rounds (HIP
+events), then classified 10 times in buffer order.  Run under `rocprofv3 --pmc ...` (one pass
+per counter set, scripts/placement_pmc.sh): the last K*10 rx_classify dispatches of the pass
+are that counter phase, mapped back to buffers by postprocessing (--summarize).  A
+measurement, not part of any product path.
+
+  placement_pmc.py run <out.json> [K]
+  placement_pmc.py summarize <root_dir_with_pass_dirs_and_run_jsons> > summary.json"""
+import csv
+import ctypes as C
+import glob
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+REPS = 10
+
+
+def run(out_path, k):
+    import torch
+
+    import pollnet_amd as pa
+
+    n, stride, off = 1 << 20, 2048, 2
+    p = pa.rx.GenParams.for_config(2)
+    s = pa.gen_frames(p, n, stride, off)
+    ctx = pa.RxContext(0)
+    ctx.set_conn_table(pa.gen_conn_table(p))
+    src = torch.from_numpy(s.reshape(-1)).cuda()
+    hip = C.CDLL("libamdhip64.so.7")
+    ptrs = []
+    for _ in range(k):
+        ptr = C.c_void_p()
+        assert hip.hipMalloc(C.byref(ptr), C.c_size_t(n * stride)) == 0
+        assert hip.hipMemcpy(ptr, C.c_void_p(src.data_ptr()), C.c_size_t(n * stride), 3) == 0
+        ptrs.append(ptr.value)
+    torch.cuda.synchronize()
+    ref = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    res = torch.empty_like(ref)
+    st = torch.cuda.current_stream()
+    ctx.classify(src, stride, off, n, ref, st)
+    for q in ptrs:
+        ctx.classify(q, stride, off, n, res, st)
+        torch.cuda.synchronize()
+        assert torch.equal(res, ref)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = [[] for _ in ptrs]
+    for _ in range(5):
+        for i, q in enumerate(ptrs):
+            ev[0].record(st)
+            for _ in range(20):
+                ctx.classify(q, stride, off, n, res, st)
+            ev[1].record(st)
+            torch.cuda.synchronize()
+            times[i].append(ev[0].elapsed_time(ev[1]) / 20)
+    for q in ptrs:  # the counter phase: REPS dispatches per buffer, in buffer order
+        for _ in range(REPS):
+            ctx.classify(q, stride, off, n, res, st)
+    torch.cuda.synchronize()
+    out = {"frames": n, "reps_per_buffer": REPS,
+           "buffers": [{"addr": hex(q), "ms_median": round(statistics.median(t), 5)} for q, t in zip(ptrs, times)]}
+    with open(out_path, "w") as f:
+        json.dump(out, f, indent=1)
+    for q in ptrs:
+        hip.hipFree(C.c_void_p(q))
+
+
+def summarize(root):
+    """Per pass directory <root>/<name>/ (rocprofv3 csv) + <root>/<name>.run.json: counters per buffer."""
+    out = {}
+    for run_json in sorted(glob.glob(os.path.join(root, "*.run.json"))):
+        name = os.path.basename(run_json)[: -len(".run.json")]
+        meta = json.load(open(run_json))
+        rows = []
+        for f in glob.glob(os.path.join(root, name, "**", "*counter_collection.csv"), recursive=True):
+            rows += [r for r in csv.DictReader(open(f)) if "rx_classify" in r.get("Kernel_Name", "")]
+        per = {}
+        for r in rows:
+            did = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            per.setdefault(did, {}).setdefault(r["Counter_Name"], 0.0)
+            per[did][r["Counter_Name"]] += float(r["Counter_Value"])
+        k, reps = len(meta["buffers"]), meta["reps_per_buffer"]
+        dids = sorted(per)[-k * reps:]
+        bufs = []
+        for i, b in enumerate(meta["buffers"]):
+            ds = dids[i * reps:(i + 1) * reps]
+            counters = {c: statistics.median(per[d][c] for d in ds) for c in per[ds[0]]}
+            bufs.append({**b, **counters})
+        out[name] = bufs
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 8)
+    else:
+        summarize(sys.argv[2])

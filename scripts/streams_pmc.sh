@@ -7,7 +7,7 @@ TAG=${1:-streams_pmc}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="scripts/bench_streams.py --configs 2 --rounds 3"
+B="scripts/bench_streams.py --configs 2 --rounds 3 --policies"
 pass() {  # name, counters...
   local name=$1; shift
   timeout -k 10 180 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o pmc -- python3 $B > $OUT/$name.json 2> $OUT/$name.err \
