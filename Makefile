@@ -15,7 +15,7 @@ KHDRS = pollnet_amd/csrc/frame_pass.hpp pollnet_amd/csrc/device_common.hpp polln
 # measurement-only library (bench ceilings; A/B variants with TUNING=1): never loaded by the product
 TUNING_LIB = pollnet_amd/libpollnet_amd_tuning.so
 TUNING_SRCS = pollnet_amd/csrc/rx_tuning.hip pollnet_amd/csrc/tx_tuning.hip
-TUNING ?= 0
+TUNING ?= 1
 ifeq ($(TUNING),1)
 TUNING_FLAGS = -DPN_TUNING_VARIANTS
 endif

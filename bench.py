@@ -445,24 +445,37 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
     torch.cuda.synchronize()
     k = min(n, 65536)
     ok = bool(np.array_equal(ids[:k].cpu().numpy().view(np.uint32), match_streams_np(slots[:k], FRAME_OFF, flt)))
+    from pollnet_amd import tuning as tn  # measurement-only library: the same-pattern ceiling
+
     R = len(frames_b)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ts = []
-    for _ in range(5):
+    sink = torch.empty_like(ids)
+
+    def timed(fn):
         ev[0].record(stream)
         for r in range(20):
-            ctx.match_streams(frames_b[r % R], STRIDE, FRAME_OFF, n, flt, ids, stream)
+            fn(frames_b[r % R])
         ev[1].record(stream)
         torch.cuda.synchronize()
-        ts.append(ev[0].elapsed_time(ev[1]) / 20)
-    ms = statistics.median(ts)
+        return ev[0].elapsed_time(ev[1]) / 20
+
+    ts, tg = [], []
+    for _ in range(5):  # the product and its loads alone (tuning variant 5), alternately
+        ts.append(timed(lambda d: ctx.match_streams(d, STRIDE, FRAME_OFF, n, flt, ids, stream)))
+        tg.append(timed(lambda d: tn.match_streams_variant(ctx, d, STRIDE, FRAME_OFF, n, flt, sink, 5, stream)))
+    ms, mg = statistics.median(ts), statistics.median(tg)
+    pmc = load_pmc(f"match_streams_c2_n{n}")
     return {"kernel": "match_streams_kernel", "frames": n, "resident_batches": R, "filters": 8, "kernel_ms": round(ms, 5),
             "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
             "algorithmic_bytes_per_launch": n * (64 + 4),
             "achieved_gbs": round(n * (64 + 4) / (ms * 1e-3) / 1e9, 1),
-            "line_gbs": round(n * (128 + 4) / (ms * 1e-3) / 1e9, 1),
+            "frac": round(n * (64 + 4) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
+            "traffic_gbs": None if pmc is None else round(pmc["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1),
+            "gather_loads_only_ms": round(mg, 5), "kernel_vs_gather_ceiling": round(mg / ms, 4),
             "first_65536_ids_vs_numpy": ok,
-            "note": "one 128-B line per 2-KiB slot is a strided gather; DESIGN §11 compares it with the same-pattern ceiling"}
+            "note": "one 128-B line per 2-KiB slot (PMC: every request 128 B); the ceiling is the same kernel's loads "
+                    "and LDS round trip alone (DESIGN §11)"}
 
 
 def server_poll():

@@ -3,7 +3,7 @@
  *
  * NOT part of the product ABI (include/pollnet_amd.h) and never loaded by the product
  * path: same-run bandwidth ceilings that bench.py reports beside the production kernel,
- * and (built with `make TUNING=1` only) the A/B variants of the RX and TX kernels that
+ * and (unless built with `make TUNING=0`) the A/B variants of the RX and TX kernels that
  * scripts/variants.py / scripts/tx_variants.py time.  Contexts come from pn_open().
  */
 #ifndef POLLNET_AMD_TUNING_H
@@ -41,7 +41,8 @@ int pn_calib_classify_ablated(pn_ctx* ctx, const void* frames_dev, uint32_t slot
 int pn_calib_tx_ablated(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n, void* stream);
 
 /* pn_match_streams in either kernel form: variant 1 = 4 lanes per frame load its header chunks
- * through LDS (production), 0 = one lane per frame loads its own (scripts/bench_streams.py). */
+ * through LDS (production), 0 = one lane per frame loads its own, 2-4 = variant 1 with nt / sc0 / sc1
+ * loads, 5 = variant 1's loads alone (timing-only same-pattern ceiling; ids not written). */
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant);
@@ -51,7 +52,7 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
  * pinned host memory.  Unrelated work in flight on a foreign stream (tests/test_gpu_notify.py). */
 int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max_ms, void* stream);
 
-/* ---- A/B variants (make TUNING=1; ids documented at their definitions) ---- */
+/* ---- A/B variants (built by default, TUNING=1; ids documented at their definitions) ---- */
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                         void* results_dev, void* stream, int variant);
 int pn_classify_indexed_variant(pn_ctx* ctx, const void* base, const uint64_t* offsets, uint32_t eth_mod16, uint32_t n,

@@ -57,6 +57,10 @@ enum : int { kSkipWaveGate = 16384 };
 // C5 -3.9 % (0.1660 -> 0.1596 ms; the probe's share over the no-probe ablation 13.6 -> 7.2 us),
 // C3 equal (profiles/r03/probe_group_c{3,5}.json).
 enum : int { kGroupProbe = 32768 };
+// With kCoopProbe: the home slot and the 3 entries after it are loaded together (one L2 round
+// trip) and resolved in registers; only runs longer than that go to the cooperative walk.  Without
+// it the home slot comes first and a lane whose run goes on fetches 2 more (two round trips).
+enum : int { kProbeAhead4 = 2048 };
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 

@@ -88,6 +88,10 @@ struct FrameState {
 };
 
 // connHashKey (Core.h:167-172) and the load of the home slot `key & tbl_mask` (Core.h:558-559).
+// kProbeAhead4: the home slot and the next 3 entries in one round trip, walked in registers as
+// findConnEntry walks them (Core.h:560-561): the probe stops at the first entry with key >= the
+// lane's key or at the array end; a run going on past them leaves e at the last one loaded.
+template <int ABL>
 __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port, bool live, const KArgs& a) {
   Probe p;
   const uint32_t ip_h = __builtin_bswap32(src_ip);
@@ -96,7 +100,31 @@ __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port,
   p.e = (uint32_t)(p.key & a.mask);
   p.k = PN_EMPTY_KEY;
   p.cid = 0;
-  if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
+  if constexpr ((ABL & kProbeAhead4) && (ABL & kCoopProbe)) {
+    if (live && p.e < a.n_entries) {
+      u32x4 ent[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ent[j] = u32x4{0u, 0x80000000u, 0u, 0u}; // PN_EMPTY_KEY past the array end: stops the walk
+        if (p.e + j < a.n_entries) ent[j] = *reinterpret_cast<const u32x4*>(a.tbl + p.e + j);
+      }
+      // the first of the 4 whose key is >= the lane's key (walking backwards keeps the first)
+      uint32_t stop = 4;
+#pragma unroll
+      for (int j = 3; j >= 0; --j)
+        if (p.e + j >= a.n_entries || (((uint64_t)ent[j].y << 32) | ent[j].x) >= p.key) stop = j;
+      const uint32_t j = stop < 4 ? stop : 3;
+      const u32x4 pick = j == 0 ? ent[0] : j == 1 ? ent[1] : j == 2 ? ent[2] : ent[3];
+      if (p.e + j < a.n_entries) {
+        p.k = ((uint64_t)pick.y << 32) | pick.x;
+        p.cid = pick.z;
+      } else {
+        p.k = PN_EMPTY_KEY; // the walk ran off the array: e == n_entries below ends it as a miss
+      }
+      p.e += j;
+      if (p.e >= a.n_entries) p.e = a.n_entries;
+    }
+  } else if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
     const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + p.e);
     p.k = ((uint64_t)ent.y << 32) | ent.x;
     p.cid = ent.z;
@@ -119,7 +147,7 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
     // walk stops at.
     const uint32_t lane = threadIdx.x;
     bool srch = live && e < a.n_entries && k < key;
-    if (__ballot(srch) != 0) {
+    if (!(ABL & kProbeAhead4) && __ballot(srch) != 0) {
       // short runs (the common case past the home slot): every searching lane fetches its
       // next kAhead entries at once -- one round trip for all of them, in parallel
       constexpr int kAhead = 2;
@@ -271,7 +299,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   // (Resolving the probe after phase 2 instead, so the home-slot load overlaps the stream loads,
   // measured no faster: profiles/r02/s3/late_probe_ab.json.)
   st.conn_id = PN_MISS;
-  if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
+  if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue<ABL>(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
   st.flags = flags;
   return st;
 }

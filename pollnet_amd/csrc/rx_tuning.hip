@@ -2,7 +2,7 @@
 // A/B variants (scripts/variants.py, history in profiles/r01_experiments) and the
 // same-run bandwidth ceilings bench.py reports beside the production kernel.  Never
 // linked into or loaded by the product path; the variants are compiled only with
-// `make TUNING=1` (-DPN_TUNING_VARIANTS).
+// `make` (TUNING=1 by default: -DPN_TUNING_VARIANTS; `make TUNING=0` leaves them out).
 #include "rx_classify.hpp"
 #include "stream_match.hpp"
 
@@ -281,6 +281,8 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     // in the history)
     case 38: launch_one<0, 1, kProdAbl | kGroupProbe>(a, s); break;  // cluster lanes resolved per run position
     case 39: launch_one<0, 1, kProdAbl & ~kGroupProbe>(a, s); break; // one lane per round trip past kAhead
+    case 40: launch_one<0, 1, kProdAbl | kProbeAhead4>(a, s); break;  // home slot + 3 in one round trip
+    case 41: launch_one<0, 1, (kProdAbl | kProbeAhead4) & ~kGroupProbe>(a, s); break;
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
@@ -365,11 +367,11 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
 
 
 // pn_match_streams in either form (stream_match.hpp): 1 cooperative chunks through LDS, 0 one lane
-// per frame; 2-4 the cooperative form with nt / sc0 / sc1 loads.  A/B by scripts/bench_streams.py.
+// per frame; 2-4 the cooperative form with nt / sc0 / sc1 loads; 5 its loads alone (a ceiling).  A/B by scripts/bench_streams.py.
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant) {
-  if (n == 0 || variant < 0 || variant > 4) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  if (n == 0 || variant < 0 || variant > 5) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
   MatchArgs a;
   int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
   if (rc) return rc;
@@ -379,6 +381,7 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
     case 2: launch_match<1, 2>(a, frame_off, s); break;  // cooperative, nt loads
     case 3: launch_match<1, 1>(a, frame_off, s); break;  // cooperative, sc0 loads
     case 4: launch_match<1, 16>(a, frame_off, s); break; // cooperative, sc1 loads
+    case 5: launch_match<2>(a, frame_off, s); break;     // timing-only ceiling: the same loads, no compare or store
     default: launch_match<0>(a, frame_off, s);
   }
   hipError_t e = hipGetLastError();

@@ -53,7 +53,7 @@ template <int MIS, int V, int LAUX = 0>
 __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
   const uint32_t f = blockIdx.x * 256 + threadIdx.x;
   Win<16> h;
-  if constexpr (V == 1) {
+  if constexpr (V >= 1) {
     // wave w of the workgroup: frames f0 .. f0 + 63; instruction i: lane l loads chunk l & 3 of
     // frame f0 + 16 i + (l >> 2)
     __shared__ u32x4 tile[256 * 4];
@@ -95,6 +95,13 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
       h.d[4 * c + 2] = v.z;
       h.d[4 * c + 3] = v.w;
     }
+  }
+  if constexpr (V == 2) { // timing only: the loads and the LDS round trip, no compare, (almost) no store
+    uint32_t x = 0;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) x ^= h.d[q];
+    if (x == 0x9E3779B9u) a.out[f] = x;
+    return;
   }
   constexpr int IP = kPre + MIS;
   const uint32_t ether_type = h.template u16<IP - 2>(); // as stored: 0x0008 for IPv4

@@ -1,5 +1,5 @@
 // Tuning library: A/B variants of the TX fill (scripts/tx_variants.py), compiled only with
-// `make TUNING=1`.  Never part of the product library.
+// `make` (TUNING=1 by default).  Never part of the product library.
 #include "tx_fill.hpp"
 
 // Same-run ceiling for pn_tx_fill (bench.py): the production launches (the fill kernel with

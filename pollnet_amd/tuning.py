@@ -2,7 +2,7 @@
 
 Measurement only — never imported by the product path: the same-run bandwidth ceilings
 that bench.py reports beside the production kernel, and (library built with
-``make TUNING=1``) the A/B kernel variants the scripts under scripts/ time.  Every call
+``make``, unless ``TUNING=0``) the A/B kernel variants the scripts under scripts/ time.  Every call
 takes an open ``RxContext`` (pn_open)."""
 from __future__ import annotations
 
@@ -43,7 +43,7 @@ _tx_variant = _sig("pn_tx_fill_variant", _i32, _vp, _vp, _u32, _u32, _u32, _vp, 
 
 def _need(fn, name):
     if fn is None:
-        raise rx.PollnetError(f"{name} needs the tuning library built with `make TUNING=1`")
+        raise rx.PollnetError(f"{name} needs the tuning library built with its variants (`make`, not `make TUNING=0`)")
     return fn
 
 

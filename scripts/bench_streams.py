@@ -60,11 +60,12 @@ def main():
             torch.cuda.synchronize()
             return ev[0].elapsed_time(ev[1]) / reps
 
-        ts, ts0 = [], []
-        for _ in range(args.rounds):  # interleaved: production, per-lane form
+        ts, ts0, tg = [], [], []
+        for _ in range(args.rounds):  # interleaved: production, per-lane form, the production loads alone
             ts.append(timed(lambda d: ctx.match_streams(d, 2048, off, n, flt, ids, st)))
             ts0.append(timed(lambda d: tn.match_streams_variant(ctx, d, 2048, off, n, flt, ids0, 0, st)))
-        ms, ms0 = statistics.median(ts), statistics.median(ts0)
+            tg.append(timed(lambda d: tn.match_streams_variant(ctx, d, 2048, off, n, flt, ids0, 5, st)))
+        ms, ms0, mg = statistics.median(ts), statistics.median(ts0), statistics.median(tg)
         pol = {}
         if args.policies:
             for v, name in ((2, "nt"), (3, "sc0"), (4, "sc1")):
@@ -94,7 +95,8 @@ def main():
                           "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
                           "algo_gbs": round(algo / (ms * 1e-3) / 1e9, 1),
                           "line_gbs": round(n * (128 + 4) / (ms * 1e-3) / 1e9, 1),
-                          "same_run_ceilings": ceil,
+                          "same_run_ceilings": dict(ceil, gather_loads_only_ms=round(mg, 5),
+                                                    kernel_vs_gather_ceiling=round(mg / ms, 4)),
                           "note": "algo = 64-B header window + 4-B id per frame; line = the 128-B line it lives in"}
         ctx.close()
         del dev

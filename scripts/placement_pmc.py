@@ -8,7 +8,11 @@ are that counter phase, mapped back to buffers by postprocessing (--summarize). 
 measurement, not part of any product path.
 
   placement_pmc.py run <out.json> [K]
-  placement_pmc.py summarize <root_dir_with_pass_dirs_and_run_jsons> > summary.json"""
+  placement_pmc.py summarize <root_dir_with_pass_dirs_and_run_jsons> > summary.json
+  placement_pmc.py orders <out.json> [K]   (no profiler) per buffer: the product kernel (XCD-contiguous
+      group order), the same kernel in blockIdx order (tuning variant 36) and a plain stream read of
+      the buffer, interleaved rounds -- is a slow placement slow for every access order, and for a
+      front-to-back read of all its bytes?"""
 import csv
 import ctypes as C
 import glob
@@ -96,8 +100,55 @@ def summarize(root):
     print(json.dumps(out, indent=1))
 
 
+def orders(out_path, k):
+    import torch
+
+    import pollnet_amd as pa
+    from pollnet_amd import tuning as tn
+
+    n, stride, off = 1 << 20, 2048, 2
+    p = pa.rx.GenParams.for_config(2)
+    s = pa.gen_frames(p, n, stride, off)
+    ctx = pa.RxContext(0)
+    ctx.set_conn_table(pa.gen_conn_table(p))
+    src = torch.from_numpy(s.reshape(-1)).cuda()
+    hip = C.CDLL("libamdhip64.so.7")
+    ptrs = []
+    for _ in range(k):
+        ptr = C.c_void_p()
+        assert hip.hipMalloc(C.byref(ptr), C.c_size_t(n * stride)) == 0
+        assert hip.hipMemcpy(ptr, C.c_void_p(src.data_ptr()), C.c_size_t(n * stride), 3) == 0
+        ptrs.append(ptr.value)
+    torch.cuda.synchronize()
+    res = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+    legs = {"product_xcd_order": lambda q: ctx.classify(q, stride, off, n, res, st),
+            "blockidx_order": lambda q: tn.classify_variant(ctx, q, stride, off, n, res, st, 36),
+            "stream_read": lambda q: tn.calib_stream_read(ctx, q, n * stride, sink, st)}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = [{name: [] for name in legs} for _ in ptrs]
+    for _ in range(7):
+        for i, q in enumerate(ptrs):
+            for name, fn in legs.items():
+                fn(q)
+                ev[0].record(st)
+                for _ in range(10):
+                    fn(q)
+                ev[1].record(st)
+                torch.cuda.synchronize()
+                times[i][name].append(ev[0].elapsed_time(ev[1]) / 10)
+    out = {"frames": n, "buffers": [{"addr": hex(q), **{name: round(statistics.median(t), 5) for name, t in ts.items()}}
+                                    for q, ts in zip(ptrs, times)]}
+    with open(out_path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 8)
+    elif sys.argv[1] == "orders":
+        orders(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 12)
     else:
         summarize(sys.argv[2])
