@@ -145,9 +145,70 @@ def orders(out_path, k):
     print(json.dumps(out, indent=1))
 
 
+def alloc(out_path, pattern):
+    """Buffers allocated in the order `pattern` (t = torch.empty, the bench's way; h = hipMalloc;
+    T = torch.from_numpy(host).to("cuda"), exactly bench.py's upload), each filled with the same C2
+    frames, then the product kernel timed on each in interleaved rounds: does the allocation path
+    or the allocation order decide the slow placement?"""
+    import numpy as np
+    import torch
+
+    import pollnet_amd as pa
+
+    n, stride, off = 1 << 20, 2048, 2
+    p = pa.rx.GenParams.for_config(2)
+    s = pa.gen_frames(p, n, stride, off)
+    ctx = pa.RxContext(0)
+    ctx.set_conn_table(pa.gen_conn_table(p))
+    hip = C.CDLL("libamdhip64.so.7")
+    bufs, keep = [], []
+    src = None
+    for kind in pattern:
+        if kind == "T":
+            b = torch.from_numpy(s.reshape(-1)).to("cuda")
+            keep.append(b)
+            bufs.append(("T", b.data_ptr()))
+        elif kind == "t":
+            b = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+            keep.append(b)
+            bufs.append(("t", b.data_ptr()))
+        else:
+            ptr = C.c_void_p()
+            assert hip.hipMalloc(C.byref(ptr), C.c_size_t(n * stride)) == 0
+            bufs.append(("h", ptr.value))
+        if src is None and kind == "T":
+            src = keep[-1]
+    if src is None:
+        src = torch.from_numpy(s.reshape(-1)).to("cuda")
+    for kind, q in bufs:
+        if q != src.data_ptr():
+            assert hip.hipMemcpy(C.c_void_p(q), C.c_void_p(src.data_ptr()), C.c_size_t(n * stride), 3) == 0
+    torch.cuda.synchronize()
+    res = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    times = [[] for _ in bufs]
+    for _ in range(7):
+        for i, (_, q) in enumerate(bufs):
+            ctx.classify(q, stride, off, n, res, st)
+            ev[0].record(st)
+            for _ in range(10):
+                ctx.classify(q, stride, off, n, res, st)
+            ev[1].record(st)
+            torch.cuda.synchronize()
+            times[i].append(ev[0].elapsed_time(ev[1]) / 10)
+    out = {"pattern": pattern, "buffers": [{"kind": k, "addr": hex(q), "ms": round(statistics.median(t), 5)}
+                                           for (k, q), t in zip(bufs, times)]}
+    with open(out_path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 8)
+    elif sys.argv[1] == "alloc":
+        alloc(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "orders":
         orders(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 12)
     else:
