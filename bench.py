@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C5/packed/TX sub-measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg")
+    ap.add_argument("--stream-ceiling-only", action="store_true",
+                    help="PMC passes (scripts/gpu_pmc.sh): only the stream-read calibration, no ablated kernel "
+                         "(its dispatches share the RX kernel's name)")
     ap.add_argument("--batches", type=int, default=4,
                     help="distinct resident batches the steps rotate over (defeats reuse of a fixed slice of "
                          "the 256 MiB memory-side cache across launches)")
@@ -279,7 +282,7 @@ def e2e_zero_copy(torch, ctx, slots, n, passes=3):
             "note": "pn_classify on pinned host 2048-B slots (zero copy), records to pinned host memory"}, host_res
 
 
-def ceilings(torch, ctx, bufs, n, res, stream, steps=20, rounds=3):
+def ceilings(torch, ctx, bufs, n, res, stream, steps=20, rounds=3, stream_only=False):
     """Same-run ceilings (kernels of the measurement-only tuning library, never the product path):
     the plain front-to-back stream read of one resident batch, and the tight one -- the production
     kernel with the conn-table probe and the lane reduction ablated (same window and stream loads,
@@ -298,6 +301,8 @@ def ceilings(torch, ctx, bufs, n, res, stream, steps=20, rounds=3):
     ev[1].record(stream)
     torch.cuda.synchronize()
     ts = ev[0].elapsed_time(ev[1]) / 10 * 1e-3
+    if stream_only:
+        return {"stream_read_gbs": round(bufs[0].numel() / ts / 1e9, 1)}
     prod, abl = [], []
     for _ in range(rounds):
         prod.append(time_launches(torch, lambda d: ctx.classify(d, STRIDE, FRAME_OFF, n, res, stream), bufs, steps,
@@ -760,7 +765,8 @@ def run_rank(rank, world, local_rank, args):
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
     if rank == 0 and world == 1:
-        out["roofline"]["same_run_ceilings"] = ceilings(torch, ctx, frames_b, n, res, stream)
+        out["roofline"]["same_run_ceilings"] = ceilings(torch, ctx, frames_b, n, res, stream,
+                                                        stream_only=args.stream_ceiling_only)
     if rank == 0 and world == 1 and not args.no_secondary and cfg == 2 and n == 1 << 20:
         t_sec = time.perf_counter()
         sec = {}

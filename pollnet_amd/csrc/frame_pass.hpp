@@ -61,6 +61,9 @@ enum : int { kGroupProbe = 32768 };
 // trip) and resolved in registers; only runs longer than that go to the cooperative walk.  Without
 // it the home slot comes first and a lane whose run goes on fetches 2 more (two round trips).
 enum : int { kProbeAhead4 = 2048 };
+// Tuning: kLateProbe issues the home-slot load in phase 1 and finishes the walk after phase 2 (the
+// round trip under the stream loads); kAblNoWalk (timing only) stops every probe at its home slot.
+enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 

@@ -85,6 +85,7 @@ struct FrameState {
   int end_rel;    // summed extent relative to the window start (even), | 1 when tcp_len is odd; 0 = nothing to stream
   uint32_t pad;   // odd tcp_len: the byte after the segment (kPadUnknown until phase 2 captured it)
   bool trunc;
+  Probe probe; // kLateProbe: the issued probe, finished after phase 2
 };
 
 // connHashKey (Core.h:167-172) and the load of the home slot `key & tbl_mask` (Core.h:558-559).
@@ -140,7 +141,9 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
   uint32_t e = p.e;
   uint64_t k = p.k;
   uint32_t cid = p.cid;
-  if constexpr (ABL & kCoopProbe) {
+  if constexpr (ABL & kAblNoWalk) {
+    // timing only: the home slot decides
+  } else if constexpr (ABL & kCoopProbe) {
     // Lanes whose run continues past the home slot are served one at a time by the whole
     // wave (all 64 lanes reach here): 64 consecutive entries per round trip, the first with
     // key >= the lane's key (or the array end) found by a ballot -- the entry the scalar
@@ -299,7 +302,8 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   // (Resolving the probe after phase 2 instead, so the home-slot load overlaps the stream loads,
   // measured no faster: profiles/r02/s3/late_probe_ab.json.)
   st.conn_id = PN_MISS;
-  if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue<ABL>(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
+  if constexpr (ABL & kLateProbe) st.probe = probe_issue<ABL>(st.src_ip, src_port, live, a);
+  else if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue<ABL>(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
   st.flags = flags;
   return st;
 }
@@ -485,6 +489,7 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
   } else {
     stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
   }
+  if constexpr (ABL & kLateProbe) probe_finish<ABL>(st.probe, live && !bad_off, a, st.conn_id, st.flags);
   if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
 }
 

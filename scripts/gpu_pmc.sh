@@ -9,7 +9,7 @@ CFG=${2:-2}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-B="bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-secondary"
+B="bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-secondary --stream-ceiling-only"
 pass() {  # name, counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o pmc -- python3 $B > $OUT/$name.json 2> $OUT/$name.err \
