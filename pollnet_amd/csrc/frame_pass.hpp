@@ -64,6 +64,12 @@ enum : int { kProbeAhead4 = 2048 };
 // Tuning: kLateProbe issues the home-slot load in phase 1 and finishes the walk after phase 2 (the
 // round trip under the stream loads); kAblNoWalk (timing only) stops every probe at its home slot.
 enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
+// kPipeProbe: the probe's dependent round trips are software-pipelined into phase 2 — the home-slot
+// load is issued in phase 1 and resolved after the first stream batch's loads are issued, the next-2
+// fetch of colliding lanes is issued there and resolved after the second batch's loads; only runs
+// longer than that walk after phase 2.  Each round trip overlaps a stream batch instead of sitting
+// between phase 1 and phase 2.
+enum : int { kPipeProbe = 65536 };
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 
@@ -209,9 +215,15 @@ __device__ __forceinline__ uint32_t stream_start(uint64_t w) { return 112u - (((
 // group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
 // frame with readlane); the total of frame fi lands on lane fi.  The header lane
 // has summed the window below stream_start (window_part).
-template <int ABL, int LAUX, int IDX>
+struct NoHook {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+
+// hook(b) runs right after batch b's loads are issued (b = 0, 1, ... while batches remain; hooks 0 and 1
+// always run, after the loop if the wave has fewer batches): kPipeProbe's probe steps.
+template <int ABL, int LAUX, int IDX, class Hook = NoHook>
 __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
-                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
+                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad, Hook hook = Hook()) {
   // window start of frame fi: strided from the group's first slot, or (indexed) the
   // address its own lane computed, broadcast with two readlanes
   auto frame_win = [&](uint32_t fi) -> const uint8_t* {
@@ -250,6 +262,7 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       }
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
+    if (b0 < 2 * kBatch) hook((int)(b0 / kBatch));
     auto sel = [](int e, int o) -> uint32_t {
       if constexpr (ABL & (kAblNoMask | kExactRange)) return 0x10001u;
       else return tail_sel(e, o);
@@ -337,6 +350,7 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
     }
   }
+  if (n_here <= kBatch) hook(1); // one batch only (n_here >= 1): the second probe step still runs
 }
 
 } // namespace pn_dev

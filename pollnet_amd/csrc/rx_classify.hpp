@@ -133,6 +133,48 @@ __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port,
   return p;
 }
 
+// kPipeProbe: the next-2 fetch of the lanes whose run goes on past the home slot, split into its issue
+// (after the first stream batch's loads) and its resolution (after the second's); the same entries and
+// the same stopping rule as probe_finish's kAhead step.
+struct ProbeAhead {
+  u32x4 nx[2];
+  bool srch, any;
+};
+__device__ __forceinline__ void pp_issue_ahead(const Probe& p, bool live, const KArgs& a, ProbeAhead& q) {
+  q.srch = live && p.e < a.n_entries && p.k < p.key; // waits for the home-slot load here
+  q.any = __ballot(q.srch) != 0;
+  if (q.any) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      q.nx[j] = u32x4{0u, 0u, 0u, 0u};
+      if (q.srch && p.e + 1 + j < a.n_entries) q.nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + p.e + 1 + j);
+    }
+  }
+}
+__device__ __forceinline__ void pp_resolve_ahead(Probe& p, const KArgs& a, const ProbeAhead& q) {
+  if (!q.any) return;
+  uint32_t step = 0, cid2 = 0;
+  uint64_t k2 = 0;
+#pragma unroll
+  for (int j = 1; j >= 0; --j) { // the first entry (in order) that stops the walk
+    const uint64_t kk = ((uint64_t)q.nx[j].y << 32) | q.nx[j].x;
+    if (p.e + 1 + j >= a.n_entries || kk >= p.key) {
+      step = j + 1;
+      k2 = kk;
+      cid2 = q.nx[j].z;
+    }
+  }
+  if (q.srch) {
+    if (step != 0) {
+      p.e += step;
+      p.k = k2;
+      p.cid = cid2;
+    } else {
+      p.e += 2; // every fetched key < key: the run goes on (p.k stays below the key)
+    }
+  }
+}
+
 // The rest of findConnEntry's ordered walk (Core.h:560-561) and the conn / TIME_WAIT / miss
 // verdict (Core.h:510).  Every lane of the wave must call it (the cooperative walk ballots).
 template <int ABL>
@@ -302,7 +344,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   // (Resolving the probe after phase 2 instead, so the home-slot load overlaps the stream loads,
   // measured no faster: profiles/r02/s3/late_probe_ab.json.)
   st.conn_id = PN_MISS;
-  if constexpr (ABL & kLateProbe) st.probe = probe_issue<ABL>(st.src_ip, src_port, live, a);
+  if constexpr (ABL & (kLateProbe | kPipeProbe)) st.probe = probe_issue<ABL>(st.src_ip, src_port, live, a);
   else if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue<ABL>(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
   st.flags = flags;
   return st;
@@ -477,19 +519,35 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
       }
     }
     st.t_all += sum;
-  } else if constexpr ((ABL & kSkipWaveGate) && (ABL & kSkipEmptyLoads)) {
-    // a frame whose extent ends before its second stream KiB: take the skipping form
-    const uint32_t e16 = (uint32_t)((st.end_rel & ~1) + 3) & ~3u;
-    const bool short_frame = live && e16 <= stream_start((uint64_t)win) + 1024;
-    constexpr int kFull = ABL & ~(kSkipEmptyLoads | kSkipWaveGate);
-    if (__ballot(short_frame) == 0)
-      stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
-    else
-      stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
   } else {
-    stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all, st.pad);
+    // kPipeProbe: the probe's steps ride on the first two stream batches (hook); otherwise no hook
+    ProbeAhead q{};
+    const bool plive = live && !bad_off;
+    auto probe_hook = [&](int b) {
+      if constexpr (ABL & kPipeProbe) {
+        if (b == 0) pp_issue_ahead(st.probe, plive, a, q);
+        else pp_resolve_ahead(st.probe, a, q);
+      }
+    };
+    if constexpr ((ABL & kSkipWaveGate) && (ABL & kSkipEmptyLoads)) {
+      // a frame whose extent ends before its second stream KiB: take the skipping form
+      const uint32_t e16 = (uint32_t)((st.end_rel & ~1) + 3) & ~3u;
+      const bool short_frame = live && e16 <= stream_start((uint64_t)win) + 1024;
+      constexpr int kFull = ABL & ~(kSkipEmptyLoads | kSkipWaveGate);
+      if (__ballot(short_frame) == 0)
+        stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
+                                       st.pad, probe_hook);
+      else
+        stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
+                                     st.pad, probe_hook);
+    } else {
+      stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
+                                   st.pad, probe_hook);
+    }
   }
   if constexpr (ABL & kLateProbe) probe_finish<ABL>(st.probe, live && !bad_off, a, st.conn_id, st.flags);
+  if constexpr (ABL & kPipeProbe) // the 2-ahead step is done: only the walk of longer runs and the verdict remain
+    probe_finish<ABL | kProbeAhead4>(st.probe, live && !bad_off, a, st.conn_id, st.flags);
   if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
 }
 
