@@ -284,6 +284,7 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_4096", runOne<4096, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_16384", runOne<16384, GpuBackend>(n_flows, polls / 4));
     leg("gpu_rxbatch_512_chunk_128", runOne<512, GpuBackend, 128>(n_flows, polls));
+    leg("gpu_rxbatch_512_chunk_256", runOne<512, GpuBackend, 256>(n_flows, polls));
     leg("gpu_rxbatch_4096_chunk_512", runOne<4096, GpuBackend, 512>(n_flows, polls));
     leg("gpu_rxbatch_4096_chunk_1024", runOne<4096, GpuBackend, 1024>(n_flows, polls));
     leg("gpu_rxbatch_16384_chunk_2048", runOne<16384, GpuBackend, 2048>(n_flows, polls / 4));
