@@ -19,22 +19,68 @@ def split_range(rank: int, world: int, n_total: int):
     return n_total * rank // world, n_total * (rank + 1) // world
 
 
-def common_window(body, dist=None):
+class ShmBarrier:
+    """A barrier for the ranks of one node in a few microseconds (gloo's over TCP takes ~0.1-1 ms, which a
+    20-step window of 0.5-ms steps would count): each rank publishes an epoch counter in its own 64-B cell
+    of a shared-memory page and spins until every cell has reached the epoch.  No atomics: one writer per
+    cell.  Set up collectively over `dist` (rank 0 creates the page, the name goes out by broadcast); a rank
+    that never arrives makes the others fail after `timeout_s` instead of hanging."""
+
+    def __init__(self, dist, rank: int, world: int, timeout_s: float = 120.0):
+        import secrets
+        from multiprocessing import shared_memory
+
+        import numpy as np
+
+        self.rank, self.world, self.timeout_s, self.epoch = rank, world, timeout_s, 0
+        name = [f"pn_barrier_{secrets.token_hex(6)}" if rank == 0 else None]
+        if rank == 0:
+            self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=64 * world)
+        dist.broadcast_object_list(name, src=0)
+        if rank != 0:
+            self.shm = shared_memory.SharedMemory(name=name[0])
+        self.cells = np.ndarray((world, 8), dtype=np.int64, buffer=self.shm.buf)
+        if rank == 0:
+            self.cells[:] = 0
+        dist.barrier()
+
+    def __call__(self):
+        self.epoch += 1
+        self.cells[self.rank, 0] = self.epoch
+        col = self.cells[:, 0]
+        deadline = None
+        while col.min() < self.epoch:
+            if deadline is None:
+                deadline = time.monotonic() + self.timeout_s
+            elif time.monotonic() > deadline:
+                raise TimeoutError(f"rank {self.rank}: shared-memory barrier {self.epoch} timed out")
+
+    def close(self, dist):
+        dist.barrier()  # nobody reads the page any more
+        del self.cells
+        self.shm.close()
+        if self.rank == 0:
+            self.shm.unlink()
+
+
+def common_window(body, dist=None, barrier=None):
     """Run body() inside one window shared by all ranks: the window opens when the start barrier
     releases this rank and closes after the end barrier, so every rank's window covers the slowest
     rank's finish.  Returns (max over ranks of the window, max over ranks of each rank's own
     body() time), both in seconds; dist = torch.distributed with an initialised group, or None for
-    one process.  Ranks that ran one after another therefore cannot look parallel."""
+    one process; barrier = the barrier to use (a ShmBarrier when the ranks share a node), default
+    dist.barrier.  Ranks that ran one after another therefore cannot look parallel."""
     import torch
 
     multi = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
+    sync = barrier if barrier is not None else (dist.barrier if multi else None)
     if multi:
-        dist.barrier()
+        sync()
     t0 = time.perf_counter()
     body()
     t_own = time.perf_counter()
     if multi:
-        dist.barrier()
+        sync()
     t1 = time.perf_counter()
     t = torch.tensor([t1 - t0, t_own - t0], dtype=torch.float64)
     if multi:

@@ -77,7 +77,7 @@ def test_two_rank_shards_match_single_process(tmp_path, cfg):
     assert wire == float(pa.wire_bytes(full, 2048, 2, world * n))
 
 
-def _window_worker(rank, world, port, flag, out_dir):
+def _window_worker(rank, world, port, flag, out_dir, shm=False):
     """Rank 1's work cannot start until rank 0's is done (a file flag): the two ran one after the
     other, so the common window must cover both (>= 0.4 s), while each rank's own body is ~0.2 s
     of work plus, on rank 1, the wait."""
@@ -99,22 +99,40 @@ def _window_worker(rank, world, port, flag, out_dir):
         if rank == 0:
             open(flag, "w").close()
 
-    wall, own = common_window(body, dist)
+    barrier = None
+    if shm:
+        from pollnet_amd.shard import ShmBarrier
+
+        barrier = ShmBarrier(dist, rank, world)
+    wall, own = common_window(body, dist, barrier)
+    if barrier is not None:
+        t0 = time.perf_counter()
+        for _ in range(200):
+            barrier()
+        per = (time.perf_counter() - t0) / 200
+        barrier.close(dist)
+    else:
+        per = 0.0
     with open(os.path.join(out_dir, f"win{rank}.txt"), "w") as f:
-        f.write(f"{wall} {own}")
+        f.write(f"{wall} {own} {per}")
     dist.destroy_process_group()
 
 
-def test_common_window_covers_serialised_ranks(tmp_path):
+@pytest.mark.parametrize("shm", [False, True])
+def test_common_window_covers_serialised_ranks(tmp_path, shm):
     """bench.py's aggregate timing (shard.common_window): ranks that ran one after another cannot
-    look parallel — every rank reports the same max window, and it spans both ranks' work."""
+    look parallel — every rank reports the same max window, and it spans both ranks' work; with gloo's
+    barrier and with the shared-memory barrier the bench uses on one node (which must also be fast)."""
     world = 2
-    mp.spawn(_window_worker, args=(world, _free_port(), str(tmp_path / "flag"), str(tmp_path)), nprocs=world,
+    mp.spawn(_window_worker, args=(world, _free_port(), str(tmp_path / "flag"), str(tmp_path), shm), nprocs=world,
              join=True)
     res = [tuple(map(float, open(tmp_path / f"win{r}.txt").read().split())) for r in range(world)]
-    assert res[0] == res[1]  # max over ranks, identical everywhere
-    wall, own = res[0]
+    assert res[0][:2] == res[1][:2]  # max over ranks, identical everywhere
+    wall, own, per = res[0]
     assert wall >= 0.4 and own >= 0.4 and wall >= own
+    if shm:
+        assert per < 2e-3, per  # a spin on shared memory, not a socket round trip
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("pn_barrier_")]
 
 
 def test_common_window_single_process():
