@@ -39,6 +39,7 @@ GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
 SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
 CLISRVTEST = tests/cpp/test_tcp_client_server
+TXHOSTTEST = tests/cpp/test_tx_host
 
 # Host programs that include HIP headers: compiled by hipcc with the device pass pinned to gfx950
 # (without --offload-arch hipcc would add a default-arch device pass for nothing)
@@ -51,7 +52,7 @@ REF_INCS = oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
 HAVE_REF_TEXT = $(or $(wildcard $(REFDIR)/example/tcpserver.cc),$(and $(wildcard oracle/_ref/tcpserver_handler.inc),$(wildcard oracle/_ref/tcpclient_handler.inc)))
 REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST))
 
-all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST)
+all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST) $(TXHOSTTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
@@ -129,6 +130,11 @@ $(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/poll
 	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
+# the engine's host-side TX checksums vs the oracle's fill (host only)
+$(TXHOSTTEST): tests/cpp/test_tx_host.cpp include/pollnet_amd/tcp_engine.hpp $(HDRS) $(ORACLE)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
 # receive-side state machine (host only): scenarios + differential vs the reference TcpStream
 $(RXCONNTEST): tests/cpp/test_rx_conn.cpp tests/cpp/segframes.hpp include/pollnet_amd/rx_conn.hpp $(HDRS) $(ORACLE)
 	g++ -O2 -std=c++17 -Wall -o $@ $< -Loracle -loracle -ldl -Wl,-rpath,'$$ORIGIN/../../oracle'
@@ -158,6 +164,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST)
+	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST)
 
 .PHONY: all ref clean

@@ -97,3 +97,17 @@ def test_gpu_client_server_match_twin():
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("gpu: handler logs identical, wire frames identical") == 4, p.stdout
     assert p.stdout.count("gpu (pipelined): handler logs identical, wire frames identical") == 4, p.stdout
+
+
+TXHOST = os.path.join(ROOT, "tests", "cpp", "test_tx_host")
+
+
+def test_engine_host_tx_checksums_equal_oracle_fill():
+    """The engine's host-side checksums for header-only TX batches (srv_detail::fill_tcp_checksums)
+    equal the oracle's PN_TX_TCP fill — itself pinned to the reference's copyAndSum / setOptDataLen
+    (tests/test_tx.py) — on 20,000 random frames, every tot_len 40..1500, frames below the headers
+    untouched."""
+    if not os.path.exists(TXHOST):
+        subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tx_host"], check=True, capture_output=True)
+    p = subprocess.run([TXHOST, "20000"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "PASS" in p.stdout, p.stdout + p.stderr
