@@ -70,6 +70,13 @@ enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
 // longer than that walk after phase 2.  Each round trip overlaps a stream batch instead of sitting
 // between phase 1 and phase 2.
 enum : int { kPipeProbe = 65536 };
+// Timing only (with kAblNoWalk): every lane of a wave loads the same home entry (the first lane's), so the
+// probe instruction touches one line instead of up to 64 — isolates the cost of the scattered probe loads.
+enum : int { kAblUniformProbe = 131072 };
+// kScalarProbe: the home-slot entries come through the scalar cache — one uniform 16-B load per lane,
+// issued 64 per wave through the constant address space — instead of one vector load that touches up to
+// 64 distinct lines in the texture path (what the probe costs, kAblUniformProbe shows).
+enum : int { kScalarProbe = 262144 };
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 

@@ -125,8 +125,31 @@ __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port,
       p.e += j;
       if (p.e >= a.n_entries) p.e = a.n_entries;
     }
+  } else if constexpr (ABL & kScalarProbe) {
+    // every lane's home entry through the scalar path: lane L's index is made uniform (readlane) and
+    // loaded from the constant address space; the loads are independent, so they overlap
+    using ctbl_t = __attribute__((address_space(4))) const u32x4*;
+    const ctbl_t tc = (ctbl_t)(const void*)a.tbl;
+    const bool want = live && p.e < a.n_entries;
+    const uint32_t e_safe = want ? p.e : 0u; // every lane's load is issued (a spare one for idle lanes)
+    u32x4 mine = u32x4{0u, 0x80000000u, 0u, 0u};
+#pragma unroll
+    for (int g = 0; g < 8; ++g) { // 8 independent loads in flight, then their 8 lanes take them
+      u32x4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = tc[__builtin_amdgcn_readlane(e_safe, 8 * g + j)];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (threadIdx.x == (uint32_t)(8 * g + j)) mine = v[j];
+    }
+    if (want) {
+      p.k = ((uint64_t)mine.y << 32) | mine.x;
+      p.cid = mine.z;
+    }
   } else if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
-    const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + p.e);
+    uint32_t eh = p.e;
+    if constexpr (ABL & kAblUniformProbe) eh = __builtin_amdgcn_readfirstlane(eh); // timing only
+    const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + eh);
     p.k = ((uint64_t)ent.y << 32) | ent.x;
     p.cid = ent.z;
   }
