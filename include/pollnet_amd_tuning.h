@@ -41,8 +41,9 @@ int pn_calib_classify_ablated(pn_ctx* ctx, const void* frames_dev, uint32_t slot
 int pn_calib_tx_ablated(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n, void* stream);
 
 /* pn_match_streams in either kernel form: variant 1 = 4 lanes per frame load its header chunks
- * through LDS (production), 0 = one lane per frame loads its own, 2-4 = variant 1 with nt / sc0 / sc1
- * loads, 5 = variant 1's loads alone (timing-only same-pattern ceiling; ids not written). */
+ * through LDS with nt loads (production), 0 = one lane per frame loads its own, 9 = variant 1 with
+ * default-policy loads, 2-4 = nt / sc0 / sc1 loads, 5 = the production loads alone (timing-only
+ * same-pattern ceiling; ids not written), 6 / 7 / 8 = sc1 id stores / nt loads + sc1 stores / nt stores. */
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant);

@@ -372,21 +372,26 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
 
 
 // pn_match_streams in either form (stream_match.hpp): 1 cooperative chunks through LDS, 0 one lane
-// per frame; 2-4 the cooperative form with nt / sc0 / sc1 loads; 5 its loads alone (a ceiling).  A/B by scripts/bench_streams.py.
+// per frame; 2-4 the cooperative form with nt / sc0 / sc1 loads; 5 its loads alone (a ceiling); 6-8 the id
+// stores write-through / nt (7: with nt loads).  A/B by scripts/bench_streams.py.
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant) {
-  if (n == 0 || variant < 0 || variant > 5) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  if (n == 0 || variant < 0 || variant > 9) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
   MatchArgs a;
   int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
-    case 1: launch_match<1>(a, frame_off, s); break;
+    case 1: launch_match<kMatchProd, kMatchLoadAux>(a, frame_off, s); break; // production
+    case 9: launch_match<1>(a, frame_off, s); break;     // cooperative, default-policy loads
     case 2: launch_match<1, 2>(a, frame_off, s); break;  // cooperative, nt loads
     case 3: launch_match<1, 1>(a, frame_off, s); break;  // cooperative, sc0 loads
     case 4: launch_match<1, 16>(a, frame_off, s); break; // cooperative, sc1 loads
-    case 5: launch_match<2>(a, frame_off, s); break;     // timing-only ceiling: the same loads, no compare or store
+    case 5: launch_match<2, kMatchLoadAux>(a, frame_off, s); break;     // timing-only ceiling: the same loads, no compare or store
+    case 6: launch_match<1, 0, 16>(a, frame_off, s); break; // ids stored write-through (sc1)
+    case 7: launch_match<1, 2, 16>(a, frame_off, s); break; // nt loads + sc1 id stores
+    case 8: launch_match<1, 0, 2>(a, frame_off, s); break;  // ids stored nt
     default: launch_match<0>(a, frame_off, s);
   }
   hipError_t e = hipGetLastError();

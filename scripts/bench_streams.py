@@ -19,7 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,3")
     ap.add_argument("--rounds", type=int, default=10)
-    ap.add_argument("--policies", action="store_true", help="also time the cooperative form's nt / sc0 / sc1 loads")
+    ap.add_argument("--policies", action="store_true", help="also time the cooperative form with other load / store cache policies")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -67,8 +67,9 @@ def main():
             tg.append(timed(lambda d: tn.match_streams_variant(ctx, d, 2048, off, n, flt, ids0, 5, st)))
         ms, ms0, mg = statistics.median(ts), statistics.median(ts0), statistics.median(tg)
         pol = {}
+        ctx.match_streams(dev[0], 2048, off, n, flt, ids, st)  # the timed loops left another batch's ids
         if args.policies:
-            for v, name in ((2, "nt"), (3, "sc0"), (4, "sc1")):
+            for v, name in ((9, "default"), (2, "nt"), (3, "sc0"), (4, "sc1"), (6, "store_sc1"), (7, "nt_load_store_sc1"), (8, "store_nt")):
                 ids_v = torch.empty_like(ids)
                 tn.match_streams_variant(ctx, dev[0], 2048, off, n, flt, ids_v, v, st)
                 torch.cuda.synchronize()
