@@ -57,26 +57,14 @@ enum : int { kSkipWaveGate = 16384 };
 // C5 -3.9 % (0.1660 -> 0.1596 ms; the probe's share over the no-probe ablation 13.6 -> 7.2 us),
 // C3 equal (profiles/r03/probe_group_c{3,5}.json).
 enum : int { kGroupProbe = 32768 };
-// With kCoopProbe: the home slot and the 3 entries after it are loaded together (one L2 round
-// trip) and resolved in registers; only runs longer than that go to the cooperative walk.  Without
-// it the home slot comes first and a lane whose run goes on fetches 2 more (two round trips).
-enum : int { kProbeAhead4 = 2048 };
 // Tuning: kLateProbe issues the home-slot load in phase 1 and finishes the walk after phase 2 (the
 // round trip under the stream loads); kAblNoWalk (timing only) stops every probe at its home slot.
 enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
-// kPipeProbe: the probe's dependent round trips are software-pipelined into phase 2 — the home-slot
-// load is issued in phase 1 and resolved after the first stream batch's loads are issued, the next-2
-// fetch of colliding lanes is issued there and resolved after the second batch's loads; only runs
-// longer than that walk after phase 2.  Each round trip overlaps a stream batch instead of sitting
-// between phase 1 and phase 2.
-enum : int { kPipeProbe = 65536 };
 // Timing only (with kAblNoWalk): every lane of a wave loads the same home entry (the first lane's), so the
 // probe instruction touches one line instead of up to 64 — isolates the cost of the scattered probe loads.
 enum : int { kAblUniformProbe = 131072 };
-// kScalarProbe: the home-slot entries come through the scalar cache — one uniform 16-B load per lane,
-// issued 64 per wave through the constant address space — instead of one vector load that touches up to
-// 64 distinct lines in the texture path (what the probe costs, kAblUniformProbe shows).
-enum : int { kScalarProbe = 262144 };
+// Retired probe forms (measured, not adopted; DESIGN §4, profiles/r03/probe_ablation/): 2048 home slot + 3
+// ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94).
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 
@@ -222,15 +210,9 @@ __device__ __forceinline__ uint32_t stream_start(uint64_t w) { return 112u - (((
 // group_ipa + fi*stride.  end_rel is this lane's frame extent (read back per
 // frame with readlane); the total of frame fi lands on lane fi.  The header lane
 // has summed the window below stream_start (window_part).
-struct NoHook {
-  __device__ __forceinline__ void operator()(int) const {}
-};
-
-// hook(b) runs right after batch b's loads are issued (b = 0, 1, ... while batches remain; hooks 0 and 1
-// always run, after the loop if the wave has fewer batches): kPipeProbe's probe steps.
-template <int ABL, int LAUX, int IDX, class Hook = NoHook>
+template <int ABL, int LAUX, int IDX>
 __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win, uint32_t n_here,
-                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad, Hook hook = Hook()) {
+                                             int lane, int end_rel, uint32_t& t_all, uint32_t& pad) {
   // window start of frame fi: strided from the group's first slot, or (indexed) the
   // address its own lane computed, broadcast with two readlanes
   auto frame_win = [&](uint32_t fi) -> const uint8_t* {
@@ -269,7 +251,6 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       }
     }
     __builtin_amdgcn_sched_barrier(0); // keep the whole batch in flight before the first wait
-    if (b0 < 2 * kBatch) hook((int)(b0 / kBatch));
     auto sel = [](int e, int o) -> uint32_t {
       if constexpr (ABL & (kAblNoMask | kExactRange)) return 0x10001u;
       else return tail_sel(e, o);
@@ -357,7 +338,6 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
     }
   }
-  if (n_here <= kBatch) hook(1); // one batch only (n_here >= 1): the second probe step still runs
 }
 
 } // namespace pn_dev

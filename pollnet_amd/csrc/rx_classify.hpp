@@ -89,9 +89,6 @@ struct FrameState {
 };
 
 // connHashKey (Core.h:167-172) and the load of the home slot `key & tbl_mask` (Core.h:558-559).
-// kProbeAhead4: the home slot and the next 3 entries in one round trip, walked in registers as
-// findConnEntry walks them (Core.h:560-561): the probe stops at the first entry with key >= the
-// lane's key or at the array end; a run going on past them leaves e at the last one loaded.
 template <int ABL>
 __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port, bool live, const KArgs& a) {
   Probe p;
@@ -101,52 +98,7 @@ __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port,
   p.e = (uint32_t)(p.key & a.mask);
   p.k = PN_EMPTY_KEY;
   p.cid = 0;
-  if constexpr ((ABL & kProbeAhead4) && (ABL & kCoopProbe)) {
-    if (live && p.e < a.n_entries) {
-      u32x4 ent[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        ent[j] = u32x4{0u, 0x80000000u, 0u, 0u}; // PN_EMPTY_KEY past the array end: stops the walk
-        if (p.e + j < a.n_entries) ent[j] = *reinterpret_cast<const u32x4*>(a.tbl + p.e + j);
-      }
-      // the first of the 4 whose key is >= the lane's key (walking backwards keeps the first)
-      uint32_t stop = 4;
-#pragma unroll
-      for (int j = 3; j >= 0; --j)
-        if (p.e + j >= a.n_entries || (((uint64_t)ent[j].y << 32) | ent[j].x) >= p.key) stop = j;
-      const uint32_t j = stop < 4 ? stop : 3;
-      const u32x4 pick = j == 0 ? ent[0] : j == 1 ? ent[1] : j == 2 ? ent[2] : ent[3];
-      if (p.e + j < a.n_entries) {
-        p.k = ((uint64_t)pick.y << 32) | pick.x;
-        p.cid = pick.z;
-      } else {
-        p.k = PN_EMPTY_KEY; // the walk ran off the array: e == n_entries below ends it as a miss
-      }
-      p.e += j;
-      if (p.e >= a.n_entries) p.e = a.n_entries;
-    }
-  } else if constexpr (ABL & kScalarProbe) {
-    // every lane's home entry through the scalar path: lane L's index is made uniform (readlane) and
-    // loaded from the constant address space; the loads are independent, so they overlap
-    using ctbl_t = __attribute__((address_space(4))) const u32x4*;
-    const ctbl_t tc = (ctbl_t)(const void*)a.tbl;
-    const bool want = live && p.e < a.n_entries;
-    const uint32_t e_safe = want ? p.e : 0u; // every lane's load is issued (a spare one for idle lanes)
-    u32x4 mine = u32x4{0u, 0x80000000u, 0u, 0u};
-#pragma unroll
-    for (int g = 0; g < 8; ++g) { // 8 independent loads in flight, then their 8 lanes take them
-      u32x4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = tc[__builtin_amdgcn_readlane(e_safe, 8 * g + j)];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (threadIdx.x == (uint32_t)(8 * g + j)) mine = v[j];
-    }
-    if (want) {
-      p.k = ((uint64_t)mine.y << 32) | mine.x;
-      p.cid = mine.z;
-    }
-  } else if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
+  if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
     uint32_t eh = p.e;
     if constexpr (ABL & kAblUniformProbe) eh = __builtin_amdgcn_readfirstlane(eh); // timing only
     const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + eh);
@@ -154,48 +106,6 @@ __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port,
     p.cid = ent.z;
   }
   return p;
-}
-
-// kPipeProbe: the next-2 fetch of the lanes whose run goes on past the home slot, split into its issue
-// (after the first stream batch's loads) and its resolution (after the second's); the same entries and
-// the same stopping rule as probe_finish's kAhead step.
-struct ProbeAhead {
-  u32x4 nx[2];
-  bool srch, any;
-};
-__device__ __forceinline__ void pp_issue_ahead(const Probe& p, bool live, const KArgs& a, ProbeAhead& q) {
-  q.srch = live && p.e < a.n_entries && p.k < p.key; // waits for the home-slot load here
-  q.any = __ballot(q.srch) != 0;
-  if (q.any) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      q.nx[j] = u32x4{0u, 0u, 0u, 0u};
-      if (q.srch && p.e + 1 + j < a.n_entries) q.nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + p.e + 1 + j);
-    }
-  }
-}
-__device__ __forceinline__ void pp_resolve_ahead(Probe& p, const KArgs& a, const ProbeAhead& q) {
-  if (!q.any) return;
-  uint32_t step = 0, cid2 = 0;
-  uint64_t k2 = 0;
-#pragma unroll
-  for (int j = 1; j >= 0; --j) { // the first entry (in order) that stops the walk
-    const uint64_t kk = ((uint64_t)q.nx[j].y << 32) | q.nx[j].x;
-    if (p.e + 1 + j >= a.n_entries || kk >= p.key) {
-      step = j + 1;
-      k2 = kk;
-      cid2 = q.nx[j].z;
-    }
-  }
-  if (q.srch) {
-    if (step != 0) {
-      p.e += step;
-      p.k = k2;
-      p.cid = cid2;
-    } else {
-      p.e += 2; // every fetched key < key: the run goes on (p.k stays below the key)
-    }
-  }
 }
 
 // The rest of findConnEntry's ordered walk (Core.h:560-561) and the conn / TIME_WAIT / miss
@@ -215,7 +125,7 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
     // walk stops at.
     const uint32_t lane = threadIdx.x;
     bool srch = live && e < a.n_entries && k < key;
-    if (!(ABL & kProbeAhead4) && __ballot(srch) != 0) {
+    if (__ballot(srch) != 0) {
       // short runs (the common case past the home slot): every searching lane fetches its
       // next kAhead entries at once -- one round trip for all of them, in parallel
       constexpr int kAhead = 2;
@@ -367,7 +277,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
   // (Resolving the probe after phase 2 instead, so the home-slot load overlaps the stream loads,
   // measured no faster: profiles/r02/s3/late_probe_ab.json.)
   st.conn_id = PN_MISS;
-  if constexpr (ABL & (kLateProbe | kPipeProbe)) st.probe = probe_issue<ABL>(st.src_ip, src_port, live, a);
+  if constexpr (ABL & kLateProbe) st.probe = probe_issue<ABL>(st.src_ip, src_port, live, a);
   else if constexpr (!(ABL & kAblNoProbe)) probe_finish<ABL>(probe_issue<ABL>(st.src_ip, src_port, live, a), live, a, st.conn_id, flags);
   st.flags = flags;
   return st;
@@ -431,8 +341,8 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // class); per-frame stream descriptors; with COOP, waves whose frames all have their
 // block 16-B aligned inside the ring load blocks cooperatively, other waves per-lane
 // bounds-checked windows.
-// 5 waves/SIMD (<= 96 VGPRs) where that compiles without spills (MIS % 4 == 0, incl. the
-// default and ef_vi layouts); the 2-mod-4 alignments and the indexed path need a few more VGPRs and keep 4.
+// Register target: 4 waves/SIMD.  Until round 3 the MIS % 4 == 0 kernels fit 5 (<= 96 VGPRs) and the
+// LDS pad below held them at 4; the grouped probe takes them to 102 VGPRs, so registers and pad now agree.
 template <int MIS, int COOP, int ABL, int LAUX, int SAUX, int IDX, int LWIN>
 __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wave_base, const int lane, u32x4* lds_recs) {
   if (wave_base >= a.n) return;
@@ -543,15 +453,6 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
     }
     st.t_all += sum;
   } else {
-    // kPipeProbe: the probe's steps ride on the first two stream batches (hook); otherwise no hook
-    ProbeAhead q{};
-    const bool plive = live && !bad_off;
-    auto probe_hook = [&](int b) {
-      if constexpr (ABL & kPipeProbe) {
-        if (b == 0) pp_issue_ahead(st.probe, plive, a, q);
-        else pp_resolve_ahead(st.probe, a, q);
-      }
-    };
     if constexpr ((ABL & kSkipWaveGate) && (ABL & kSkipEmptyLoads)) {
       // a frame whose extent ends before its second stream KiB: take the skipping form
       const uint32_t e16 = (uint32_t)((st.end_rel & ~1) + 3) & ~3u;
@@ -559,18 +460,16 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
       constexpr int kFull = ABL & ~(kSkipEmptyLoads | kSkipWaveGate);
       if (__ballot(short_frame) == 0)
         stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
-                                       st.pad, probe_hook);
+                                       st.pad);
       else
         stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
-                                     st.pad, probe_hook);
+                                     st.pad);
     } else {
       stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
-                                   st.pad, probe_hook);
+                                   st.pad);
     }
   }
   if constexpr (ABL & kLateProbe) probe_finish<ABL>(st.probe, live && !bad_off, a, st.conn_id, st.flags);
-  if constexpr (ABL & kPipeProbe) // the 2-ahead step is done: only the walk of longer runs and the verdict remain
-    probe_finish<ABL | kProbeAhead4>(st.probe, live && !bad_off, a, st.conn_id, st.flags);
   if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
 }
 
@@ -578,10 +477,10 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
 // GRP > 1 (tuning variants): GRP consecutive groups per workgroup, their records kept in
 // LDS and written in one GRP-KiB burst at the end (scripts/write_grouping.py probe).
 // GOPT (tuning): bit 0 = GRP groups per workgroup but records stored per group (no LDS);
-// bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 5;
+// bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 4;
 // GOPT >> 4 = KiB of LDS padding, which caps workgroups per CU.  Production pads 2 KiB:
 // with the 8-KiB window tile that is 10 KiB per workgroup, 16 per CU = 4 waves/SIMD where
-// registers would allow 5 -- C2 -1.2 %, C3 -2.5 %, C5 -0.3 % (3 waves: C3 +9 %, C5 +13 %;
+// registers allowed 5 before the grouped probe -- C2 -1.2 %, C3 -2.5 %, C5 -0.3 % (3 waves: C3 +9 %, C5 +13 %;
 // profiles/r01_experiments/occupancy_c{2,3,5}.json).
 // Bit 3: XCD-aware order.  Workgroup b is dispatched to XCD b % 8; mapping it to group
 // (b % 8) * ceil(G / 8) + b / 8 gives every XCD one contiguous eighth of the batch (its own
@@ -594,7 +493,7 @@ constexpr int kProdGopt = (2 << 4) | kXcdOrder;
 constexpr int kSignalDone = 1 << 12;
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
           int GRP = 1, int GOPT = kProdGopt>
-__global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : (MIS % 4 == 0 && !IDX) ? 5 : 4) void rx_classify_kernel(KArgs a) {
+__global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : 4) void rx_classify_kernel(KArgs a) {
   const int lane = threadIdx.x;
   static_assert(!(GOPT & kSignalDone) || ((GOPT & 8) && GRP == 1), "the completion word is set on the XCD-ordered one-group path");
   if constexpr (((GOPT >> 4) & 0xff) > 0) {

@@ -281,13 +281,9 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     // in the history)
     case 38: launch_one<0, 1, kProdAbl | kGroupProbe>(a, s); break;  // cluster lanes resolved per run position
     case 39: launch_one<0, 1, kProdAbl & ~kGroupProbe>(a, s); break; // one lane per round trip past kAhead
-    case 40: launch_one<0, 1, kProdAbl | kProbeAhead4>(a, s); break;  // home slot + 3 in one round trip
-    case 41: launch_one<0, 1, (kProdAbl | kProbeAhead4) & ~kGroupProbe>(a, s); break;
     case 42: launch_one<0, 1, kProdAbl | kLateProbe>(a, s); break;   // walk finished after phase 2
     case 43: launch_one<0, 1, kProdAbl | kAblNoWalk>(a, s); break;   // timing only: home slot decides
-    case 44: launch_one<0, 1, kProdAbl | kPipeProbe>(a, s); break;   // probe steps pipelined into phase 2
     case 45: launch_one<0, 1, kProdAbl | kAblNoWalk | kAblUniformProbe>(a, s); break; // timing only: one line per probe
-    case 46: launch_one<0, 1, kProdAbl | kScalarProbe>(a, s); break;  // home entries through the scalar path
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
