@@ -131,7 +131,7 @@ $(TCPRXTEST): tests/cpp/test_gpu_tcp_rx.cpp tests/cpp/segframes.hpp include/poll
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # the engine's host-side TX checksums vs the oracle's fill (host only)
-$(TXHOSTTEST): tests/cpp/test_tx_host.cpp include/pollnet_amd/tcp_engine.hpp $(HDRS) $(ORACLE)
+$(TXHOSTTEST): tests/cpp/test_tx_host.cpp include/pollnet_amd/tcp_engine.hpp $(HDRS) $(LIB) $(ORACLE)
 	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
