@@ -104,6 +104,29 @@ def test_full_size_digest(torch_cuda, ctx, golden_dir, cfg):
         assert counts[1] == n - n // 1024
 
 
+def test_every_c4_shard_digest(torch_cuda, ctx, golden_dir):
+    """All 8 index shards of BASELINE configs[3] (C4: 16 Mi frames, 2 Mi per GPU), one after another on
+    this GPU: each shard's records hash to the digest the N=8 bench line gates that rank on."""
+    with open(os.path.join(golden_dir, "full_digests.json")) as f:
+        shards = json.load(f)["c4_shards"]
+    assert len(shards) == 8
+    p = pa.rx.GenParams.for_config(4)
+    t = pa.gen_conn_table(p)
+    ctx.set_conn_table(t)
+    n = shards[0]["n"]
+    host = np.empty((n, STRIDE), dtype=np.uint8)
+    frames = torch_cuda.empty(n * STRIDE, dtype=torch_cuda.uint8, device="cuda")
+    res = torch_cuda.empty(n * 16, dtype=torch_cuda.uint8, device="cuda")
+    for r, ref in enumerate(shards):
+        assert ref["first_index"] == r * n and ref["n"] == n
+        pa.gen_frames(p, n, STRIDE, FRAME_OFF, first_index=ref["first_index"], out=host)
+        assert pa.wire_bytes(host, STRIDE, FRAME_OFF, n) == ref["wire_bytes"]
+        frames.copy_(torch_cuda.from_numpy(host.reshape(-1)))
+        ctx.classify(frames, STRIDE, FRAME_OFF, n, res, torch_cuda.cuda.current_stream())
+        torch_cuda.cuda.synchronize()
+        assert hashlib.sha256(res.cpu().numpy().tobytes()).hexdigest() == ref["records_sha256"], f"shard {r}"
+
+
 @pytest.mark.parametrize("frame_off", [0, 2, 4, 6, 8, 10, 12, 14, 16, 24, 34, 38, 18, 50, 66, 82, 98, 114, 120, 126])
 def test_every_alignment_specialisation(torch_cuda, ctx, frame_off):
     """(frame_off + 14) % 16 selects one of 8 kernel specialisations; ef_vi's layout is
