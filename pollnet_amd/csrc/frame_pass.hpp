@@ -63,13 +63,9 @@ enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
 // Timing only (with kAblNoWalk): every lane of a wave loads the same home entry (the first lane's), so the
 // probe instruction touches one line instead of up to 64 — isolates the cost of the scattered probe loads.
 enum : int { kAblUniformProbe = 131072 };
-// With kCoopProbe | kGroupProbe: the device table's pad word holds the run length from each entry (written by
-// pn_set_conn_table); a lane whose home run is longer than kLongRun skips the next-kAhead step and joins the
-// group walk, whose first 64-entry fetch goes out in the same round trip as the short lanes' next entries.
-enum : int { kRunHint = 524288 };
-constexpr uint32_t kLongRun = 8;
 // Retired probe forms (measured, not adopted; DESIGN §4, profiles/r03/probe_ablation/): 2048 home slot + 3
-// ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94).
+// ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94);
+// 524288 a run-length hint in the device table's pad word sending long runs straight to the group walk (c3575ae).
 // The production RX configuration.
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
 

@@ -35,7 +35,6 @@ struct pn_ctx {
   std::vector<hipEvent_t> retired;  // recorded on those streams at the last set (pooled)
   size_t n_retired = 0;
   hipStream_t copy_stream = nullptr; // internal, non-blocking: table uploads
-  std::vector<pn_conn_entry> staging; // the snapshot with each entry's run length in its pad word
   void* tx_patch = nullptr;          // pn_tx_fill's per-frame patch records (8 B each)
   uint32_t tx_patch_n = 0;
   pn_fence tx;                       // the last launch that used tx_patch

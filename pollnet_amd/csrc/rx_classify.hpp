@@ -76,7 +76,6 @@ struct Probe {
   uint32_t e;
   uint64_t k;   // key of entry e (PN_EMPTY_KEY when not loaded)
   uint32_t cid; // conn_id of entry e
-  uint32_t run; // kRunHint: entries from e to the end of its run (the device table's pad word)
 };
 
 // Per-frame state the header lane keeps from phase 1 to phase 3.
@@ -99,49 +98,14 @@ __device__ __forceinline__ Probe probe_issue(uint32_t src_ip, uint32_t src_port,
   p.e = (uint32_t)(p.key & a.mask);
   p.k = PN_EMPTY_KEY;
   p.cid = 0;
-  p.run = 0;
   if (live && p.e < a.n_entries) { // the home slot: almost every lookup ends here
     uint32_t eh = p.e;
     if constexpr (ABL & kAblUniformProbe) eh = __builtin_amdgcn_readfirstlane(eh); // timing only
     const u32x4 ent = *reinterpret_cast<const u32x4*>(a.tbl + eh);
     p.k = ((uint64_t)ent.y << 32) | ent.x;
     p.cid = ent.z;
-    p.run = ent.w;
   }
   return p;
-}
-
-// Resolve every lane of `group` (lanes standing at one run position, base - 1) against the entries
-// base .. base + 63, lane j holding entry base + j: each stops at the first entry with key >= its own
-// (or the array end) -- the entry its scalar walk stops at.  Returns the lanes not resolved (every
-// fetched key below theirs).  Wave-uniform; kRunHint's first group fetch.
-__device__ __forceinline__ uint64_t resolve_fetched(uint64_t group, uint32_t base, const u32x4& ent, uint64_t key,
-                                                    uint32_t n_entries, uint32_t& e, uint64_t& k, uint32_t& cid,
-                                                    bool& srch) {
-  const uint32_t lane = threadIdx.x;
-  const uint32_t idx = base + lane;
-  const uint64_t kk = ((uint64_t)ent.y << 32) | ent.x;
-  uint64_t left = 0;
-  for (uint64_t pend = group; pend != 0; pend &= pend - 1) {
-    const uint32_t L = (uint32_t)__builtin_ctzll(pend);
-    const uint64_t kl = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(key >> 32), L) << 32) |
-                        (uint32_t)__builtin_amdgcn_readlane((uint32_t)key, L);
-    const uint64_t stop = __ballot(idx >= n_entries || kk >= kl);
-    if (stop != 0) {
-      const uint32_t first = (uint32_t)__builtin_ctzll(stop);
-      const uint32_t klo = __builtin_amdgcn_readlane(ent.x, first), khi = __builtin_amdgcn_readlane(ent.y, first);
-      const uint32_t c = __builtin_amdgcn_readlane(ent.z, first);
-      if (lane == L) {
-        e = base + first;
-        k = ((uint64_t)khi << 32) | klo;
-        cid = c;
-        srch = false;
-      }
-    } else {
-      left |= 1ull << L;
-    }
-  }
-  return left;
 }
 
 // The rest of findConnEntry's ordered walk (Core.h:560-561) and the conn / TIME_WAIT / miss
@@ -162,24 +126,6 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
     const uint32_t lane = threadIdx.x;
     bool srch = live && e < a.n_entries && k < key;
     if (__ballot(srch) != 0) {
-      // kRunHint: lanes in a long run (the hint from the home load) go to the group walk at once;
-      // its first fetch (the first long lane's position + 1 .. + 64) is issued here, beside the
-      // short lanes' next entries, so both come back in one round trip
-      bool shrt = srch;
-      uint64_t group = 0;
-      uint32_t gbase = 0;
-      u32x4 gent = {0u, 0u, 0u, 0u};
-      if constexpr (ABL & kRunHint) {
-        const bool lng = srch && p.run > kLongRun;
-        shrt = srch && !lng;
-        const uint64_t nl = __ballot(lng);
-        if (nl != 0) { // wave-uniform
-          const uint32_t e0 = __builtin_amdgcn_readlane(e, (uint32_t)__builtin_ctzll(nl));
-          group = __ballot(lng && e == e0);
-          gbase = e0 + 1;
-          if (gbase + lane < a.n_entries) gent = *reinterpret_cast<const u32x4*>(a.tbl + gbase + lane);
-        }
-      }
       // short runs (the common case past the home slot): every searching lane fetches its
       // next kAhead entries at once -- one round trip for all of them, in parallel
       constexpr int kAhead = 2;
@@ -187,7 +133,7 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
 #pragma unroll
       for (int j = 0; j < kAhead; ++j) {
         nx[j] = u32x4{0u, 0u, 0u, 0u};
-        if (shrt && e + 1 + j < a.n_entries) nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + e + 1 + j);
+        if (srch && e + 1 + j < a.n_entries) nx[j] = *reinterpret_cast<const u32x4*>(a.tbl + e + 1 + j);
       }
       uint32_t step = 0, cid2 = 0;
       uint64_t k2 = 0;
@@ -200,7 +146,7 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
           cid2 = nx[j].z;
         }
       }
-      if (shrt) {
+      if (srch) {
         if (step != 0) {
           e += step;
           k = k2;
@@ -208,12 +154,6 @@ __device__ __forceinline__ void probe_finish(const Probe& p, bool live, const KA
           srch = false;
         } else {
           e += kAhead; // every fetched key < key: the run goes on
-        }
-      }
-      if constexpr (ABL & kRunHint) {
-        if (group != 0) { // wave-uniform
-          const uint64_t left = resolve_fetched(group, gbase, gent, key, a.n_entries, e, k, cid, srch);
-          if ((left >> lane) & 1) e = gbase + kWave - 1; // all 64 fetched keys below the lane's: go on from there
         }
       }
     }

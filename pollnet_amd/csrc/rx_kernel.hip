@@ -120,17 +120,8 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
     e = hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking);
     if (e != hipSuccess) return hip_err(ctx, e, "hipStreamCreate(table uploads)");
   }
-  // The device copy carries, in each entry's pad word (unused by the reference), the number of
-  // occupied entries from it to the end of its run: the probe's hint for long runs (kRunHint,
-  // rx_classify.hpp).  It only picks how the walk fetches; every walk stops where the scalar one does.
-  ctx->staging.assign(entries, entries + n_entries);
-  uint32_t run = 0;
-  for (uint32_t i = n_entries; i-- > 0;) {
-    run = ctx->staging[i].key == PN_EMPTY_KEY ? 0 : (run == UINT32_MAX ? run : run + 1);
-    ctx->staging[i]._pad = run;
-  }
-  e = hipMemcpyAsync(ctx->tbl_buf[nxt], ctx->staging.data(), (size_t)n_entries * sizeof(pn_conn_entry),
-                     hipMemcpyHostToDevice, ctx->copy_stream);
+  e = hipMemcpyAsync(ctx->tbl_buf[nxt], entries, (size_t)n_entries * sizeof(pn_conn_entry), hipMemcpyHostToDevice,
+                     ctx->copy_stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->copy_stream);
   if (e != hipSuccess) return hip_err(ctx, e, "hipMemcpyAsync(conn table)");
   // everything launched so far reads (at most) the buffer being retired: mark its end
