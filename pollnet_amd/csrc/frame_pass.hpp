@@ -26,6 +26,8 @@ constexpr int kWinBytes = 16 * kWinChunks;
 using Window = Win<4 * kWinChunks>;
 
 constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
+// A buffer-load offset past every descriptor's range (<= 4 MiB here): the load returns zeros and fetches nothing.
+constexpr uint32_t kNoFetch = 0x80000000u;
 
 // Timing-only ablations (scripts/variants.py; records are wrong when set):
 // bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail
@@ -63,6 +65,10 @@ enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
 // Timing only (with kAblNoWalk): every lane of a wave loads the same home entry (the first lane's), so the
 // probe instruction touches one line instead of up to 64 — isolates the cost of the scattered probe loads.
 enum : int { kAblUniformProbe = 131072 };
+// Tuning: the window loads and the LDS-pad test as they were until round 3 (kSerialWindow): a branch around
+// each window load (the compiler waited for each before issuing the next) and a per-lane write to a.n in the
+// pad test (a divergent a.n made every descriptor built from it a waterfall loop).
+enum : int { kSerialWindow = 1 << 20 };
 // Retired probe forms (measured, not adopted; DESIGN §4, profiles/r03/probe_ablation/): 2048 home slot + 3
 // ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94);
 // 524288 a run-length hint in the device table's pad word sending long runs straight to the group walk (c3575ae).
@@ -97,7 +103,7 @@ __device__ __forceinline__ bool block_part_needed(uint32_t blk_lo, uint32_t part
   return MIS + 64 > (int)s0 || 16 * part < 128 - lo;
 }
 
-template <int MIS, int COOP, int LAUX>
+template <int MIS, int COOP, int LAUX, bool SERIAL = false>
 __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t rs, int lane, uint32_t stride,
                                                         uint32_t ipa_off, uint32_t base_lo, Window& h) {
   uint32_t ether_type;
@@ -105,13 +111,31 @@ __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t r
     static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
     u32x4* tile = coop_tile();
     const uint32_t blk = coop_block(ipa_off);
+    // All 8 loads in flight before the first LDS write: a part that is not needed gets an offset past
+    // the descriptor's range (returns zeros, fetches nothing) instead of a branch around its load --
+    // with the branches the compiler waited for each load before issuing the next (8 round trips).
+    if constexpr (SERIAL) { // tuning (kSerialWindow): the round-1..3 form, a branch around each load
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (block_part_needed<MIS>(base_lo + r * stride + blk, part))
+          v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + blk + 16 * part, 0, LAUX);
+        tile[r * 8 + (part ^ (r & 7))] = v;
+      }
+    }
+    u32x4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8 && !SERIAL; ++i) {
       const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (block_part_needed<MIS>(base_lo + r * stride + blk, part))
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * stride + blk + 16 * part, 0, LAUX);
-      tile[r * 8 + (part ^ (r & 7))] = v;
+      const uint32_t off = r * stride + blk + 16 * part;
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, block_part_needed<MIS>(base_lo + r * stride + blk, part) ? off : kNoFetch,
+                                                   0, LAUX);
+    }
+#pragma unroll
+    for (int i = 0; i < 8 && !SERIAL; ++i) {
+      const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+      tile[r * 8 + (part ^ (r & 7))] = v[i];
     }
     constexpr uint32_t p0 = 1; // the window starts at the block's second chunk
 #pragma unroll

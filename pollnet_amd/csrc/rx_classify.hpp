@@ -379,16 +379,25 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
         line_addr[lane] = use ? (uint64_t)(win - 16) : 0ull;
         __syncthreads();
         u32x4* tile = coop_tile();
+        // all 8 loads in flight before the first LDS write (as load_window_strided): a part that is not
+        // needed reads its block's first chunk instead -- a line the same instruction fetches anyway (or,
+        // for an unused row, the ring's first line) -- and is zeroed, rather than a branch around its load
+        u32x4 v[8];
+        bool need[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
           const uint64_t la = line_addr[r];
-          u32x4 v = {0u, 0u, 0u, 0u};
-          if (la && block_part_needed<MIS>((uint32_t)la, part)) {
-            if constexpr (LWIN == 0) v = reinterpret_cast<const u32x4*>(la)[part]; // default policy (tuning)
-            else v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(la) + part);
-          }
-          tile[r * 8 + (part ^ (r & 7))] = v;
+          need[i] = la && block_part_needed<MIS>((uint32_t)la, part);
+          const u32x4* src = need[i] ? reinterpret_cast<const u32x4*>(la) + part
+                                     : reinterpret_cast<const u32x4*>(la ? la : (uint64_t)(uintptr_t)a.frames);
+          if constexpr (LWIN == 0) v[i] = *src; // default policy (tuning)
+          else v[i] = __builtin_nontemporal_load(src);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
+          tile[r * 8 + (part ^ (r & 7))] = need[i] ? v[i] : u32x4{0u, 0u, 0u, 0u};
         }
         __syncthreads();
 #pragma unroll
@@ -422,7 +431,8 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
       }
     }
   } else {
-    ether_type = load_window_strided<MIS, COOP, LWIN>(rs, lane, a.stride, a.ipa_off, (uint32_t)(uintptr_t)wave_slot, h);
+    ether_type = load_window_strided<MIS, COOP, LWIN, (ABL & kSerialWindow) != 0>(rs, lane, a.stride, a.ipa_off,
+                                                                                    (uint32_t)(uintptr_t)wave_slot, h);
   }
   if constexpr (!IDX) win = wave_slot + (uint64_t)lane * a.stride + a.ipa_off;
   FrameState st = header_phase<MIS, ABL>(h, ether_type, live && !bad_off, stream_start((uint64_t)win), a);
@@ -499,7 +509,14 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : 4) void rx
   if constexpr (((GOPT >> 4) & 0xff) > 0) {
     __shared__ uint32_t pad_lds[((GOPT >> 4) & 0xff) * 256];
     pad_lds[lane] = lane;
-    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
+    // never true: keeps the padding allocated.  The test is wave-uniform (readfirstlane), so a.n stays
+    // a scalar: a per-lane write to it made every descriptor built from it divergent, and the compiler
+    // then wrapped each buffer load in a waterfall loop and serialized the window loads.
+    if constexpr (ABL & kSerialWindow) {
+      if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0;
+    } else {
+      if (__builtin_amdgcn_readfirstlane(pad_lds[(lane + 1) & 63]) == 0x7fffffffu) a.n = 0;
+    }
   }
   if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
     // contiguous eighth of the batch instead of every eighth group

@@ -284,6 +284,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 42: launch_one<0, 1, kProdAbl | kLateProbe>(a, s); break;   // walk finished after phase 2
     case 43: launch_one<0, 1, kProdAbl | kAblNoWalk>(a, s); break;   // timing only: home slot decides
     case 45: launch_one<0, 1, kProdAbl | kAblNoWalk | kAblUniformProbe>(a, s); break; // timing only: one line per probe
+    case 47: launch_one<0, 1, kProdAbl | kSerialWindow>(a, s); break; // window loads one round trip each (before round 3)
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;

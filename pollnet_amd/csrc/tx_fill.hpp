@@ -102,7 +102,8 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   // LAUX0: the line-0 window loads keep the default policy (not nt), so the line the
   // patch kernel later writes is still in the memory-side cache
   Window h;
-  (void)load_window_strided<MIS, COOP, LAUX0>(rs, lane, a.stride, a.ipa_off, (uint32_t)(uintptr_t)wave_slot, h);
+  (void)load_window_strided<MIS, COOP, LAUX0, (SABL & kSerialWindow) != 0>(rs, lane, a.stride, a.ipa_off,
+                                                                           (uint32_t)(uintptr_t)wave_slot, h);
   uint8_t* ip = wave_slot + (uint64_t)lane * a.stride + a.ipa_off + MIS;
 
   // IpHeader (Core.h:57-69): tot_len at ip+2, checksum at ip+10

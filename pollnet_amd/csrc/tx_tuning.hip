@@ -116,6 +116,14 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
         return 0;
       }
+      case 43: { // pn_tx_fill's two phases with the window loads serialized as before round 3 (kSerialWindow)
+        TArgs b = a;
+        b.fpw = frames_per_wave(n);
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kExactRange | kSerialWindow>),
+                           dim3((n + b.fpw - 1) / b.fpw), block, 0, s, b);
+        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
+        return 0;
+      }
       case 40: case 41: {
         TArgs b = a;
         b.fpw = frames_per_wave(n);
