@@ -65,9 +65,10 @@ enum : int { kLateProbe = 4096, kAblNoWalk = 8192 };
 // Timing only (with kAblNoWalk): every lane of a wave loads the same home entry (the first lane's), so the
 // probe instruction touches one line instead of up to 64 — isolates the cost of the scattered probe loads.
 enum : int { kAblUniformProbe = 131072 };
-// Tuning: the window loads and the LDS-pad test as they were until round 3 (kSerialWindow): a branch around
-// each window load (the compiler waited for each before issuing the next) and a per-lane write to a.n in the
-// pad test (a divergent a.n made every descriptor built from it a waterfall loop).
+// kSerialWindow: the window loads as they were until round 3, a branch around each (the compiler waits for
+// each before issuing the next); in the RX kernel (tuning only) also the LDS-pad test's per-lane write to a.n
+// that made every descriptor built from it a waterfall loop.  RX production issues all 8 at once (C3 -3.8 %,
+// C5 -4.3 %, C2 equal); the TX fill keeps the serial form, measured faster there (tx_fill.hpp, kTxStream).
 enum : int { kSerialWindow = 1 << 20 };
 // Retired probe forms (measured, not adopted; DESIGN §4, profiles/r03/probe_ablation/): 2048 home slot + 3
 // ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94);

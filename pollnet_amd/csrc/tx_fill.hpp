@@ -81,9 +81,13 @@ constexpr int kWbPatch = -2;
 // SABL: the stream phase's options.  Every stream load is issued (kExactRange): TX batches are
 // mostly full-size frames, where skipping empty loads measured 1.8 % slower at frame_off 2 and
 // equal at 14 (tuning variant 42 = with kSkipEmptyLoads, profiles/r02/s3/tx_skip_ab_off*.json).
+// The window loads go out one round trip apart (kSerialWindow), not all at once as in the RX kernel:
+// the fill measured 1.3 % faster that way at frame_off 2 and 2.5 % at 14, both variant orders, 4 rotating
+// batches (tuning variants 40 vs 43, profiles/r03/window/tx_window_off*.json).
 // SIG: completion word (pn_tx_fill_notify, signal_done in frame_pass.hpp).
+constexpr int kTxStream = kExactRange | kSerialWindow;
 template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false,
-          int SABL = kExactRange, bool SIG = false>
+          int SABL = kTxStream, bool SIG = false>
 __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   const int lane = threadIdx.x;
   const uint32_t wave_base = (XCD ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x) * a.fpw;
@@ -290,10 +294,10 @@ void launch(const TArgs& a, hipStream_t s) {
   const dim3 grid((a.n + a.fpw - 1) / a.fpw), block(kWave);
   // XCD-contiguous group order, as the RX kernel: -1.7 % (profiles/r01_experiments/tx_xcd_order_off{2,14}.json)
   if (coop_layout(a)) {
-    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, WB, 0, 0, 0, true, kExactRange, SIG>), grid, block, 0, s, a);
+    hipLaunchKernelGGL((tx_fill_kernel<MIS, 1, MODE, WB, 0, 0, 0, true, kTxStream, SIG>), grid, block, 0, s, a);
     return;
   }
-  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, WB, 0, 0, 0, true, kExactRange, SIG>), grid, block, 0, s, a);
+  hipLaunchKernelGGL((tx_fill_kernel<MIS, 0, MODE, WB, 0, 0, 0, true, kTxStream, SIG>), grid, block, 0, s, a);
 }
 
 template <int MODE, int WB, bool SIG = false>

@@ -27,7 +27,7 @@ extern "C" int pn_calib_tx_ablated(pn_ctx* ctx, void* frames, uint32_t slot_stri
   if (rc) return rc;
   a.patch = (uint2*)ctx->tx_patch;
   const dim3 grid((n + a.fpw - 1) / a.fpw), block(kWave);
-  constexpr int SABL = kExactRange | kAblNoReduce;
+  constexpr int SABL = kTxStream | kAblNoReduce;
   if (frame_off == 2)
     hipLaunchKernelGGL((tx_fill_kernel<0, 1, PN_TX_TCP, kWbPatch, 0, 0, 0, true, SABL>), grid, block, 0, s, a);
   else
@@ -111,15 +111,15 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
       case 42: { // pn_tx_fill's two phases with empty stream loads skipped (kSkipEmptyLoads, measured, not adopted)
         TArgs b = a;
         b.fpw = frames_per_wave(n);
-        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kExactRange | kSkipEmptyLoads>), dim3((n + b.fpw - 1) / b.fpw), block,
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kTxStream | kSkipEmptyLoads>), dim3((n + b.fpw - 1) / b.fpw), block,
                            0, s, b);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
         return 0;
       }
-      case 43: { // pn_tx_fill's two phases with the window loads serialized as before round 3 (kSerialWindow)
+      case 43: { // pn_tx_fill's two phases with the 8 window loads in flight at once (the RX kernel's form; slower here)
         TArgs b = a;
         b.fpw = frames_per_wave(n);
-        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kExactRange | kSerialWindow>),
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kExactRange>),
                            dim3((n + b.fpw - 1) / b.fpw), block, 0, s, b);
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
         return 0;
