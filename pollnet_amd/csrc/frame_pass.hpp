@@ -70,6 +70,9 @@ enum : int { kAblUniformProbe = 131072 };
 // that made every descriptor built from it a waterfall loop.  RX production issues all 8 at once (C3 -3.8 %,
 // C5 -4.3 %, C2 equal); the TX fill keeps the serial form, measured faster there (tx_fill.hpp, kTxStream).
 enum : int { kSerialWindow = 1 << 20 };
+// Tuning: phase 2 software-pipelined by half batches (stream_phase_pipelined): the full-size waves' form,
+// and with kPipeSkip also the short-frame waves' (kSkipEmptyLoads) form.
+enum : int { kPipeStream = 1 << 21, kPipeSkip = 1 << 22 };
 // Retired probe forms (measured, not adopted; DESIGN §4, profiles/r03/probe_ablation/): 2048 home slot + 3
 // ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94);
 // 524288 a run-length hint in the device table's pad word sending long runs straight to the group walk (c3575ae).
@@ -363,6 +366,132 @@ __device__ __forceinline__ void stream_phase(uint32_t stride, const uint8_t* gro
       const uint32_t tot = __shfl(v, (lane & 7) * 8);
       if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
     }
+  }
+}
+
+// Phase 2 software-pipelined by half batches (kPipeStream; strides up to 2048, where no frame reaches
+// past its two stream KiBs, and every load issued): the next half's 8 loads go out before the current
+// half is summed, so a wave always has 8-16 loads in flight instead of draining to none at each batch
+// boundary.  Same loads, same sums, same reduction as stream_phase.
+template <int ABL, int LAUX, int IDX>
+__device__ __forceinline__ void stream_phase_pipelined(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win,
+                                                       uint32_t n_here, int lane, int end_rel, uint32_t& t_all,
+                                                       uint32_t& pad) {
+  static_assert(ABL & kExactRange, "pipelined phase 2: exact ranges");
+  // kSkipEmptyLoads (short-frame waves): a frame's first-KiB load is always issued (an empty range
+  // fetches nothing) and its second-KiB load only when the frame reaches it -- a branch after all of
+  // the half's first loads, so the compiler's count of loads in flight stays exact for them.
+  constexpr bool kSkip = (ABL & kSkipEmptyLoads) != 0;
+  constexpr int kHalf = kBatch / 2;
+  auto frame_win = [&](uint32_t fi) -> const uint8_t* {
+    if constexpr (IDX) {
+      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)my_win, fi & 63);
+      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(my_win >> 32), fi & 63);
+      return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+    } else {
+      return group_ipa + (uint64_t)fi * stride;
+    }
+  };
+  int ends[kBatch], s0s[kBatch];
+  u32x4 w0s[kBatch], w1s[kBatch];
+  uint32_t acc[kBatch];
+  // the loads of frames fi0 .. fi0+3 into slots j0 .. j0+3 (frames past n_here: end_rel 0, nothing fetched)
+  auto issue = [&](uint32_t fi0, int j0) {
+#pragma unroll
+    for (int q = 0; q < kHalf; ++q) {
+      const int j = j0 + q;
+      const uint32_t fi = fi0 + q; // wave-uniform
+      // past the wave's frames (the last batch's look-ahead): an empty range, the load fetches nothing
+      const int end = fi < n_here ? __builtin_amdgcn_readlane(end_rel, fi & 63) & ~1 : 0;
+      ends[j] = end;
+      const uint32_t end16 = (uint32_t)(end + 3) & ~3u;
+      const uint8_t* fw = frame_win(fi);
+      const int s0 = (int)stream_start((uint64_t)fw);
+      s0s[j] = s0;
+      const __amdgpu_buffer_rsrc_t rs = frame_rsrc(fw, end16);
+      w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX);
+      if constexpr (!kSkip) w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX);
+    }
+    if constexpr (kSkip) {
+#pragma unroll
+      for (int q = 0; q < kHalf; ++q) {
+        const int j = j0 + q;
+        const uint32_t end16 = (uint32_t)(ends[j] + 3) & ~3u;
+        w1s[j] = u32x4{0u, 0u, 0u, 0u};
+        if (end16 > (uint32_t)s0s[j] + 1024) { // wave-uniform
+          const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi0 + q), end16);
+          w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0s[j] + 1024 + lane * 16, 0, LAUX);
+        }
+      }
+    }
+  };
+  // sum slots j0 .. j0+3 (frames fi0 ..) into acc, with the 2-mod-4 correction and the odd-length pad byte
+  auto consume = [&](uint32_t fi0, int j0) {
+#pragma unroll
+    for (int q = 0; q < kHalf; ++q) {
+      const int j = j0 + q;
+      const int end = ends[j], s0 = s0s[j];
+      const u32x4 w0 = w0s[j], w1 = w1s[j];
+      uint32_t sum = 0;
+      sum = dot2(w0.x, 0x10001u, sum);
+      sum = dot2(w0.y, 0x10001u, sum);
+      sum = dot2(w0.z, 0x10001u, sum);
+      sum = dot2(w0.w, 0x10001u, sum);
+      sum = dot2(w1.x, 0x10001u, sum);
+      sum = dot2(w1.y, 0x10001u, sum);
+      sum = dot2(w1.z, 0x10001u, sum);
+      sum = dot2(w1.w, 0x10001u, sum);
+      const int q2 = end - 2 - s0; // wave-uniform
+      if ((end & 2) && q2 >= 0 && q2 < 2048) {
+        const u32x4 w = (q2 < 1024) ? w0 : w1;
+        const int dw = (q2 >> 2) & 3;
+        const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
+        if (lane == ((q2 & 1023) >> 4)) sum -= d >> 16;
+      }
+      acc[j] = sum;
+      const int p = end - 1;
+      if ((__builtin_amdgcn_readlane(end_rel, (fi0 + q) & 63) & 1) && p >= s0 && p < s0 + 2048) {
+        const int qq = p - s0;
+        const u32x4 w = (qq < 1024) ? w0 : w1;
+        const int dw = (qq >> 2) & 3;
+        const uint32_t d = dw == 0 ? w.x : dw == 1 ? w.y : dw == 2 ? w.z : w.w;
+        const uint32_t b = __builtin_amdgcn_readlane((d >> (8 * (qq & 3))) & 0xff, (qq & 1023) >> 4);
+        if ((uint32_t)lane == fi0 + q) pad = b;
+      }
+    }
+  };
+  issue(0, 0);
+  for (uint32_t b0 = 0; b0 < n_here; b0 += kBatch) {
+    issue(b0 + kHalf, kHalf);
+    consume(b0, 0);
+    // the next batch's first half, under this one's second.  Unconditional (past the last batch its
+    // ranges are empty): behind a branch the compiler could no longer count the loads in flight and
+    // would wait for them before summing this batch's second half.
+    issue(b0 + kBatch, 0);
+    consume(b0 + kHalf, kHalf);
+    // transpose-reduce 8 frames x 64 lanes as stream_phase: lane l ends with the total of frame (l>>3)&7
+    uint32_t r8[kBatch];
+#pragma unroll
+    for (int i = 0; i < kBatch; ++i) r8[i] = acc[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const auto r = __builtin_amdgcn_permlane32_swap(r8[i], r8[i + 4], false, false);
+      r8[i] = r[0] + r[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const auto r = __builtin_amdgcn_permlane16_swap(r8[i], r8[i + 2], false, false);
+      r8[i] = r[0] + r[1];
+    }
+    const bool b3 = lane & 8;
+    const uint32_t keep = b3 ? r8[1] : r8[0];
+    const uint32_t send = b3 ? r8[0] : r8[1];
+    uint32_t v = keep + dpp<0x128>(send);
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x141>(v);
+    const uint32_t tot = __shfl(v, (lane & 7) * 8);
+    if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += tot;
   }
 }
 

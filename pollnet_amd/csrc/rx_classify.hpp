@@ -468,9 +468,33 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
       const uint32_t e16 = (uint32_t)((st.end_rel & ~1) + 3) & ~3u;
       const bool short_frame = live && e16 <= stream_start((uint64_t)win) + 1024;
       constexpr int kFull = ABL & ~(kSkipEmptyLoads | kSkipWaveGate);
-      if (__ballot(short_frame) == 0)
-        stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
-                                       st.pad);
+      if (__ballot(short_frame) == 0) {
+        if constexpr ((ABL & kPipeStream) && !IDX) {
+          if (a.stride <= 2048) // no frame reaches past its two stream KiBs
+            stream_phase_pipelined<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane,
+                                                     st.end_rel, st.t_all, st.pad);
+          else
+            stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
+                                           st.t_all, st.pad);
+        } else {
+          stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
+                                         st.t_all, st.pad);
+        }
+      } else if constexpr ((ABL & kPipeSkip) && !IDX) {
+        if (a.stride <= 2048)
+          stream_phase_pipelined<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane,
+                                                 st.end_rel, st.t_all, st.pad);
+        else
+          stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
+                                       st.t_all, st.pad);
+      } else {
+        stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
+                                     st.pad);
+      }
+    } else if constexpr ((ABL & kPipeStream) && !IDX && !(ABL & kSkipEmptyLoads)) {
+      if (a.stride <= 2048)
+        stream_phase_pipelined<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
+                                               st.t_all, st.pad);
       else
         stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
                                      st.pad);
