@@ -70,14 +70,16 @@ enum : int { kAblUniformProbe = 131072 };
 // that made every descriptor built from it a waterfall loop.  RX production issues all 8 at once (C3 -3.8 %,
 // C5 -4.3 %, C2 equal); the TX fill keeps the serial form, measured faster there (tx_fill.hpp, kTxStream).
 enum : int { kSerialWindow = 1 << 20 };
-// Tuning: phase 2 software-pipelined by half batches (stream_phase_pipelined): the full-size waves' form,
-// and with kPipeSkip also the short-frame waves' (kSkipEmptyLoads) form.
-enum : int { kPipeStream = 1 << 21, kPipeSkip = 1 << 22 };
+// With kSkipWaveGate: phase 2 of full-size waves software-pipelined by half batches
+// (stream_phase_pipelined; slot strides up to 2048).  C2 -1.4 %, C3/C5 unchanged (their waves take
+// the skipping form), records identical (profiles/r03/pipe_stream/).  Pipelining the skipping form
+// as well gained 0.2-0.7 % (not adopted); issuing every load so that all waves pipeline cost C3/C5 8 %.
+enum : int { kPipeStream = 1 << 21 };
 // Retired probe forms (measured, not adopted; DESIGN §4, profiles/r03/probe_ablation/): 2048 home slot + 3
 // ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94);
 // 524288 a run-length hint in the device table's pad word sending long runs straight to the group walk (c3575ae).
 // The production RX configuration.
-constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate;
+constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate | kPipeStream;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at
 // r*stride from the descriptor base `rs`, window at slot + ipa_off).  Returns the
@@ -377,11 +379,7 @@ template <int ABL, int LAUX, int IDX>
 __device__ __forceinline__ void stream_phase_pipelined(uint32_t stride, const uint8_t* group_ipa, uint64_t my_win,
                                                        uint32_t n_here, int lane, int end_rel, uint32_t& t_all,
                                                        uint32_t& pad) {
-  static_assert(ABL & kExactRange, "pipelined phase 2: exact ranges");
-  // kSkipEmptyLoads (short-frame waves): a frame's first-KiB load is always issued (an empty range
-  // fetches nothing) and its second-KiB load only when the frame reaches it -- a branch after all of
-  // the half's first loads, so the compiler's count of loads in flight stays exact for them.
-  constexpr bool kSkip = (ABL & kSkipEmptyLoads) != 0;
+  static_assert(!(ABL & kSkipEmptyLoads) && (ABL & kExactRange), "pipelined phase 2: every load issued, exact ranges");
   constexpr int kHalf = kBatch / 2;
   auto frame_win = [&](uint32_t fi) -> const uint8_t* {
     if constexpr (IDX) {
@@ -410,19 +408,7 @@ __device__ __forceinline__ void stream_phase_pipelined(uint32_t stride, const ui
       s0s[j] = s0;
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(fw, end16);
       w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + lane * 16, 0, LAUX);
-      if constexpr (!kSkip) w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX);
-    }
-    if constexpr (kSkip) {
-#pragma unroll
-      for (int q = 0; q < kHalf; ++q) {
-        const int j = j0 + q;
-        const uint32_t end16 = (uint32_t)(ends[j] + 3) & ~3u;
-        w1s[j] = u32x4{0u, 0u, 0u, 0u};
-        if (end16 > (uint32_t)s0s[j] + 1024) { // wave-uniform
-          const __amdgpu_buffer_rsrc_t rs = frame_rsrc(frame_win(fi0 + q), end16);
-          w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0s[j] + 1024 + lane * 16, 0, LAUX);
-        }
-      }
+      w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, s0 + 1024 + lane * 16, 0, LAUX);
     }
   };
   // sum slots j0 .. j0+3 (frames fi0 ..) into acc, with the 2-mod-4 correction and the odd-length pad byte
@@ -469,6 +455,13 @@ __device__ __forceinline__ void stream_phase_pipelined(uint32_t stride, const ui
     // would wait for them before summing this batch's second half.
     issue(b0 + kBatch, 0);
     consume(b0 + kHalf, kHalf);
+    if constexpr (ABL & kAblNoReduce) { // timing only (the ablated ceiling kernel), as stream_phase
+      uint32_t x = 0;
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j) x += acc[j];
+      if ((uint32_t)(lane >> 3) == b0 / kBatch) t_all += x;
+      continue;
+    }
     // transpose-reduce 8 frames x 64 lanes as stream_phase: lane l ends with the total of frame (l>>3)&7
     uint32_t r8[kBatch];
 #pragma unroll

@@ -480,24 +480,10 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
           stream_phase<kFull, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
                                          st.t_all, st.pad);
         }
-      } else if constexpr ((ABL & kPipeSkip) && !IDX) {
-        if (a.stride <= 2048)
-          stream_phase_pipelined<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane,
-                                                 st.end_rel, st.t_all, st.pad);
-        else
-          stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
-                                       st.t_all, st.pad);
       } else {
         stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
                                      st.pad);
       }
-    } else if constexpr ((ABL & kPipeStream) && !IDX && !(ABL & kSkipEmptyLoads)) {
-      if (a.stride <= 2048)
-        stream_phase_pipelined<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel,
-                                               st.t_all, st.pad);
-      else
-        stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
-                                     st.pad);
     } else {
       stream_phase<ABL, LAUX, IDX>(a.stride, wave_slot + a.ipa_off, (uint64_t)win, n_here, lane, st.end_rel, st.t_all,
                                    st.pad);

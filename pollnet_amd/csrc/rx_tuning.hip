@@ -285,10 +285,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 43: launch_one<0, 1, kProdAbl | kAblNoWalk>(a, s); break;   // timing only: home slot decides
     case 45: launch_one<0, 1, kProdAbl | kAblNoWalk | kAblUniformProbe>(a, s); break; // timing only: one line per probe
     case 47: launch_one<0, 1, kProdAbl | kSerialWindow>(a, s); break; // window loads one round trip each (before round 3)
-    case 48: launch_one<0, 1, kProdAbl | kPipeStream>(a, s); break;   // full-size waves' phase 2 pipelined by half batches
-    case 50: launch_one<0, 1, kProdAbl | kPipeStream | kPipeSkip>(a, s); break; // both wave forms pipelined
-    case 49: launch_one<0, 1, (kProdAbl & ~(kSkipEmptyLoads | kSkipWaveGate)) | kPipeStream>(a, s); break; // every wave
-                                                                      // pipelined, every load issued (empty ones fetch nothing)
+    case 48: launch_one<0, 1, kProdAbl & ~kPipeStream>(a, s); break;  // phase 2 not pipelined (before round 3)
     case 11: launch_one<0, 1, kAblNoProbe | kProdAbl>(a, s); break;           // timing-only ablations from here
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;

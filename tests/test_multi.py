@@ -106,10 +106,12 @@ def _window_worker(rank, world, port, flag, out_dir, shm=False):
         barrier = ShmBarrier(dist, rank, world)
     wall, own = common_window(body, dist, barrier)
     if barrier is not None:
-        t0 = time.perf_counter()
+        ts = []
         for _ in range(200):
+            t0 = time.perf_counter()
             barrier()
-        per = (time.perf_counter() - t0) / 200
+            ts.append(time.perf_counter() - t0)
+        per = sorted(ts)[len(ts) // 2]  # median: a rank descheduled by a busy host does not skew it
         barrier.close(dist)
     else:
         per = 0.0
