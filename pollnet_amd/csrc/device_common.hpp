@@ -31,6 +31,10 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP, 0xf, 0xf, false);
 }
 
+// A buffer-load offset past every descriptor's range (at most a few MiB here): the load returns zeros and
+// fetches nothing.  Used instead of a branch around a load, so that loads stay in flight together.
+constexpr uint32_t kNoFetch = 0x80000000u;
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const uint8_t* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }

@@ -26,8 +26,6 @@ constexpr int kWinBytes = 16 * kWinChunks;
 using Window = Win<4 * kWinChunks>;
 
 constexpr uint32_t kPadUnknown = 0xFFFFFFFFu;
-// A buffer-load offset past every descriptor's range (<= 4 MiB here): the load returns zeros and fetches nothing.
-constexpr uint32_t kNoFetch = 0x80000000u;
 
 // Timing-only ablations (scripts/variants.py; records are wrong when set):
 // bit0 skip the conn-table probe, bit1 skip the lane reduction, bit2 no tail

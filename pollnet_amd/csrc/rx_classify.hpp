@@ -326,8 +326,11 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   } else if constexpr (ABL & kAblGlobalStore) { // the record through a plain global store (SAUX ignored)
     *reinterpret_cast<u32x4*>(a.out + f) = rec;
   } else {
-    // one coalesced 1-KiB store per wave; the descriptor covers this wave's 64 records
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc((const uint8_t*)(a.out + (f & ~63u)), 64 * 16);
+    // one coalesced 1-KiB store per wave; the descriptor covers this wave's 64 records.  The block is the
+    // same on every lane (a wave's frames never cross a 64-frame boundary): readfirstlane makes the
+    // descriptor scalar, where a per-lane one would be a waterfall loop around the store
+    const uint32_t blk = __builtin_amdgcn_readfirstlane(f & ~63u);
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc((const uint8_t*)(a.out + blk), 64 * 16);
     __builtin_amdgcn_raw_buffer_store_b128(rec, rs, (f & 63u) * 16, 0, SAUX);
   }
 }

@@ -59,20 +59,28 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
     // frame f0 + 16 i + (l >> 2)
     __shared__ u32x4 tile[256 * 4];
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t f0 = blockIdx.x * 256 + w * 64;
+    // wave-uniform (readfirstlane): a descriptor built from a per-lane value is a waterfall loop
+    const uint32_t f0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 256 + w * 64);
     u32x4* wt = tile + w * 256;
     const uint32_t c = lane & 3;
     const uint32_t n_here = f0 < a.n ? min(64u, a.n - f0) : 0u;
-    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.frames + (uint64_t)f0 * a.stride + a.ipa_off - kPre,
-                                                 n_here ? (n_here - 1) * a.stride + 64 : 0);
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane(n_here ? (n_here - 1) * a.stride + 64 : 0u); // kept scalar
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.frames + (uint64_t)f0 * a.stride + a.ipa_off - kPre, nrec);
+    // all 4 loads in flight before the LDS writes: a chunk that is not needed gets an offset past the
+    // range (zeros, no fetch) instead of a branch around its load (which serialized the loads)
+    const bool need = (c == 0 && chunk_needed<MIS>(0)) || (c == 1 && chunk_needed<MIS>(1)) ||
+                      (c == 2 && chunk_needed<MIS>(2)) || (c == 3 && chunk_needed<MIS>(3));
+    u32x4 v[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint32_t r = 16 * i + (lane >> 2);
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if ((c == 0 && chunk_needed<MIS>(0)) || (c == 1 && chunk_needed<MIS>(1)) || (c == 2 && chunk_needed<MIS>(2)) ||
-          (c == 3 && chunk_needed<MIS>(3)))
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, r * a.stride + 16 * c, 0, LAUX); // past n: zeros, no fetch
-      wt[r * 4 + (c ^ (r & 3))] = v;
+      const uint32_t off = (r * a.stride + 16 * c) | (need ? 0u : kNoFetch); // past n or not needed: zeros
+      v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LAUX);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = 16 * i + (lane >> 2);
+      wt[r * 4 + (c ^ (r & 3))] = v[i];
     }
     __syncthreads();
 #pragma unroll
