@@ -151,7 +151,14 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
     const int end_rel = ok ? (int)(even_end | (tot & 1)) : 0;
     uint32_t t_all = window_part<MIS>(h, end_rel & ~1, stream_start((uint64_t)(ip - MIS)));
     uint32_t pad = kPadUnknown;
-    stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
+    if constexpr ((SABL & kPipeStream) && !(SABL & kSkipEmptyLoads)) {
+      if (a.stride <= 2048) // no frame reaches past its two stream KiBs
+        stream_phase_pipelined<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
+      else
+        stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
+    } else {
+      stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
+    }
     if (ok && (tot & 1) && pad == kPadUnknown) pad = ip[tot]; // pad byte inside the window
     const uint32_t tcp_chk_old = h.template u16<MIS + 36>(); // TcpHeader.checksum at tcp+16 (Core.h:84)
     const uint32_t s_seg = t_all - s_ip_stored - tcp_chk_old - ((tot & 1) ? (pad << 8) : 0u);
