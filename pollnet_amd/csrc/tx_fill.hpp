@@ -83,7 +83,8 @@ constexpr int kWbPatch = -2;
 // equal at 14 (tuning variant 42 = with kSkipEmptyLoads, profiles/r02/s3/tx_skip_ab_off*.json).
 // The window loads go out one round trip apart (kSerialWindow), not all at once as in the RX kernel:
 // the fill measured 1.3 % faster that way at frame_off 2 and 2.5 % at 14, both variant orders, 4 rotating
-// batches (tuning variants 40 vs 43, profiles/r03/window/tx_window_off*.json).
+// batches (tuning variants 40 vs 43, profiles/r03/window/tx_window_off*.json).  Phase 2 pipelined by half
+// batches as in the RX kernel gained 0.1-0.2 % here (profiles/r03/pipe_stream/tx_pipe_*.json): not taken.
 // SIG: completion word (pn_tx_fill_notify, signal_done in frame_pass.hpp).
 constexpr int kTxStream = kExactRange | kSerialWindow;
 template <int MIS, int COOP, int MODE, int WB = kWbPatch, int SAUX = 0, int LAUX0 = 0, int PADK = 0, bool XCD = false,
@@ -151,14 +152,7 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
     const int end_rel = ok ? (int)(even_end | (tot & 1)) : 0;
     uint32_t t_all = window_part<MIS>(h, end_rel & ~1, stream_start((uint64_t)(ip - MIS)));
     uint32_t pad = kPadUnknown;
-    if constexpr ((SABL & kPipeStream) && !(SABL & kSkipEmptyLoads)) {
-      if (a.stride <= 2048) // no frame reaches past its two stream KiBs
-        stream_phase_pipelined<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
-      else
-        stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
-    } else {
-      stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
-    }
+    stream_phase<SABL, kLoadAux, 0>(a.stride, wave_slot + a.ipa_off, 0, n_here, lane, end_rel, t_all, pad);
     if (ok && (tot & 1) && pad == kPadUnknown) pad = ip[tot]; // pad byte inside the window
     const uint32_t tcp_chk_old = h.template u16<MIS + 36>(); // TcpHeader.checksum at tcp+16 (Core.h:84)
     const uint32_t s_seg = t_all - s_ip_stored - tcp_chk_old - ((tot & 1) ? (pad << 8) : 0u);

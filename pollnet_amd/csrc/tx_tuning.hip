@@ -124,17 +124,6 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
         return 0;
       }
-      case 44: case 45: { // pn_tx_fill's two phases with phase 2 pipelined by half batches (44: serial window, 45: not)
-        TArgs b = a;
-        b.fpw = frames_per_wave(n);
-        const dim3 g((n + b.fpw - 1) / b.fpw);
-        if (variant == 44)
-          hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kTxStream | kPipeStream>), g, block, 0, s, b);
-        else
-          hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true, kExactRange | kPipeStream>), g, block, 0, s, b);
-        hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
-        return 0;
-      }
       case 40: case 41: {
         TArgs b = a;
         b.fpw = frames_per_wave(n);
