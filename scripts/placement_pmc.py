@@ -125,6 +125,7 @@ def orders(out_path, k):
     st = torch.cuda.current_stream()
     legs = {"product_xcd_order": lambda q: ctx.classify(q, stride, off, n, res, st),
             "blockidx_order": lambda q: tn.classify_variant(ctx, q, stride, off, n, res, st, 36),
+            "no_pipe_stream": lambda q: tn.classify_variant(ctx, q, stride, off, n, res, st, 48),
             "stream_read": lambda q: tn.calib_stream_read(ctx, q, n * stride, sink, st)}
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     times = [{name: [] for name in legs} for _ in ptrs]
