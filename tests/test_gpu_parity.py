@@ -170,6 +170,29 @@ def test_ragged_batch_sizes(torch_cuda, ctx, n):
     assert_same(got, exp)
 
 
+@pytest.mark.parametrize("n", [8, 9, 64, 100, 1000, 16369, 32737, 65473])
+@pytest.mark.parametrize("frame_off,stride", [(2, 2048), (18, 2048), (2, 1536), (0, 2048), (2, 4096)])
+def test_full_size_waves_ragged_extents(torch_cuda, ctx, n, frame_off, stride):
+    """Waves whose every frame reaches its second stream KiB take the full-size form of phase 2, which
+    is software-pipelined by half batches at strides up to 2048 (frame_pass.hpp stream_phase_pipelined):
+    C4 frames (1024 flows) cut to random tot_len in [1300, 1500] -- odd lengths with a non-zero byte after
+    the segment, 2-mod-4 extents, stale checksums -- at every frames-per-wave choice and ragged n."""
+    p = pa.rx.GenParams.for_config(4)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    s = pa.gen_frames(p, n, stride, frame_off)
+    rng = np.random.default_rng(n * 131 + frame_off * 7 + stride)
+    tot = rng.integers(1300, 1501, n)
+    ip = frame_off + 14
+    s[:, ip + 2] = (tot >> 8).astype(np.uint8)
+    s[:, ip + 3] = (tot & 0xFF).astype(np.uint8)
+    s[np.arange(n), ip + tot] = rng.integers(1, 256, n).astype(np.uint8)  # the byte after the segment
+    exp = orc.classify_batch(s, stride, frame_off, n, e, m, t.max_conn_cnt)
+    assert (exp["flags"] & 0x2000).sum() == 0  # nothing truncated: every frame streams both KiBs' worth
+    got = gpu_classify(torch_cuda, ctx, s, stride, frame_off, n, e, m, t.max_conn_cnt, canary=64)
+    assert_same(got, exp)
+
+
 @pytest.mark.parametrize("n,frame_off,stride", [(9, 18, 2048), (100, 18, 2048), (20000, 18, 2048), (333, 2, 1536),
                                                 (20001, 0, 4096)])
 def test_small_batch_wave_split_layouts(torch_cuda, ctx, n, frame_off, stride):
