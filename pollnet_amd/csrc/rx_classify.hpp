@@ -500,7 +500,8 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
 // GRP > 1 (tuning variants): GRP consecutive groups per workgroup, their records kept in
 // LDS and written in one GRP-KiB burst at the end (scripts/write_grouping.py probe).
 // GOPT (tuning): bit 0 = GRP groups per workgroup but records stored per group (no LDS);
-// bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 4;
+// bit 1 / bit 2 = register budget for 3 / 2 waves per SIMD instead of 4 (a budget for 5 spills and costs 8.6 %
+// on the round-3 final tree, profiles/r03/window/five_waves_c*.json);
 // GOPT >> 4 = KiB of LDS padding, which caps workgroups per CU.  Production pads 2 KiB:
 // with the 8-KiB window tile that is 10 KiB per workgroup, 16 per CU = 4 waves/SIMD where
 // registers allowed 5 before the grouped probe -- C2 -1.2 %, C3 -2.5 %, C5 -0.3 % (3 waves: C3 +9 %, C5 +13 %;
