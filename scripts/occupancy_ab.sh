@@ -1,6 +1,6 @@
 #!/bin/bash
 # Production (4 waves/SIMD) vs a 5-wave register budget (variant 52; 96 VGPRs, 16 B/lane of spill), after the
-# round-3 window fix and pipelining; records must equal production.
+# round-3 window fix and pipelining.  Variant 52 was removed after the measurement (profiles/r03/window/five_waves_c*.json).
 set -o pipefail
 OUT=gpurun_out/${1:-occ_ab}
 mkdir -p $OUT
