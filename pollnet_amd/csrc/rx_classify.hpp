@@ -418,15 +418,22 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
     }
     if (live && !coop_done) {
       if (!bad_off) {
-        // window chunk c spans eth + (14 - MIS) + 16c .. +16: load it only inside avail
+        // window chunk c spans eth + (14 - MIS) + 16c .. +16: used only inside avail.  A chunk past it
+        // re-reads chunk 0 (a line this lane fetches anyway) and is dropped, rather than a branch around
+        // its load, so the 7 loads are in flight together
+        u32x4 v[kWinChunks];
+#pragma unroll
+        for (int c = 0; c < kWinChunks; ++c) {
+          const bool in = (uint32_t)(14 - MIS + 16 * c + 16) <= a.avail;
+          v[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(win) + (in ? c : 0));
+        }
 #pragma unroll
         for (int c = 0; c < kWinChunks; ++c) {
           if ((uint32_t)(14 - MIS + 16 * c + 16) <= a.avail) {
-            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(win) + c);
-            h.d[4 * c + 0] = v.x;
-            h.d[4 * c + 1] = v.y;
-            h.d[4 * c + 2] = v.z;
-            h.d[4 * c + 3] = v.w;
+            h.d[4 * c + 0] = v[c].x;
+            h.d[4 * c + 1] = v[c].y;
+            h.d[4 * c + 2] = v[c].z;
+            h.d[4 * c + 3] = v[c].w;
           }
         }
         if constexpr (MIS >= 2) ether_type = h.template u16<MIS - 2>();
