@@ -384,18 +384,29 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
         u32x4* tile = coop_tile();
         // all 8 loads in flight before the first LDS write (as load_window_strided): a part that is not
         // needed reads its block's first chunk instead -- a line the same instruction fetches anyway (or,
-        // for an unused row, the ring's first line) -- and is zeroed, rather than a branch around its load
+        // for an unused row, the first used frame's block) -- and is zeroed, rather than a branch around it
+        const uint64_t used = __ballot(use);
+        const uint32_t l0 = used ? (uint32_t)__builtin_ctzll(used) : 0u;
+        const uint64_t wb = (uint64_t)(win - 16);
+        const uint64_t safe = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(wb >> 32), l0) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((uint32_t)wb, l0);
         u32x4 v[8];
         bool need[8];
+        const u32x4* src[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
           const uint64_t la = line_addr[r];
           need[i] = la && block_part_needed<MIS>((uint32_t)la, part);
-          const u32x4* src = need[i] ? reinterpret_cast<const u32x4*>(la) + part
-                                     : reinterpret_cast<const u32x4*>(la ? la : (uint64_t)(uintptr_t)a.frames);
-          if constexpr (LWIN == 0) v[i] = *src; // default policy (tuning)
-          else v[i] = __builtin_nontemporal_load(src);
+          src[i] = need[i] ? reinterpret_cast<const u32x4*>(la) + part : reinterpret_cast<const u32x4*>(la ? la : safe);
+          v[i] = u32x4{0u, 0u, 0u, 0u};
+        }
+        if (used != 0) { // wave-uniform: a wave with no frame to classify loads nothing
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            if constexpr (LWIN == 0) v[i] = *src[i]; // default policy (tuning)
+            else v[i] = __builtin_nontemporal_load(src[i]);
+          }
         }
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
