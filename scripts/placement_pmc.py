@@ -75,6 +75,57 @@ def run(out_path, k):
         hip.hipFree(C.c_void_p(q))
 
 
+def channels(root):
+    """Per-instance counters (rocprofv3 --output-format json: one record per TCC channel x XCC) of each buffer's
+    counter-phase dispatches: per pass <root>/<name>/pmc_results.json + <root>/<name>.run.json.  For each buffer:
+    the dispatches' median duration under the profiler, the per-instance medians, their spread across the 16
+    channels (summed over XCCs) and across all 128 instances."""
+    out = {}
+    for run_json in sorted(glob.glob(os.path.join(root, "*.run.json"))):
+        name = os.path.basename(run_json)[: -len(".run.json")]
+        meta = json.load(open(run_json))
+        res = glob.glob(os.path.join(root, name, "**", "*results.json"), recursive=True)
+        if not res:
+            continue
+        tool = json.load(open(res[0]))["rocprofiler-sdk-tool"][0]
+        names = {k["kernel_id"]: k["kernel_name"] for k in tool["kernel_symbols"]}
+        cinfo = {c["id"]["handle"]: c for c in tool["counters"]}
+        recs = []
+        for r in tool["callback_records"]["counter_collection"]:
+            di = r["dispatch_data"]["dispatch_info"]
+            if "rx_classify" not in names.get(di["kernel_id"], ""):
+                continue
+            by_counter = {}
+            for x in r["records"]:
+                by_counter.setdefault(x["counter_id"]["handle"], []).append(x["value"])
+            dur = r["dispatch_data"]["end_timestamp"] - r["dispatch_data"]["start_timestamp"]
+            recs.append((di["dispatch_id"], dur, by_counter))
+        recs.sort()
+        k, reps = len(meta["buffers"]), meta["reps_per_buffer"]
+        recs = recs[-k * reps:]
+        bufs = []
+        for i, b in enumerate(meta["buffers"]):
+            rs = recs[i * reps:(i + 1) * reps]
+            entry = {**b, "profiled_dispatch_us": round(statistics.median(r[1] for r in rs) / 1e3, 2)}
+            for cid, vals in rs[0][2].items():
+                cname = cinfo[cid]["name"]
+                inst = [statistics.median(r[2][cid][j] for r in rs) for j in range(len(vals))]
+                dims = [{d["dimension_name"]: d["index"] for d in x["dimensions"]} for x in cinfo[cid]["instances"]]
+                chan = {}
+                for v, d in zip(inst, dims):
+                    chan[d.get("DIMENSION_INSTANCE", 0)] = chan.get(d.get("DIMENSION_INSTANCE", 0), 0) + v
+                cv = [chan[c] for c in sorted(chan)]
+                mean_c, mean_i = statistics.mean(cv), statistics.mean(inst)
+                entry[cname] = {"total": sum(inst), "per_channel": cv,
+                                "channel_max_over_mean": round(max(cv) / mean_c, 4) if mean_c else None,
+                                "channel_cv": round(statistics.pstdev(cv) / mean_c, 4) if mean_c else None,
+                                "instance_max_over_mean": round(max(inst) / mean_i, 4) if mean_i else None,
+                                "instance_cv": round(statistics.pstdev(inst) / mean_i, 4) if mean_i else None}
+            bufs.append(entry)
+        out[name] = bufs
+    print(json.dumps(out, indent=1))
+
+
 def summarize(root):
     """Per pass directory <root>/<name>/ (rocprofv3 csv) + <root>/<name>.run.json: counters per buffer."""
     out = {}
@@ -212,5 +263,7 @@ if __name__ == "__main__":
         alloc(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "orders":
         orders(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 12)
+    elif sys.argv[1] == "channels":
+        channels(sys.argv[2])
     else:
         summarize(sys.argv[2])
