@@ -345,7 +345,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
 // block 16-B aligned inside the ring load blocks cooperatively, other waves per-lane
 // bounds-checked windows.
 // Register target: 4 waves/SIMD.  Until round 3 the MIS % 4 == 0 kernels fit 5 (<= 96 VGPRs) and the
-// LDS pad below held them at 4; the grouped probe takes them to 102 VGPRs, so registers and pad now agree.
+// LDS pad below held them at 4; the grouped probe takes them to 102 VGPRs (104 with the pipelined phase 2), so registers and pad agree.
 template <int MIS, int COOP, int ABL, int LAUX, int SAUX, int IDX, int LWIN>
 __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wave_base, const int lane, u32x4* lds_recs) {
   if (wave_base >= a.n) return;
