@@ -58,3 +58,39 @@ def test_match_streams_vs_numpy(cfg, frame_off):
         assert np.array_equal(got[:n], exp), (k, int(np.count_nonzero(got[:n] != exp)))
         assert (exp != pa.PN_NO_STREAM).any() and (exp == pa.PN_NO_STREAM).any()
     ctx.close()
+
+
+# Every IP-header class (frame_off + 14) % 16 the kernel is instantiated for, slot strides from the
+# contract's minimum (frame_off + 96, on the 16-B grid) to 64 KiB, and batches that end inside a wave
+# (the per-wave buffer range and the no-fetch offsets of the cooperative loads).
+@pytest.mark.parametrize("frame_off,stride,n", [(2, 112, 1), (4, 112, 63), (6, 1536, 1000), (8, 2048, 65),
+                                                (12, 4096, 130), (14, 128, 257), (16, 65536, 200),
+                                                (26, 2048, 4097)])
+def test_match_streams_layouts(frame_off, stride, n):
+    import torch
+
+    rng = np.random.default_rng(frame_off * 7 + n)
+    p = pa.rx.GenParams.for_config(3)
+    full = pa.gen_frames(p, n, 2048, frame_off)
+    slots = np.zeros((n, stride), np.uint8)
+    w = min(stride, 2048)
+    slots[:, :w] = full[:, :w]  # the filter reads only the first frame_off + 38 bytes of a slot
+    slots[rng.random(n) < 0.2, frame_off + 23] = 17  # some UDP frames
+    ctx = pa.RxContext(0)
+    dev = torch.from_numpy(slots.reshape(-1)).cuda()
+    out = torch.full((n + 64,), 0xAB, dtype=torch.int32, device="cuda")
+    flt = np.roll(_filters(rng, slots, frame_off, 8), -1)  # the catch-all dst filter last: every id can win
+    ctx.match_streams(dev, stride, frame_off, n, flt, out, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    assert (got[n:] == 0xAB).all(), "wrote past n"
+    exp = match_streams_np(slots, frame_off, flt)
+    assert np.array_equal(got[:n], exp), int(np.count_nonzero(got[:n] != exp))
+    # no filters: every frame gets PN_NO_STREAM; n = 0 writes nothing
+    ctx.match_streams(dev, stride, frame_off, n, np.zeros(0, pa.STREAM_FILTER_DTYPE), out,
+                      torch.cuda.current_stream())
+    ctx.match_streams(dev, stride, frame_off, 0, flt, out[n:], torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(np.uint32)
+    assert (got[:n] == pa.PN_NO_STREAM).all() and (got[n:] == 0xAB).all()
+    ctx.close()
