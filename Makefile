@@ -40,6 +40,8 @@ SERVERTEST = tests/cpp/test_tcp_server
 PEERTEST = tests/cpp/test_tcp_server_peer
 CLISRVTEST = tests/cpp/test_tcp_client_server
 TXHOSTTEST = tests/cpp/test_tx_host
+REFSERVERTEST = tests/cpp/test_ref_server
+REFCONNTEST = tests/cpp/test_ref_conn
 
 # Host programs that include HIP headers: compiled by hipcc with the device pass pinned to gfx950
 # (without --offload-arch hipcc would add a default-arch device pass for nothing)
@@ -49,8 +51,13 @@ HOSTHIP = $(HIPCC) --offload-arch=$(ARCH)
 # (oracle/_ref/*.inc, never committed, never sent to the GPU box).  Where neither that text nor
 # the reference is present (a fresh GPU box), they are not rebuilt: their prebuilt binaries are used.
 REF_INCS = oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
+# efvitcp's own TcpConn / TcpServer / EfviTcpServer and Core's ef_vi-free members (oracle/ref.mk `conn`)
+CONN_INCS = $(addprefix oracle/_ref/,conn_tcpconn.inc conn_tcpserver.inc conn_efvitcpserver.inc conn_timer_types.inc \
+  conn_sendbuf.inc conn_core_consts.inc conn_core_init.inc conn_core_getns.inc conn_core_rst.inc conn_core_rx.inc \
+  conn_core_tbl.inc conn_core_timer.inc conn_core_members.inc core_defs.inc conn_tcpclient_head.inc \
+  conn_tcpclient_tail.inc conn_efvitcpclient.inc conn_core_autoport.inc)
 HAVE_REF_TEXT = $(or $(wildcard $(REFDIR)/example/tcpserver.cc),$(and $(wildcard oracle/_ref/tcpserver_handler.inc),$(wildcard oracle/_ref/tcpclient_handler.inc)))
-REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST))
+REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST) $(REFSERVERTEST) $(REFCONNTEST))
 
 all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST) $(TXHOSTTEST)
 
@@ -62,12 +69,24 @@ $(SERVERTEST): tests/cpp/test_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/s
 	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
-$(REF_INCS):
+$(REF_INCS) $(CONN_INCS):
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR) $(@:oracle/%=%); \
 	else echo "$@: no $(REFDIR) to extract it from" >&2; exit 1; fi
 
+# GpuTcpServer (twin and GPU) vs the reference's own EfviTcpServer / TcpServer / TcpConn (oracle/ref_server.hpp)
+$(REFSERVERTEST): tests/cpp/test_ref_server.cpp tests/cpp/peer_population.hpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
+  oracle/ref_server.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp \
+  include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) $(CONN_INCS)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -Wno-unused-result -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# RxConn (the receive half) vs the reference's own TcpConn::onPack, segment by segment (host only)
+$(REFCONNTEST): tests/cpp/test_ref_conn.cpp tests/cpp/segframes.hpp oracle/ref_server.hpp include/pollnet_amd/rx_conn.hpp \
+  $(HDRS) $(ORACLE) $(CONN_INCS)
+	g++ -O2 -std=c++17 -Wall -Wno-unused-result -o $@ $< -Loracle -loracle -Wl,-rpath,'$$ORIGIN/../../oracle'
+
 # GpuTcpClient <-> GpuTcpServer running both reference example handlers over a lossy in-memory wire
-$(CLISRVTEST): tests/cpp/test_tcp_client_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
+$(CLISRVTEST): tests/cpp/test_tcp_client_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp oracle/ref_server.hpp $(CONN_INCS) \
   include/pollnet_amd/tcp_client.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp \
   include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) \
   oracle/_ref/tcpserver_handler.inc oracle/_ref/tcpclient_handler.inc
@@ -75,7 +94,7 @@ $(CLISRVTEST): tests/cpp/test_tcp_client_server.cpp tests/cpp/segframes.hpp test
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
 
 # GpuTcpServer against reactive in-memory TCP peers (loss, timers, windows), GPU vs twin
-$(PEERTEST): tests/cpp/test_tcp_server_peer.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
+$(PEERTEST): tests/cpp/test_tcp_server_peer.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp tests/cpp/peer_population.hpp \
   include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE)
 	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
@@ -164,6 +183,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST)
+	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST) $(REFSERVERTEST) $(REFCONNTEST)
 
 .PHONY: all ref clean

@@ -114,6 +114,7 @@ class RxConn {
   bool pendingAck() const { return pending_ack_; }
   bool closed() const { return closed_; }
   uint32_t recentTs() const { return recent_ts_; }
+  uint32_t lastAckSeq() const { return last_ack_seq_; } // the ack number last sent (updateLastAck)
 
   // One classified segment of this connection.  eth: the frame (host memory);
   // rec: its pn_result.

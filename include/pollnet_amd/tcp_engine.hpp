@@ -845,7 +845,9 @@ class TcpEngine {
     c.peer_ip_ = peer_ip;
     c.peer_port_ = peer_port;
     c.local_port_ = local_port;
-    c.err_ = nullptr;
+    // err_ is left as the slot's last connection left it: TcpConn::reset does not touch UserData
+    // (EfviTcp.h:208-211), so a server's new connection reports the previous one's error until
+    // its own (the client's is set by connect's result, EfviTcp.h:122)
     c.established_ = c.fin_sent_ = c.fin_received_ = c.fast_re_ = c.in_recover_ = false;
     c.send_una_ = c.send_next_ = c.data_next_size_ = c.dup_ack_cnt_ = c.retries_ = 0;
     c.data_next_ = 1;

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "../../include/pollnet_amd/tcp_client.hpp"
+#include "../../oracle/ref_server.hpp"
 #include "../../include/pollnet_amd/tcp_server.hpp"
 #include "segframes.hpp"
 #include "server_harness.hpp"
@@ -168,6 +169,27 @@ PN_END_SERVER
 #include "../../oracle/_ref/tcpclient_handler.inc"
 PN_END_CLIENT
 
+// Both ends as the reference's own EfviTcpServer / EfviTcpClient (oracle/ref_server.hpp: efvitcp's
+// TcpServer, TcpClient, TcpConn and Core compiled from /root/reference, ef_vi plumbing restated)
+#define PN_DEFINE_REF_ENDS(NS)                                                      \
+  namespace NS {                                                                    \
+  using TcpServer = efvitcp::EfviTcpServer<ServerConf>;                             \
+  using TcpClient = efvitcp::EfviTcpClient<ClientConf>;                             \
+  TcpServer& server = *new TcpServer;                                               \
+  TcpClient& client = *new TcpClient;                                               \
+  Packet pack;                                                                      \
+  namespace srv {                                                                   \
+  LogStream cout;                                                                   \
+  int exits = 0;                                                                    \
+  void exit(int) { ++exits; }                                                       \
+  void pollOnce() {
+
+PN_DEFINE_REF_ENDS(on_ref)
+#include "../../oracle/_ref/tcpserver_handler.inc"
+PN_END_SERVER
+#include "../../oracle/_ref/tcpclient_handler.inc"
+PN_END_CLIENT
+
 struct Result {
   std::string srv_log, cli_log;
   std::vector<std::vector<uint8_t>> wire;
@@ -181,11 +203,13 @@ static bool run(S& server, C& client, void (*poll_srv)(), void (*poll_cli)(), Lo
   Wire w(seed);
   slog.os.str(std::string());
   clog.os.str(std::string());
-  g_wire = &w;
+  static Wire drain; // a re-init closes the previous run's connections (RSTs): not part of this run
+  g_wire = &drain;
   g_now = kT0;
   if (!server.initWithLink("10.0.0.1", 1234, g_now)) return std::printf("server init: %s\n", server.getLastError()), false;
   if (!client.initWithLink("10.0.0.2", "10.0.0.1", 1234, 40000, g_now))
     return std::printf("client init: %s\n", client.getLastError()), false;
+  g_wire = &w;
   const int64_t ms = 1 << 20; // one tick (ns >> 20)
   for (int t = 0; t < 22000; t++) {  // ~22 s of simulated time: ~20 send timeouts
     g_now += ms;
@@ -208,6 +232,89 @@ static bool run(S& server, C& client, void (*poll_srv)(), void (*poll_cli)(), Lo
   static Wire sink; // frames sent after the run (the ends' destructors RST open connections)
   g_wire = &sink;
   return true;
+}
+
+// The reference ends: the same wire, clock and script; their ef_vi plumbing goes to WireLinks.
+static bool run_ref(Result& out, uint32_t seed, bool wall_clock = false) {
+  using namespace on_ref;
+  static WireLink<true> slink;
+  static WireLink<false> clink;
+  // fresh ends for every run: the reference's init re-arms nothing (its timer lists, ids and table
+  // are set up for one init per object), so a second init over live connections is not meaningful
+  static Wire drain;
+  g_wire = &drain; // the old ends' destructors RST their connections
+  server.~TcpServer();
+  client.~TcpClient();
+  new (&server) TcpServer;
+  new (&client) TcpClient;
+  Wire w(seed);
+  srv::cout.os.str(std::string());
+  cli::cout.os.str(std::string());
+  g_wire = &w;
+  g_now = kT0;
+  efvitcp::RefEnv& env = efvitcp::refEnv();
+  env.now_ns = g_now;
+  env.init_ns = g_now;
+  env.wall_clock_time = wall_clock;
+  env.link = &slink;
+  env.fill = [](void* l, uint8_t* s, uint32_t st, uint32_t off, uint32_t cap) {
+    return static_cast<WireLink<true>*>(l)->fill(s, st, off, cap);
+  };
+  env.send = [](void* l, const uint8_t* eth, uint32_t len) { static_cast<WireLink<true>*>(l)->send(eth, len); };
+  env.local_ip = slink.localIp();
+  std::memcpy(env.local_mac, kServerMac, 6);
+  if (!server.init("wire", "10.0.0.1", 1234)) return std::printf("ref server init: %s\n", server.getLastError()), false;
+  env.link = &clink;
+  env.fill = [](void* l, uint8_t* s, uint32_t st, uint32_t off, uint32_t cap) {
+    return static_cast<WireLink<false>*>(l)->fill(s, st, off, cap);
+  };
+  env.send = [](void* l, const uint8_t* eth, uint32_t len) { static_cast<WireLink<false>*>(l)->send(eth, len); };
+  env.local_ip = clink.localIp();
+  std::memcpy(env.local_mac, kClientMac, 6);
+  std::memcpy(env.peer_mac, kServerMac, 6);
+  if (!client.init("wire", "10.0.0.1", 1234, 40000)) return std::printf("ref client init: %s\n", client.getLastError()), false;
+  const int64_t ms = 1 << 20;
+  for (int t = 0; t < 22000; t++) {
+    g_now += ms;
+    env.now_ns = g_now;
+    cli::pollOnce();
+    srv::pollOnce();
+  }
+  out.connected = client.isConnected();
+  client.close("bye");
+  for (int t = 0; t < 3000; t++) {
+    g_now += ms;
+    env.now_ns = g_now;
+    cli::pollOnce();
+    srv::pollOnce();
+  }
+  out.conns_after = server.getConnCnt();
+  out.srv_log = srv::cout.os.str();
+  out.cli_log = cli::cout.os.str();
+  out.wire = w.log;
+  out.drops = w.drops;
+  static Wire sink;
+  g_wire = &sink;
+  env.wall_clock_time = false;
+  return true;
+}
+
+// The reconnect clock, the one other intended difference: EfviTcpClient::poll times its reconnect
+// interval with time(0), the host's wall clock (EfviTcp.h:116-121), whatever `ns` the caller polls
+// with; GpuTcpClient times it on the poll's clock.  Under a simulated clock (25 s of polls in well
+// under a second of wall time) the reference client with the real time(0) does not reconnect after
+// close("bye") (5-s ConnRetrySec not yet passed on the wall clock); the product does, as the
+// reference does when its time(0) follows the same clock (the runs above).
+static int reconnect_clock_divergence() {
+  Result r;
+  if (!run_ref(r, 0, true)) return 1;
+  size_t conns = 0;
+  for (size_t p = 0; (p = r.srv_log.find("new connection from", p)) != std::string::npos; p++) conns++;
+  const bool ok = conns == 1 && r.conns_after == 0;
+  std::printf("reconnect clock: reference client on the wall clock made %zu connection(s), %u open after the close "
+              "(product on the poll clock: 2, 1) -> %s\n",
+              conns, r.conns_after, ok ? "as documented" : "UNEXPECTED");
+  return ok ? 0 : 1;
 }
 
 static int check(const char* tag, const Result& r) {
@@ -259,6 +366,29 @@ int main(int argc, char** argv) {
     Result tw;
     if (!run(ts, tc, tps, tpc, tsl, tcl, tw, seed)) return 100;
     f += check((std::string("twin") + name).c_str(), tw);
+    if (!name[0]) { // the classify-every-poll ends against the reference's own ends
+      on_ref::pack = Packet{};
+      Result rr;
+      if (!run_ref(rr, seed)) return 100;
+      f += check("reference", rr);
+      const bool logs = rr.srv_log == tw.srv_log && rr.cli_log == tw.cli_log;
+      size_t same = 0;
+      while (same < rr.wire.size() && same < tw.wire.size() && rr.wire[same] == tw.wire[same]) same++;
+      const bool wire = same == rr.wire.size() && same == tw.wire.size();
+      std::printf("twin vs reference EfviTcpServer/EfviTcpClient: handler logs %s, wire frames %s (%zu vs %zu%s)\n",
+                  logs ? "identical" : "DIFFERENT", wire ? "identical" : "DIFFERENT", tw.wire.size(), rr.wire.size(),
+                  wire ? "" : (", first difference at " + std::to_string(same)).c_str());
+      f += !logs + !wire;
+      if (!wire) {
+        auto dump = [](const char* t, const std::vector<uint8_t>& x) {
+          std::printf("  %s %zu B:", t, x.size());
+          for (size_t i = 0; i < x.size() && i < 64; i++) std::printf(" %02x", x[i]);
+          std::printf("\n");
+        };
+        if (same < tw.wire.size()) dump("twin", tw.wire[same]);
+        if (same < rr.wire.size()) dump("ref ", rr.wire[same]);
+      }
+    }
     if (show) std::printf("server log:\n%s\nclient log:\n%s\n", tw.srv_log.c_str(), tw.cli_log.c_str());
     if (gpu) {
       Result g;
@@ -272,6 +402,7 @@ int main(int argc, char** argv) {
     }
     return f;
   };
+  fail += reconnect_clock_divergence();
   for (uint32_t seed = 0; seed < runs; seed++) {
     if (runs > 1) std::printf("== loss pattern %u ==\n", seed);
     fail += mode("", on_twin::server, on_twin::client, on_twin::srv::pollOnce, on_twin::cli::pollOnce,

@@ -27,6 +27,7 @@
 
 #include "segframes.hpp"
 #include "server_harness.hpp"
+#include "peer_population.hpp"
 
 using namespace pollnet_amd;
 
@@ -61,255 +62,6 @@ struct PeerConfPipe : PeerConf {
   static const bool RxPipeline = true;
 };
 
-static const int64_t kT0 = (int64_t)777777 << 20;
-
-enum Kind : uint8_t { kFinEnd, kRstEnd, kIdle, kServerFin };
-
-struct Client {
-  uint32_t ip;
-  uint16_t port;
-  Kind kind;
-  uint32_t start, window;
-  std::vector<uint8_t> stream;
-  std::mt19937 rng;
-  // state
-  enum { kWait, kSynSent, kEst, kDone } st = kWait;
-  uint32_t isn = 0, srv_isn = 0;
-  uint32_t snd_una = 0, snd_nxt = 0, srv_wnd = 0, last_tx = 0, last_progress = 0;
-  bool fin_sent = false, got_rst = false, got_fin = false, refused = false, established = false;
-  std::vector<uint8_t> echo;
-  std::map<uint32_t, std::vector<uint8_t>> ooo;
-};
-
-// Population and loss seeds: run k of a soak (argv[2] runs) perturbs both; 0 = the original.
-static uint32_t g_seed = 0;
-
-// The client population as a link: fill() = frames the clients send this tick,
-// send() = a frame from the server, handed to its client.
-struct PeerLink {
-  std::vector<Client> clients;
-  std::vector<std::vector<uint8_t>> q;   // client -> server, this tick
-  std::vector<std::vector<uint8_t>> out; // every server frame (the comparison)
-  std::mt19937 loss{0xD20Bu ^ g_seed};
-  uint32_t tick = 0;
-  uint32_t drops_c2s = 0, drops_s2c = 0;
-
-  const char* open(const char*) { return nullptr; }
-  uint32_t localIp() const { return htonl(0x0a000001); }
-  const uint8_t* localMac() const {
-    static const uint8_t m[6] = {2, 0, 0, 0, 0, 1};
-    return m;
-  }
-
-  void emit(Client& c, uint32_t seq, uint32_t ack, uint8_t flags, const uint8_t* p = nullptr, uint32_t len = 0,
-            bool mss = false) {
-    segtest::Seg s;
-    s.src_ip = c.ip;
-    s.src_port = c.port;
-    s.seq = seq;
-    s.ack = ack;
-    s.flags = flags;
-    s.payload = p;
-    s.len = len;
-    if (mss) s.opts = {2, 4, 0x05, 0xb4};
-    uint8_t buf[2048];
-    const uint32_t n = segtest::build(buf, s);
-    segtest::put16(buf + 48, (uint16_t)c.window); // the client's receive window
-    segtest::put16(buf + 50, 0);
-    {
-      uint8_t* tcp = buf + 34;
-      const uint32_t tcp_len = n - 34;
-      uint32_t ph = (c.ip >> 16) + (c.ip & 0xffff) + (0x0a000001 >> 16) + (0x0a000001 & 0xffff) + 6 + tcp_len;
-      segtest::put16(tcp + 16, segtest::rfc_sum(tcp, tcp_len, ph));
-    }
-    q.emplace_back(buf, buf + n);
-  }
-  uint32_t ackNum(const Client& c) const { return c.srv_isn + 1 + (uint32_t)c.echo.size() + (c.got_fin ? 1 : 0); }
-
-  void step(Client& c) {
-    const uint32_t base = c.isn + 1;
-    switch (c.st) {
-      case Client::kWait:
-        if (tick >= c.start) {
-          c.st = Client::kSynSent;
-          c.last_tx = tick;
-          emit(c, c.isn, 0, segtest::SYN, nullptr, 0, true);
-        }
-        break;
-      case Client::kSynSent:
-        if (tick - c.last_tx >= 300) {
-          c.last_tx = tick;
-          emit(c, c.isn, 0, segtest::SYN, nullptr, 0, true);
-        }
-        break;
-      case Client::kEst: {
-        const uint32_t limit = c.kind == kIdle ? (uint32_t)c.stream.size() / 2 : (uint32_t)c.stream.size();
-        if (c.snd_una < c.snd_nxt && tick - c.last_progress >= 150 && tick - c.last_tx >= 150) { // RTO: resend una
-          const uint32_t n = std::min<uint32_t>(c.snd_nxt - c.snd_una, 1000);
-          emit(c, base + c.snd_una, ackNum(c), segtest::ACK | segtest::PSH, c.stream.data() + c.snd_una, n);
-          c.last_tx = tick;
-        }
-        for (int k = 0; k < 3 && c.snd_nxt < limit && !c.fin_sent; k++) {
-          const uint32_t room = c.srv_wnd - std::min(c.srv_wnd, c.snd_nxt - c.snd_una); // what the window admits
-          const uint32_t n = std::min<uint32_t>({limit - c.snd_nxt, 1 + (uint32_t)(c.rng() % 1460), room});
-          if (n == 0) break;
-          emit(c, base + c.snd_nxt, ackNum(c), segtest::ACK | segtest::PSH, c.stream.data() + c.snd_nxt, n);
-          if (c.snd_una == c.snd_nxt) c.last_progress = tick;
-          c.snd_nxt += n;
-          c.last_tx = tick;
-        }
-        const bool all_acked = c.snd_una == limit && c.snd_nxt == limit;
-        // the handler echoes whole 8-byte words on ports divisible by 5 (the rest comes with the FIN)
-        const uint32_t echo_due = c.port % 5 == 0 ? limit & ~7u : limit;
-        if (c.kind == kRstEnd && all_acked && c.echo.size() >= echo_due) {
-          emit(c, base + c.snd_nxt, 0, segtest::RST);
-          c.st = Client::kDone;
-        } else if ((c.kind == kFinEnd && all_acked && c.echo.size() >= echo_due) || (c.got_fin && !c.fin_sent)) {
-          if (!c.fin_sent || tick - c.last_tx >= 200) { // (re)send our FIN until the server's RST
-            emit(c, base + c.snd_nxt, ackNum(c), segtest::ACK | segtest::FIN);
-            c.fin_sent = true;
-            c.last_tx = tick;
-          }
-        } else if (c.fin_sent && tick - c.last_tx >= 200) {
-          emit(c, base + c.snd_nxt, ackNum(c), segtest::ACK | segtest::FIN);
-          c.last_tx = tick;
-        } else if (tick - c.last_tx >= 300) { // keepalive / window probe: a live server ACKs, a closed one RSTs
-          emit(c, base + c.snd_nxt - 1, ackNum(c), segtest::ACK);
-          c.last_tx = tick;
-        }
-        break;
-      }
-      case Client::kDone: break;
-    }
-  }
-
-  uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
-    ++tick;
-    for (auto& c : clients) step(c);
-    uint32_t n = 0;
-    size_t i = 0;
-    for (; i < q.size() && n < cap; i++) {
-      if (loss() % 100 < 3) {
-        drops_c2s++;
-        continue;
-      }
-      uint8_t* s = slots + (size_t)n * stride;
-      std::memset(s, 0, stride);
-      std::memcpy(s + off, q[i].data(), q[i].size());
-      n++;
-    }
-    q.erase(q.begin(), q.begin() + i);
-    return n;
-  }
-
-  void send(const uint8_t* eth, uint32_t len) {
-    out.emplace_back(eth, eth + len);
-    if (loss() % 100 < 3) {
-      drops_s2c++;
-      return;
-    }
-    uint16_t dport;
-    std::memcpy(&dport, eth + 36, 2);
-    Client* cp = nullptr;
-    for (auto& c : clients)
-      if (htons(c.port) == dport) cp = &c;
-    if (!cp || cp->st == Client::kDone) return;
-    Client& c = *cp;
-    const uint8_t fl = eth[47];
-    const uint32_t seq = srv_detail::rd32(eth + 38), ack = srv_detail::rd32(eth + 42);
-    const uint16_t wnd = (uint16_t)(eth[48] << 8 | eth[49]);
-    const uint32_t plen = len - 54;
-    if (fl & segtest::RST) {
-      c.got_rst = true;
-      if (c.st == Client::kSynSent) c.refused = true;
-      c.st = Client::kDone;
-      return;
-    }
-    if ((fl & segtest::SYN) && (fl & segtest::ACK)) {
-      if (c.st == Client::kSynSent) {
-        c.srv_isn = seq;
-        c.st = Client::kEst;
-        c.established = true;
-        c.srv_wnd = wnd;
-        c.last_progress = tick;
-      }
-      if (c.st == Client::kEst) emit(c, c.isn + 1 + c.snd_nxt, ackNum(c), segtest::ACK); // (re-)ACK the SYN-ACK
-      return;
-    }
-    if (c.st != Client::kEst) return;
-    // ACK field
-    const uint32_t acked = ack - (c.isn + 1);
-    if ((int32_t)(acked - c.snd_una) > 0 && acked <= c.snd_nxt) {
-      c.snd_una = acked;
-      c.last_progress = tick;
-    }
-    c.srv_wnd = wnd;
-    // data + FIN from the server
-    bool owe_ack = false;
-    if (plen) {
-      const uint32_t off = seq - (c.srv_isn + 1);
-      if (off <= c.echo.size() && off + plen > c.echo.size()) {
-        c.echo.insert(c.echo.end(), eth + 54 + (c.echo.size() - off), eth + 54 + plen);
-        for (auto it = c.ooo.begin(); it != c.ooo.end() && it->first <= c.echo.size();) {
-          if (it->first + it->second.size() > c.echo.size())
-            c.echo.insert(c.echo.end(), it->second.begin() + (c.echo.size() - it->first), it->second.end());
-          it = c.ooo.erase(it);
-        }
-      } else if (off > c.echo.size()) {
-        c.ooo[off].assign(eth + 54, eth + 54 + plen);
-      }
-      owe_ack = true;
-    }
-    if ((fl & segtest::FIN) && seq + plen == c.srv_isn + 1 + c.echo.size() && !c.got_fin) {
-      c.got_fin = true;
-      owe_ack = true;
-    }
-    if (owe_ack) emit(c, c.isn + 1 + c.snd_nxt, ackNum(c), segtest::ACK);
-  }
-};
-
-template <class Conn>
-struct PeerHandler {
-  std::string* log;
-  void line(const char* what, Conn& c) {
-    sockaddr_in a;
-    c.getPeername(a);
-    char b[160];
-    std::snprintf(b, sizeof b, "%s %u:%u id=%u err=%s echoed=%u\n", what, ntohl(a.sin_addr.s_addr), ntohs(a.sin_port),
-                  c.getConnId(), c.getLastError() ? c.getLastError() : "-", c.echoed);
-    *log += b;
-  }
-  bool allowNewConnection(uint32_t ip, uint16_t port_be) { return ntohs(port_be) % 7 != 0; }
-  void onTcpConnected(Conn& c) {
-    c.echoed = 0;
-    c.fin_asked = false;
-    line("connected", c);
-  }
-  uint32_t onTcpData(Conn& c, const uint8_t* d, uint32_t n) {
-    sockaddr_in a;
-    c.getPeername(a);
-    const uint16_t port = ntohs(a.sin_port);
-    if (port % 5 == 0 && n > 7) { // consume only whole 8-byte words: the rest is re-presented
-      const uint32_t take = n & ~7u;
-      if (!c.fin_asked && c.writeNonblock(d, take)) c.echoed += take;
-      return n - take;
-    }
-    if (!c.fin_asked && c.writeNonblock(d, n)) c.echoed += n;
-    if (port % 11 == 0 && c.echoed >= 4000 && !c.fin_asked) { // half-close from the server
-      c.fin_asked = true;
-      c.sendFin();
-      line("sendFin", c);
-    }
-    return 0;
-  }
-  void onTcpDisconnect(Conn& c) { line("disconnect", c); }
-  void onRecvTimeout(Conn& c) {
-    line("recv timeout", c);
-    c.close("timeout");
-  }
-  void onSendTimeout(Conn& c) { line("send timeout", c); }
-};
-
 template <class Backend, class Conf = PeerConf>
 struct Run {
   using Server = GpuTcpServer<Conf, PeerLink, Backend>;
@@ -337,25 +89,6 @@ struct Run {
     return true;
   }
 };
-
-static std::vector<Client> population() {
-  std::mt19937_64 rng(0xC11E27ull + 0x9E3779B97F4A7C15ull * g_seed);
-  std::vector<Client> cs(120);
-  for (uint32_t i = 0; i < cs.size(); i++) {
-    Client& c = cs[i];
-    c.ip = 0x0a020000 | (i + 1);
-    c.port = (uint16_t)(20000 + i * 13);
-    c.kind = (Kind)(i % 4 == 3 ? kIdle : i % 3 == 2 ? kRstEnd : kFinEnd);
-    if (c.port % 11 == 0) c.kind = kServerFin;
-    c.start = 1 + (uint32_t)(rng() % 400);
-    c.window = (i % 6 == 1) ? 2500 : 60000;
-    c.stream.resize(2000 + rng() % 20000);
-    for (auto& b : c.stream) b = (uint8_t)rng();
-    c.isn = (uint32_t)rng();
-    c.rng.seed((uint32_t)rng());
-  }
-  return cs;
-}
 
 template <class R>
 static int check(const char* tag, R& r) {

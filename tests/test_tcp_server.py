@@ -83,10 +83,14 @@ def test_client_server_twin_reference_examples():
     """GpuTcpClient <-> GpuTcpServer over a lossy in-memory wire, running the reference's
     example client and server handlers (tcpclient.cc:68-95, tcpserver.cc:61-90) unchanged:
     connect, 1-s send timeouts echoed in order, close, reconnect (sequential backends);
-    8 loss patterns."""
+    8 loss patterns.  Each classify-every-poll run is also run with both ends as the reference's
+    own EfviTcpServer / EfviTcpClient (oracle/ref_server.hpp: efvitcp's TcpServer, TcpClient,
+    TcpConn and Core compiled from /root/reference): every wire frame and both logs identical."""
     p = _clisrv("twin", 8)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout
+    assert p.stdout.count("twin vs reference EfviTcpServer/EfviTcpClient: handler logs identical, wire frames "
+                          "identical") == 8, p.stdout
 
 
 @pytest.mark.gpu
