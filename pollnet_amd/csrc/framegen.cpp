@@ -113,7 +113,11 @@ void gen_one(const pn_gen_params& p, const std::vector<Flow>& flows, uint64_t gi
   // flow
   Flow f;
   if ((p.cfg == 3 || p.cfg == 5) && r.below(64) == 0) {
-    f = {ip4(10, 2, r.below(256), r.below(256)), __builtin_bswap16((uint16_t)(1024 + r.below(64000)))};
+    // one draw per statement: the frames must not depend on the compiler's argument order
+    const uint32_t c = r.below(256);
+    const uint32_t d = r.below(256);
+    const uint32_t port = 1024 + r.below(64000);
+    f = {ip4(10, 2, c, d), __builtin_bswap16((uint16_t)port)};
   } else if (p.cfg == 2) {
     f = flows[0];
   } else {
@@ -200,7 +204,10 @@ void gen_one(const pn_gen_params& p, const std::vector<Flow>& flows, uint64_t gi
   } else {
     uint32_t d = r.below(2048);
     if (d < 2) {
-      if (plen) pay[r.below(plen)] ^= (uint8_t)(1u << r.below(8));
+      if (plen) {
+        const uint32_t bit = r.below(8); // (the committed goldens draw the bit before the byte)
+        pay[r.below(plen)] ^= (uint8_t)(1u << bit);
+      }
       else tcp[16] ^= 0x40;
     } else if (d == 2) {
       ip[8] ^= 0x10; // TTL: IP sum breaks, TCP (no TTL in pseudo-header) stays valid

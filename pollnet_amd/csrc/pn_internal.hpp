@@ -156,6 +156,12 @@ inline int notify_counter(pn_ctx* ctx, int kind, hipStream_t s, uint32_t** out) 
     e = hipMalloc(&ctx->sig_count, 128);
     if (e == hipSuccess) e = hipMemsetAsync(ctx->sig_count, 0, 128, s); // ordered before this first launch
     if (e != hipSuccess) return hip_err(ctx, e, "hipMalloc(notify counters)");
+    // both counters were zeroed on s: a first launch of the other kind on another stream waits for it
+    for (pn_fence& f : ctx->sig) {
+      f.s = s;
+      f.state = 1;
+    }
+    note_stream(ctx, s);
   }
   int rc = fence_use(ctx, ctx->sig[kind], s);
   if (rc) return rc;

@@ -544,11 +544,7 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : 4) void rx
     // never true: keeps the padding allocated.  The test is wave-uniform (readfirstlane), so a.n stays
     // a scalar: a per-lane write to it made every descriptor built from it divergent, and the compiler
     // then wrapped each buffer load in a waterfall loop and serialized the window loads.
-    if constexpr (ABL & kSerialWindow) {
-      if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0;
-    } else {
-      if (__builtin_amdgcn_readfirstlane(pad_lds[(lane + 1) & 63]) == 0x7fffffffu) a.n = 0;
-    }
+    if (__builtin_amdgcn_readfirstlane(pad_lds[(lane + 1) & 63]) == 0x7fffffffu) a.n = 0;
   }
   if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
     // contiguous eighth of the batch instead of every eighth group

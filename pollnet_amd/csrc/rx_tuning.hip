@@ -87,7 +87,8 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_var_kernel(const uint8_
   __shared__ uint32_t pad_lds[512];
   const int lane = threadIdx.x;
   pad_lds[lane] = lane;
-  if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) n = 0; // never true: keeps the padding allocated
+  // never true: keeps the padding allocated (wave-uniform, so n and the descriptors stay scalar)
+  if (__builtin_amdgcn_readfirstlane(pad_lds[(lane + 1) & 63]) == 0x7fffffffu) n = 0;
   const uint32_t wave_base = xcd_group(blockIdx.x, gridDim.x) * kFramesPerWave;
   if (wave_base >= n) return;
   const uint32_t n_here = min((uint32_t)kFramesPerWave, n - wave_base);
@@ -97,7 +98,9 @@ __global__ __launch_bounds__(kWave) void calib_slot_read_var_kernel(const uint8_
     u32x4 w0s[kBatch], w1s[kBatch];
 #pragma unroll
     for (int j = 0; j < kBatch; ++j) {
-      const uint32_t nb = (b0 + j < n_here) ? min(lens[wave_base + b0 + j], min(stride, 2048u)) : 0u;
+      // one frame per load: its length is the same on every lane (scalar descriptor)
+      const uint32_t nb = __builtin_amdgcn_readfirstlane(
+          (b0 + j < n_here) ? min(lens[wave_base + b0 + j], min(stride, 2048u)) : 0u);
       const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wb + (uint64_t)(b0 + j) * stride, nb);
       w0s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, 0, 0);
       w1s[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, 1024 + lane * 16, 0, 0);

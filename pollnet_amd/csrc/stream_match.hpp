@@ -93,12 +93,16 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
     }
     if (f >= a.n) return;
   } else {
+    // one descriptor per wave (scalar), each lane at its own slot's offset
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t f0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 256 + (threadIdx.x >> 6) * 64);
+    const uint32_t n_here = f0 < a.n ? min(64u, a.n - f0) : 0u;
+    const uint32_t nrec = __builtin_amdgcn_readfirstlane(n_here ? (n_here - 1) * a.stride + 64 : 0u);
     if (f >= a.n) return;
-    const __amdgpu_buffer_rsrc_t rs =
-        frame_rsrc(a.frames + (uint64_t)f * a.stride + a.ipa_off - kPre, kPre + 48);
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc(a.frames + (uint64_t)f0 * a.stride + a.ipa_off - kPre, nrec);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * c, 0, 0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * a.stride + 16 * c, 0, 0);
       h.d[4 * c + 0] = v.x;
       h.d[4 * c + 1] = v.y;
       h.d[4 * c + 2] = v.z;
@@ -129,7 +133,7 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
     }
   }
   if constexpr (SAUX >= 0) {
-    const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.out + (f & ~255u)), 256 * 4);
+    const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.out + blockIdx.x * 256), 256 * 4); // scalar
     __builtin_amdgcn_raw_buffer_store_b32(id, ro, (f & 255u) * 4, 0, SAUX);
   } else {
     a.out[f] = id;

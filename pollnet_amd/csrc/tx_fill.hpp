@@ -95,7 +95,10 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
   if constexpr (PADK > 0) {
     __shared__ uint32_t pad_lds[PADK * 256];
     pad_lds[lane] = lane;
-    if (pad_lds[(lane + 1) & 63] == 0x7fffffffu) a.n = 0; // never true: keeps the padding allocated
+    // never true: keeps the padding allocated.  Wave-uniform (readfirstlane) so a.n stays scalar: a
+    // per-lane write would make the descriptors built from it divergent (waterfall loops, as in the RX
+    // kernel's pad test before round 3)
+    if (__builtin_amdgcn_readfirstlane(pad_lds[(lane + 1) & 63]) == 0x7fffffffu) a.n = 0;
   }
   if (wave_base >= a.n) return;
   const uint32_t f = wave_base + lane;
@@ -172,7 +175,9 @@ __global__ __launch_bounds__(kWave, 5) void tx_fill_kernel(TArgs a) {
     if (live) reinterpret_cast<u32x4*>(a.patch)[f] = u32x4{ip_chk, l4, tot_word, f};
   } else if constexpr (WB == -4) { // timing only: the 16-B record through RX's buffer store (sc1)
     if (live) {
-      const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.patch + 2 * (f & ~63u)), 64 * 16);
+      // the wave's 64-record block: wave-uniform (readfirstlane), so the descriptor stays scalar
+      const uint32_t blk = __builtin_amdgcn_readfirstlane(f & ~63u);
+      const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.patch + 2 * blk), 64 * 16);
       __builtin_amdgcn_raw_buffer_store_b128(u32x4{ip_chk, l4, tot_word, f}, ro, (f & 63u) * 16, 0, kStoreAux);
     }
   } else {

@@ -2,6 +2,7 @@
 shards, no exchange, conn table replicated.  Used by bench.py and the gloo tests."""
 from __future__ import annotations
 
+import os
 import time
 
 
@@ -39,6 +40,11 @@ class ShmBarrier:
         dist.broadcast_object_list(name, src=0)
         if rank != 0:
             self.shm = shared_memory.SharedMemory(name=name[0])
+            # attaching registers the segment with this process's resource tracker too (Python < 3.13),
+            # which would unlink it again at exit after rank 0 has: only the creator owns it
+            from multiprocessing import resource_tracker
+
+            resource_tracker.unregister(self.shm._name, "shared_memory")
         self.cells = np.ndarray((world, 8), dtype=np.int64, buffer=self.shm.buf)
         if rank == 0:
             self.cells[:] = 0
@@ -49,11 +55,15 @@ class ShmBarrier:
         self.cells[self.rank, 0] = self.epoch
         col = self.cells[:, 0]
         deadline = None
+        spins = 0
         while col.min() < self.epoch:
+            spins += 1
             if deadline is None:
                 deadline = time.monotonic() + self.timeout_s
             elif time.monotonic() > deadline:
                 raise TimeoutError(f"rank {self.rank}: shared-memory barrier {self.epoch} timed out")
+            if spins > 256:  # past the first tens of microseconds: let an oversubscribed peer run
+                os.sched_yield()
 
     def close(self, dist):
         dist.barrier()  # nobody reads the page any more

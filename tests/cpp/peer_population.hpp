@@ -362,7 +362,7 @@ static std::vector<Client> population() {
 
 
 // Clients that send adversarial segment streams (kChaos, ports >= 30000) beside ordinary ones.
-static std::vector<Client> chaos_population(uint32_t n_chaos = 60, uint32_t n_plain = 20) {
+inline std::vector<Client> chaos_population(uint32_t n_chaos = 60, uint32_t n_plain = 20) {
   std::mt19937_64 rng(0xC4A05ull + 0x9E3779B97F4A7C15ull * g_seed);
   auto U = [&](uint32_t lo, uint32_t hi) { return lo + (uint32_t)(rng() % (hi - lo + 1)); };
   std::vector<Client> cs(n_chaos + n_plain);

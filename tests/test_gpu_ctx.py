@@ -206,3 +206,56 @@ def test_tx_scratch_across_streams(torch_cuda):
     got_small = small.cpu().numpy().reshape(n, STRIDE)[: 3 * 4096]
     assert np.array_equal(got_small, exp[: 3 * 4096])
     c.close()
+
+
+def test_notify_counters_zeroed_before_either_kind(torch_cuda):
+    """The notify counters are zeroed on the stream of the ctx's first notify launch.  A first
+    launch of the OTHER kind on another stream must wait for that zeroing: with the first
+    classify_notify queued behind a spin, a tx_fill_notify on a free stream does not complete until
+    the spin is released; then both words arrive, and again on a repeat of both."""
+    torch = torch_cuda
+    p = pa.rx.GenParams.for_config(3)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    n = 512
+    s = pa.gen_frames(p, n, STRIDE, FRAME_OFF)
+    exp = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, threads=8)
+    ref_tx = torch.from_numpy(s.reshape(-1).copy()).cuda()
+    c0 = pa.RxContext(0)
+    c0.tx_fill(ref_tx, STRIDE, FRAME_OFF, n)
+    torch.cuda.synchronize()
+    c0.close()
+    exp_tx = ref_tx.cpu().numpy()
+    c = pa.RxContext(0)
+    c.set_conn_table(t)
+    slots = torch.zeros(n * STRIDE, dtype=torch.uint8, pin_memory=True)
+    slots.numpy()[:] = s.reshape(-1)
+    txf = torch.zeros(n * STRIDE, dtype=torch.uint8, pin_memory=True)
+    rec = torch.zeros(n * 16, dtype=torch.uint8, pin_memory=True)
+    words = torch.zeros(64, dtype=torch.int32, pin_memory=True)
+    wnp = words.numpy()
+    held, free = torch.cuda.Stream(), torch.cuda.Stream()
+    spin = Spin(torch, held)
+    try:
+        txf.numpy()[:] = s.reshape(-1)
+        c.classify_notify(slots, STRIDE, FRAME_OFF, n, rec, words[0:], 5, held)   # first notify: zeroing on held
+        c.tx_fill_notify(txf, STRIDE, FRAME_OFF, n, words[16:], 6, stream=free)  # other kind, other stream
+        time.sleep(0.1)
+        tx_waited = int(wnp[16]) == 0 and spin.done() == 0
+    finally:
+        spin.release()
+    assert tx_waited, "tx_fill_notify ran before the counters were zeroed"
+    for rnd in range(2):
+        tok_c, tok_t = 5 + 10 * rnd, 6 + 10 * rnd
+        if rnd:
+            rec.zero_()
+            txf.numpy()[:] = s.reshape(-1)
+            c.classify_notify(slots, STRIDE, FRAME_OFF, n, rec, words[0:], tok_c, held)
+            c.tx_fill_notify(txf, STRIDE, FRAME_OFF, n, words[16:], tok_t, stream=free)
+        t0 = time.time()
+        while int(wnp[0]) != tok_c or int(wnp[16]) != tok_t:
+            assert time.time() - t0 < 10, f"round {rnd}: words {int(wnp[0])}, {int(wnp[16])}"
+        assert np.array_equal(rec.numpy().view(pa.RESULT_DTYPE), exp)
+        assert np.array_equal(txf.numpy(), exp_tx)
+    torch.cuda.synchronize()
+    c.close()
