@@ -29,6 +29,13 @@ using namespace pn_dev;
 using pn_internal::hip_err;
 using pn_internal::set_err;
 
+// A filter as values and care-masks: frame passes it iff ((field ^ v) & m) == 0 for its three words
+// (a zero filter field is a wildcard: mask 0).  ports = src_port | dst_port << 16, both as stored.
+struct MatchMask {
+  uint32_t vs, vd, vp; // src ip, dst ip, ports
+  uint32_t ms, md, mp;
+};
+
 struct MatchArgs {
   const uint8_t* frames;
   uint32_t* out;
@@ -37,6 +44,7 @@ struct MatchArgs {
   uint32_t ipa_off; // (frame_off + 14) & ~15
   uint32_t n_filters;
   pn_stream_filter f[PN_MAX_STREAM_FILTERS];
+  MatchMask m[PN_MAX_STREAM_FILTERS];
 };
 
 // MIS = (frame_off + 14) % 16: the IP header's offset in its 16-B chunk.  The window
@@ -140,6 +148,92 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
   }
 }
 
+// Round 4 form: the same cooperative 64-B loads (4 lanes per frame, one line request per frame), then
+//   - each wave orders its own LDS tile round trip by itself: the DS instructions of one wave execute
+//     in order, so a wave reads its tile right after writing it, without waiting at a workgroup barrier
+//     for the other waves' loads;
+//   - G groups of 64 frames per wave, all G x 4 loads in flight before the first group is compared;
+//   - the filters as value / care-mask words (MatchMask): per filter 3 xor, 1 and, 2 and-or, 1 compare and
+//     1 select per frame, no branch, last to first so the first passing filter wins.
+// OPT & 2 (tuning): the loads and the tile round trip alone, no compare or store (its ceiling).
+template <int MIS, int G, int LAUX, int OPT = 0>
+__global__ __launch_bounds__(256) void match_streams_mask_kernel(MatchArgs a) {
+  constexpr uint32_t kWaveFrames = 64 * G;
+  __shared__ u32x4 tile[4 * 256];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t f0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x >> 6) + w) * kWaveFrames);
+  if (f0 >= a.n) return; // wave-uniform, and no workgroup barrier below
+  const uint32_t n_here = min(kWaveFrames, a.n - f0);
+  const __amdgpu_buffer_rsrc_t rs =
+      frame_rsrc(a.frames + (uint64_t)f0 * a.stride + a.ipa_off - kPre, (n_here - 1) * a.stride + 64);
+  u32x4* wt = tile + w * 256;
+  const uint32_t c = lane & 3;
+  const bool need = (c == 0 && chunk_needed<MIS>(0)) || (c == 1 && chunk_needed<MIS>(1)) ||
+                    (c == 2 && chunk_needed<MIS>(2)) || (c == 3 && chunk_needed<MIS>(3));
+  // instruction (g, i): lane l loads chunk l & 3 of frame 64 g + 16 i + (l >> 2); rows past n_here
+  // read zeros (the descriptor's range), unneeded chunks fetch nothing
+  u32x4 v[G][4];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = 64 * g + 16 * i + (lane >> 2);
+      v[g][i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (r * a.stride + 16 * c) | (need ? 0u : kNoFetch), 0, LAUX);
+    }
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t r = 16 * i + (lane >> 2);
+      wt[r * 4 + (c ^ (r & 3))] = v[g][i];
+    }
+    Win<16> h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const u32x4 x = wt[lane * 4 + (q ^ (lane & 3))];
+      h.d[4 * q + 0] = x.x;
+      h.d[4 * q + 1] = x.y;
+      h.d[4 * q + 2] = x.z;
+      h.d[4 * q + 3] = x.w;
+    }
+    const uint32_t f = f0 + 64 * g + lane;
+    if constexpr (OPT & 2) { // timing only
+      uint32_t x = 0;
+#pragma unroll
+      for (int q = 0; q < 12; ++q) x ^= h.d[q];
+      if (x == 0x9E3779B9u && f < a.n) a.out[f] = x;
+      continue;
+    }
+    constexpr int IP = kPre + MIS;
+    const uint32_t sip = h.template u32<IP + 12>(), dip = h.template u32<IP + 16>(), ports = h.template u32<IP + 20>();
+    uint32_t id = PN_NO_STREAM;
+    for (int k = (int)a.n_filters - 1; k >= 0; --k) {
+      const MatchMask& q = a.m[k];
+      const uint32_t t = ((sip ^ q.vs) & q.ms) | ((dip ^ q.vd) & q.md) | ((ports ^ q.vp) & q.mp);
+      id = t == 0 ? (uint32_t)k : id;
+    }
+    if (h.template u16<IP - 2>() != 0x0008 || h.template b8<IP + 9>() != 6) id = PN_NO_STREAM;
+    if (f < a.n) a.out[f] = id;
+  }
+}
+
+template <int G, int LAUX, int OPT = 0>
+void launch_match_mask(const MatchArgs& a, uint32_t frame_off, uint32_t waves_per_wg, hipStream_t s) {
+  const uint32_t per_wg = 64 * G * waves_per_wg;
+  const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * waves_per_wg);
+  switch ((frame_off + 14) & 15) {
+    case 0: hipLaunchKernelGGL((match_streams_mask_kernel<0, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((match_streams_mask_kernel<2, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((match_streams_mask_kernel<4, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((match_streams_mask_kernel<6, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((match_streams_mask_kernel<8, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((match_streams_mask_kernel<10, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((match_streams_mask_kernel<12, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((match_streams_mask_kernel<14, G, LAUX, OPT>), grid, block, 0, s, a); break;
+  }
+}
+
 // The production form (A/B: scripts/bench_streams.py, tuning variant pn_match_streams_variant):
 // cooperative loads, non-temporal (glc slc = 2).  Measured 5-7 % faster than the default policy on
 // C2 and C3 (profiles/r03/match_streams_policies.json); the slot lines are read once here.
@@ -178,7 +272,12 @@ inline int match_args(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uin
   a.stride = slot_stride;
   a.ipa_off = (frame_off + 14) & ~15u;
   a.n_filters = n_filters;
-  for (uint32_t k = 0; k < n_filters; ++k) a.f[k] = filters[k]; // host memory: copied into the kernel arguments
+  for (uint32_t k = 0; k < n_filters; ++k) { // host memory: copied into the kernel arguments
+    const pn_stream_filter& q = filters[k];
+    a.f[k] = q;
+    a.m[k] = {q.src_ip, q.dst_ip, (uint32_t)q.src_port | (uint32_t)q.dst_port << 16, q.src_ip ? ~0u : 0u,
+              q.dst_ip ? ~0u : 0u, (q.src_port ? 0xffffu : 0u) | (q.dst_port ? 0xffff0000u : 0u)};
+  }
   return PN_OK;
 }
 

@@ -14,6 +14,7 @@ tail -1 $OUT/gpu_tests.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { cat $OUT/smoke.log; exit 1; }
 timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail $OUT/bench.err; exit 1; }
 head -c 600 $OUT/bench.json; echo
+timeout -k 10 300 python scripts/match_ab.py > $OUT/match_ab.json 2> $OUT/match_ab.err || { echo "match_ab failed"; tail $OUT/match_ab.err; exit 1; }
 PORT=$((20000 + RANDOM % 20000))
 ( while sleep 30; do free -g | awk 'NR==2{print "host mem used GiB", $3}'; done ) > $OUT/n8_mem.log 2>&1 &
 MON=$!
