@@ -35,6 +35,7 @@ struct MatchMask {
   uint32_t vs, vd, vp; // src ip, dst ip, ports
   uint32_t ms, md, mp;
 };
+constexpr uint32_t kMaskBlock = 8; // filters compared per block of kernel-argument loads
 
 struct MatchArgs {
   const uint8_t* frames;
@@ -43,6 +44,7 @@ struct MatchArgs {
   uint32_t stride;
   uint32_t ipa_off; // (frame_off + 14) & ~15
   uint32_t n_filters;
+  uint32_t n_blocks; // ceil(n_filters / kMaskBlock): m[] is padded to whole blocks
   pn_stream_filter f[PN_MAX_STREAM_FILTERS];
   MatchMask m[PN_MAX_STREAM_FILTERS];
 };
@@ -208,10 +210,18 @@ __global__ __launch_bounds__(256) void match_streams_mask_kernel(MatchArgs a) {
     constexpr int IP = kPre + MIS;
     const uint32_t sip = h.template u32<IP + 12>(), dip = h.template u32<IP + 16>(), ports = h.template u32<IP + 20>();
     uint32_t id = PN_NO_STREAM;
-    for (int k = (int)a.n_filters - 1; k >= 0; --k) {
-      const MatchMask& q = a.m[k];
-      const uint32_t t = ((sip ^ q.vs) & q.ms) | ((dip ^ q.vd) & q.md) | ((ports ^ q.vp) & q.mp);
-      id = t == 0 ? (uint32_t)k : id;
+    // blocks of kMaskBlock filters, last block first: each block's scalar loads go out together
+    // (padding entries repeat the last filter; their index clamps to it, so they change nothing)
+    const uint32_t last = a.n_filters - 1;
+    for (int b = (int)a.n_blocks - 1; b >= 0; --b) {
+      MatchMask q[kMaskBlock];
+#pragma unroll
+      for (int j = 0; j < (int)kMaskBlock; ++j) q[j] = a.m[b * kMaskBlock + j];
+#pragma unroll
+      for (int j = kMaskBlock - 1; j >= 0; --j) {
+        const uint32_t t = ((sip ^ q[j].vs) & q[j].ms) | ((dip ^ q[j].vd) & q[j].md) | ((ports ^ q[j].vp) & q[j].mp);
+        id = t == 0 ? min((uint32_t)(b * kMaskBlock + j), last) : id;
+      }
     }
     if (h.template u16<IP - 2>() != 0x0008 || h.template b8<IP + 9>() != 6) id = PN_NO_STREAM;
     if (f < a.n) a.out[f] = id;
@@ -278,6 +288,8 @@ inline int match_args(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uin
     a.m[k] = {q.src_ip, q.dst_ip, (uint32_t)q.src_port | (uint32_t)q.dst_port << 16, q.src_ip ? ~0u : 0u,
               q.dst_ip ? ~0u : 0u, (q.src_port ? 0xffffu : 0u) | (q.dst_port ? 0xffff0000u : 0u)};
   }
+  a.n_blocks = (n_filters + kMaskBlock - 1) / kMaskBlock;
+  for (uint32_t k = n_filters; k < a.n_blocks * kMaskBlock; ++k) a.m[k] = a.m[n_filters - 1]; // the same verdict
   return PN_OK;
 }
 
