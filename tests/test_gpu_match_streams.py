@@ -94,3 +94,37 @@ def test_match_streams_layouts(frame_off, stride, n):
     got = out.cpu().numpy().view(np.uint32)
     assert (got[:n] == pa.PN_NO_STREAM).all() and (got[n:] == 0xAB).all()
     ctx.close()
+
+
+# The round-4 kernel forms (match_streams_mask_kernel, tuning variants 10-14: wave-ordered tile, mask
+# compare in blocks of 8 filters, 1-4 groups of 64 frames per wave, 1 or 4 waves per workgroup) on
+# the same layouts and 0, 1, 7, 8, 9 and 64 filters (padded blocks), against numpy.
+@pytest.mark.parametrize("variant", [10, 11, 12, 13, 14])
+@pytest.mark.parametrize("frame_off,stride,n", [(2, 112, 1), (4, 2048, 700), (14, 128, 257), (16, 65536, 200),
+                                                (26, 2048, 4097)])
+def test_match_streams_mask_variants(variant, frame_off, stride, n):
+    import torch
+
+    from pollnet_amd import tuning as tn
+
+    rng = np.random.default_rng(frame_off * 7 + n + variant)
+    p = pa.rx.GenParams.for_config(5)
+    full = pa.gen_frames(p, n, 2048, frame_off)
+    slots = np.zeros((n, stride), np.uint8)
+    w = min(stride, 2048)
+    slots[:, :w] = full[:, :w]
+    slots[rng.random(n) < 0.2, frame_off + 23] = 17  # some UDP frames
+    slots[rng.random(n) < 0.1, frame_off + 12] = 0x86  # some non-IPv4 ethertypes
+    ctx = pa.RxContext(0)
+    dev = torch.from_numpy(slots.reshape(-1)).cuda()
+    out = torch.full((n + 300,), 0xAB, dtype=torch.int32, device="cuda")
+    for k in (0, 1, 7, 8, 9, 64):
+        flt = np.roll(_filters(rng, slots, frame_off, k), -1) if k else np.zeros(0, pa.STREAM_FILTER_DTYPE)
+        out.fill_(0xAB)
+        tn.match_streams_variant(ctx, dev, stride, frame_off, n, flt, out, variant, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert (got[n:] == 0xAB).all(), ("wrote past n", k)
+        exp = match_streams_np(slots, frame_off, flt)
+        assert np.array_equal(got[:n], exp), (k, int(np.count_nonzero(got[:n] != exp)))
+    ctx.close()
