@@ -626,7 +626,7 @@ def secondary_c4_shard(torch, pa, ctx_dev, steps, R, stream):
             "value": round(8 * wire / (kern * 1e-3) / 1e9, 2), "unit": "Gbit/s",
             "mframes_per_s": round(n / (kern * 1e-3) / 1e6, 2),
             "algorithmic_bytes_per_launch": algo, "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "batches_sha256_gated": f"{sum(1 for _ in sha) if gd is not None else 0}/{R}",
+            "batches_sha256_gated": f"{len(sha) if gd is not None else 0}/{R}",
             "gated_batches_sha256_match_golden": bool(gd is not None and all(sha)),
             "note": "the per-GPU workload of the N>1 line, on one GPU: N x this value is the ideal N-GPU aggregate"}
 

@@ -112,7 +112,7 @@ class TcpServer<RefConnKey> {
           {(uint32_t)tcp[8] << 24 | (uint32_t)tcp[9] << 16 | (uint32_t)tcp[10] << 8 | tcp[11], (uint16_t)(tcp[14] << 8 | tcp[15]), (tcp[13] & 4) != 0});
     }
     // TcpServer.h:88-93: entry, reset, onSyn, sendSyn; then the handshake ACK (TcpServer.h:111-113)
-    uint32_t open(uint8_t* syn_eth, uint8_t* ack_eth_without_ack, uint32_t peer_ip_be, uint16_t peer_port_be) {
+    uint32_t open(uint8_t* syn_eth, uint32_t peer_ip_be, uint16_t peer_port_be) {
       RefEnv& env = refEnv();
       env.link = this;
       env.fill = fill0;
@@ -129,7 +129,6 @@ class TcpServer<RefConnKey> {
       conn->onSyn((IpHeader*)(syn_eth + 14));
       conn->sendSyn();
       const uint32_t srv_isn = ntohl(conn->getSendBuf(0)->tcp_hdr.seq_num);
-      (void)ack_eth_without_ack;
       return srv_isn;
     }
     void established(uint8_t* ack_eth) {
@@ -259,7 +258,7 @@ static bool one_stream(uint64_t seed, Stats& st) {
     }
     build(isn, 0, segtest::SYN, nullptr, 0, o);
   }
-  const uint32_t srv_isn = ref->open(frame.data(), nullptr, htonl(peer_ip), htons(peer_port));
+  const uint32_t srv_isn = ref->open(frame.data(), htonl(peer_ip), htons(peer_port));
   prod.c->open(isn, use_ts, tsval);
   prod.c->ackSent(); // the SYN-ACK carried the ACK (sendSyn -> sendBuf -> updateLastAck)
   const uint32_t ack = srv_isn + 1;
