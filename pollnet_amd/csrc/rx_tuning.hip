@@ -378,7 +378,7 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant) {
-  if (n == 0 || variant < 0 || variant > 19) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  if (n == 0 || variant < 0 || variant > 29) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
   MatchArgs a;
   int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
   if (rc) return rc;
@@ -393,17 +393,28 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
     case 6: launch_match<1, 0, 16>(a, frame_off, s); break; // ids stored write-through (sc1)
     case 7: launch_match<1, 2, 16>(a, frame_off, s); break; // nt loads + sc1 id stores
     case 8: launch_match<1, 0, 2>(a, frame_off, s); break;  // ids stored nt
-    // round 4: wave-ordered tile, mask compare, G groups per wave (match_streams_mask_kernel)
-    case 10: launch_match_mask<1, kMatchLoadAux>(a, frame_off, 4, s); break;     // G 1, 4 waves per workgroup
-    case 11: launch_match_mask<2, kMatchLoadAux>(a, frame_off, 4, s); break;     // G 2
-    case 12: launch_match_mask<4, kMatchLoadAux>(a, frame_off, 4, s); break;     // G 4
-    case 13: launch_match_mask<1, kMatchLoadAux>(a, frame_off, 1, s); break;     // G 1, one wave per workgroup
-    case 14: launch_match_mask<2, kMatchLoadAux>(a, frame_off, 1, s); break;     // G 2, one wave per workgroup
-    case 15: launch_match_mask<1, kMatchLoadAux, 2>(a, frame_off, 4, s); break;  // timing only: 10's loads + tile
-    case 16: launch_match_mask<2, kMatchLoadAux, 2>(a, frame_off, 4, s); break;  // timing only: 11's loads + tile
-    case 17: launch_match_mask<4, kMatchLoadAux, 2>(a, frame_off, 4, s); break;  // timing only: 12's loads + tile
-    case 18: launch_match_mask<1, kMatchLoadAux, 2>(a, frame_off, 1, s); break;  // timing only: 13's
-    case 19: launch_match_mask<2, kMatchLoadAux, 2>(a, frame_off, 1, s); break;  // timing only: 14's
+    // round 4: wave-ordered tile, mask compare, G groups per wave, W waves per workgroup
+    // (match_streams_mask_kernel<.., G, .., OPT, W>); the odd-numbered-after-19 / 15-19 ids: loads + tile only
+    case 10: launch_match_mask<1, kMatchLoadAux, 0, 4>(a, frame_off, s); break;
+    case 11: launch_match_mask<2, kMatchLoadAux, 0, 4>(a, frame_off, s); break;
+    case 12: launch_match_mask<4, kMatchLoadAux, 0, 4>(a, frame_off, s); break;
+    case 13: launch_match_mask<1, kMatchLoadAux, 0, 1>(a, frame_off, s); break;
+    case 14: launch_match_mask<2, kMatchLoadAux, 0, 1>(a, frame_off, s); break;
+    case 15: launch_match_mask<1, kMatchLoadAux, 2, 4>(a, frame_off, s); break;  // timing only: 10's loads + tile
+    case 16: launch_match_mask<2, kMatchLoadAux, 2, 4>(a, frame_off, s); break;  // 11's
+    case 17: launch_match_mask<4, kMatchLoadAux, 2, 4>(a, frame_off, s); break;  // 12's
+    case 18: launch_match_mask<1, kMatchLoadAux, 2, 1>(a, frame_off, s); break;  // 13's
+    case 19: launch_match_mask<2, kMatchLoadAux, 2, 1>(a, frame_off, s); break;  // 14's
+    case 20: launch_match_mask<4, kMatchLoadAux, 0, 1>(a, frame_off, s); break;
+    case 21: launch_match_mask<4, kMatchLoadAux, 2, 1>(a, frame_off, s); break;  // 20's
+    case 22: launch_match_mask<4, kMatchLoadAux, 0, 2>(a, frame_off, s); break;
+    case 23: launch_match_mask<4, kMatchLoadAux, 2, 2>(a, frame_off, s); break;  // 22's
+    case 24: launch_match_mask<8, kMatchLoadAux, 0, 4>(a, frame_off, s); break;
+    case 25: launch_match_mask<8, kMatchLoadAux, 2, 4>(a, frame_off, s); break;  // 24's
+    case 26: launch_match_mask<8, kMatchLoadAux, 0, 1>(a, frame_off, s); break;
+    case 27: launch_match_mask<8, kMatchLoadAux, 2, 1>(a, frame_off, s); break;  // 26's
+    case 28: launch_match_mask<2, kMatchLoadAux, 0, 2>(a, frame_off, s); break;
+    case 29: launch_match_mask<2, kMatchLoadAux, 2, 2>(a, frame_off, s); break;  // 28's
     default: launch_match<0>(a, frame_off, s);
   }
   hipError_t e = hipGetLastError();

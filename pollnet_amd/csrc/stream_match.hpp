@@ -157,14 +157,15 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 //   - G groups of 64 frames per wave, all G x 4 loads in flight before the first group is compared;
 //   - the filters as value / care-mask words (MatchMask): per filter 3 xor, 1 and, 2 and-or, 1 compare and
 //     1 select per frame, no branch, last to first so the first passing filter wins.
+// WPW waves per workgroup, each with its own 4-KiB tile.
 // OPT & 2 (tuning): the loads and the tile round trip alone, no compare or store (its ceiling).
-template <int MIS, int G, int LAUX, int OPT = 0>
-__global__ __launch_bounds__(256) void match_streams_mask_kernel(MatchArgs a) {
+template <int MIS, int G, int LAUX, int OPT = 0, int WPW = 4>
+__global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs a) {
   constexpr uint32_t kWaveFrames = 64 * G;
-  __shared__ u32x4 tile[4 * 256];
+  __shared__ u32x4 tile[WPW * 256];
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t f0 = __builtin_amdgcn_readfirstlane((blockIdx.x * (blockDim.x >> 6) + w) * kWaveFrames);
+  const uint32_t w = WPW == 1 ? 0u : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t f0 = __builtin_amdgcn_readfirstlane((blockIdx.x * WPW + w) * kWaveFrames);
   if (f0 >= a.n) return; // wave-uniform, and no workgroup barrier below
   const uint32_t n_here = min(kWaveFrames, a.n - f0);
   const __amdgpu_buffer_rsrc_t rs =
@@ -228,19 +229,19 @@ __global__ __launch_bounds__(256) void match_streams_mask_kernel(MatchArgs a) {
   }
 }
 
-template <int G, int LAUX, int OPT = 0>
-void launch_match_mask(const MatchArgs& a, uint32_t frame_off, uint32_t waves_per_wg, hipStream_t s) {
-  const uint32_t per_wg = 64 * G * waves_per_wg;
-  const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * waves_per_wg);
+template <int G, int LAUX, int OPT = 0, int WPW = 4>
+void launch_match_mask(const MatchArgs& a, uint32_t frame_off, hipStream_t s) {
+  constexpr uint32_t per_wg = 64 * G * WPW;
+  const dim3 grid((a.n + per_wg - 1) / per_wg), block(64 * WPW);
   switch ((frame_off + 14) & 15) {
-    case 0: hipLaunchKernelGGL((match_streams_mask_kernel<0, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL((match_streams_mask_kernel<2, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((match_streams_mask_kernel<4, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    case 6: hipLaunchKernelGGL((match_streams_mask_kernel<6, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((match_streams_mask_kernel<8, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    case 10: hipLaunchKernelGGL((match_streams_mask_kernel<10, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    case 12: hipLaunchKernelGGL((match_streams_mask_kernel<12, G, LAUX, OPT>), grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL((match_streams_mask_kernel<14, G, LAUX, OPT>), grid, block, 0, s, a); break;
+    case 0: hipLaunchKernelGGL((match_streams_mask_kernel<0, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((match_streams_mask_kernel<2, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((match_streams_mask_kernel<4, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    case 6: hipLaunchKernelGGL((match_streams_mask_kernel<6, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((match_streams_mask_kernel<8, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    case 10: hipLaunchKernelGGL((match_streams_mask_kernel<10, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    case 12: hipLaunchKernelGGL((match_streams_mask_kernel<12, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
+    default: hipLaunchKernelGGL((match_streams_mask_kernel<14, G, LAUX, OPT, WPW>), grid, block, 0, s, a); break;
   }
 }
 

@@ -15,13 +15,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-TIMING_ONLY = {5, 15, 16, 17, 18, 19}
+TIMING_ONLY = {5, 15, 16, 17, 18, 19, 21, 23, 25, 27, 29}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=9)
-    ap.add_argument("--variants", default="1,5,10,11,12,13,14,15,16,17,18,19")
+    ap.add_argument("--variants", default="1,5,12,13,17,18,20,21,22,23,24,25,26,27,28,29")
     ap.add_argument("--configs", default="2,3")
     args = ap.parse_args()
     import numpy as np
