@@ -470,12 +470,12 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
         return ev[0].elapsed_time(ev[1]) / 20
 
     ts, tg = [], []
-    for _ in range(5):  # the product and its loads alone (tuning variant 5), alternately
+    for _ in range(5):  # the product and its loads + tile round trip alone (tuning variant 18), alternately
         ts.append(timed(lambda d: ctx.match_streams(d, STRIDE, FRAME_OFF, n, flt, ids, stream)))
-        tg.append(timed(lambda d: tn.match_streams_variant(ctx, d, STRIDE, FRAME_OFF, n, flt, sink, 5, stream)))
+        tg.append(timed(lambda d: tn.match_streams_variant(ctx, d, STRIDE, FRAME_OFF, n, flt, sink, 18, stream)))
     ms, mg = statistics.median(ts), statistics.median(tg)
     pmc = load_pmc(f"match_streams_c2_n{n}")
-    return {"kernel": "match_streams_kernel", "frames": n, "resident_batches": R, "filters": 8, "kernel_ms": round(ms, 5),
+    return {"kernel": "match_streams_mask_kernel", "frames": n, "resident_batches": R, "filters": 8, "kernel_ms": round(ms, 5),
             "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
             "algorithmic_bytes_per_launch": n * (64 + 4),
             "achieved_gbs": round(n * (64 + 4) / (ms * 1e-3) / 1e9, 1),
@@ -485,7 +485,7 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
             "gather_loads_only_ms": round(mg, 5), "kernel_vs_gather_ceiling": round(mg / ms, 4),
             "first_65536_ids_vs_numpy": ok,
             "note": "one 128-B line per 2-KiB slot (PMC: every request 128 B); the ceiling is the same kernel's loads "
-                    "and LDS round trip alone (DESIGN §11)"}
+                    "and LDS tile round trip alone, no compare or store (tuning variant 18, DESIGN §11)"}
 
 
 def server_poll():

@@ -384,7 +384,7 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
-    case 1: launch_match<kMatchProd, kMatchLoadAux>(a, frame_off, s); break; // production
+    case 1: launch_match<kMatchProd, kMatchLoadAux>(a, frame_off, s); break; // round-3 production
     case 9: launch_match<1>(a, frame_off, s); break;     // cooperative, default-policy loads
     case 2: launch_match<1, 2>(a, frame_off, s); break;  // cooperative, nt loads
     case 3: launch_match<1, 1>(a, frame_off, s); break;  // cooperative, sc0 loads

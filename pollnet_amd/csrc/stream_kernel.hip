@@ -12,7 +12,7 @@ extern "C" int pn_match_streams(pn_ctx* ctx, const void* frames, uint32_t slot_s
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  launch_match<kMatchProd, kMatchLoadAux>(a, frame_off, s);
+  launch_match_mask<kMatchG, kMatchLoadAux, 0, kMatchWPW>(a, frame_off, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "match_streams launch");
   pn_internal::note_stream(ctx, s);

@@ -229,6 +229,14 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
   }
 }
 
+// Production (round 4): one group of 64 frames per wave, one wave per workgroup (a 4-KiB tile each).
+// Interleaved A/B, 9 rounds, 1 Mi resident slots x 4 batches, 8 filters (profiles/r04/match_streams/):
+// 0.0269 -> 0.0219 ms on C2 and 0.0275 -> 0.0220 on C3 against the round-3 kernel (tuning variant 1),
+// at 0.94 of its own loads + tile round trip (variant 18); more groups per wave (2, 4, 8) or more
+// waves per workgroup (2, 4) measured 2-10 % slower.
+constexpr int kMatchG = 1;
+constexpr int kMatchWPW = 1;
+
 template <int G, int LAUX, int OPT = 0, int WPW = 4>
 void launch_match_mask(const MatchArgs& a, uint32_t frame_off, hipStream_t s) {
   constexpr uint32_t per_wg = 64 * G * WPW;
@@ -245,7 +253,7 @@ void launch_match_mask(const MatchArgs& a, uint32_t frame_off, hipStream_t s) {
   }
 }
 
-// The production form (A/B: scripts/bench_streams.py, tuning variant pn_match_streams_variant):
+// The round-3 production form, now tuning variant 1 (A/B: scripts/bench_streams.py, match_ab.py):
 // cooperative loads, non-temporal (glc slc = 2).  Measured 5-7 % faster than the default policy on
 // C2 and C3 (profiles/r03/match_streams_policies.json); the slot lines are read once here.
 constexpr int kMatchProd = 1;
