@@ -210,15 +210,16 @@ struct BurstLink {
     return m;
   }
 };
-static std::vector<std::vector<uint8_t>> burst() {
+static std::vector<std::vector<uint8_t>> burst(uint32_t n = 3, bool corrupt = false) {
   std::vector<std::vector<uint8_t>> f;
-  for (uint32_t k = 0; k < 3; k++) {
+  for (uint32_t k = 0; k < n; k++) {
     segtest::Seg s;
     s.src_ip = 0x0a050000 + k;
     s.src_port = (uint16_t)(50000 + k);
     s.seq = 1000 * k;
     s.ack = 77 + k;
     s.flags = segtest::ACK;
+    s.corrupt = corrupt;
     std::vector<uint8_t> b(128);
     b.resize(segtest::build(b.data(), s));
     f.push_back(b);
@@ -264,10 +265,88 @@ static int nic_queue_divergence() {
   return fail;
 }
 
+// The reference server as the harness runs it, on one burst of frames; returns its frames after each poll.
+static std::vector<size_t> ref_polls(std::vector<std::vector<uint8_t>> frames, int polls, BurstLink& link) {
+  using Srv = efvitcp::EfviTcpServer<RefConf>;
+  link.in = std::move(frames);
+  efvitcp::RefEnv& env = efvitcp::refEnv();
+  env.link = &link;
+  env.fill = [](void* l, uint8_t* s, uint32_t st, uint32_t off, uint32_t cap) {
+    return static_cast<BurstLink*>(l)->fill(s, st, off, cap);
+  };
+  env.send = [](void* l, const uint8_t* eth, uint32_t len) { static_cast<BurstLink*>(l)->send(eth, len); };
+  env.init_ns = kT0;
+  env.local_ip = link.localIp();
+  std::memcpy(env.local_mac, link.localMac(), 6);
+  env.tx_complete_next_poll = false;
+  std::unique_ptr<Srv> ref(new Srv());
+  ref->init("burst", "10.0.0.1", 1234);
+  std::string log;
+  PeerHandler<Srv::Conn> h{&log};
+  std::vector<size_t> out;
+  for (int k = 1; k <= polls; k++) {
+    ref->poll(h, kT0 + ((int64_t)k << 20));
+    out.push_back(link.out.size());
+  }
+  return out;
+}
+template <class Conf>
+static std::vector<size_t> prod_polls(std::vector<std::vector<uint8_t>> frames, int polls, bool drop_bad,
+                                      std::vector<std::vector<uint8_t>>* sent) {
+  using P = GpuTcpServer<Conf, BurstLink, OracleBackend>;
+  auto p = std::make_unique<P>();
+  p->initWithLink("10.0.0.1", 1234, kT0);
+  p->setDropBadChecksum(drop_bad);
+  p->link().in = std::move(frames);
+  std::string log;
+  PeerHandler<typename P::Conn> h{&log};
+  std::vector<size_t> out;
+  for (int k = 1; k <= polls; k++) {
+    p->poll(h, kT0 + ((int64_t)k << 20));
+    out.push_back(p->link().out.size());
+  }
+  *sent = p->link().out;
+  return out;
+}
+
+// Frames per poll: the reference takes at most 64 RX events per pollNet (Core.h:496-498), the engine up to
+// Conf::RxBatch (default 512).  100 unknown-flow segments in one burst: the reference answers 64 in the
+// first poll and 36 in the second, the engine all 100 in the first (and with RxBatch = 64, as the reference);
+// the 100 RSTs are the same frames in the same order.
+static int rx_batch_divergence() {
+  BurstLink link;
+  const auto ref = ref_polls(burst(100), 2, link);
+  std::vector<std::vector<uint8_t>> a, b;
+  const auto def = prod_polls<RefConf>(burst(100), 2, true, &a);
+  const auto b64 = prod_polls<ProdConf>(burst(100), 2, true, &b);
+  const bool ok = ref == std::vector<size_t>{64, 100} && def == std::vector<size_t>{100, 100} && b64 == ref &&
+                  a == link.out && b == link.out;
+  std::printf("frames per poll: reference %zu then %zu RSTs, product (RxBatch 512) %zu then %zu, product (RxBatch 64) "
+              "%zu then %zu; the same 100 frames -> %s\n",
+              ref[0], ref[1], def[0], def[1], b64[0], b64[1], ok ? "as documented" : "UNEXPECTED");
+  return ok ? 0 : 1;
+}
+
+// Bad checksums: the reference relies on the NIC to discard them (an ef_vi RX_DISCARD event); run without a
+// NIC it answers a corrupted unknown-flow segment with an RST.  The engine discards it after pn_classify
+// (setDropBadChecksum, default on); with the discard off it sends the reference's RST, byte for byte.
+static int bad_checksum_divergence() {
+  BurstLink link;
+  const auto ref = ref_polls(burst(3, true), 1, link);
+  std::vector<std::vector<uint8_t>> dropped, kept;
+  const auto on = prod_polls<ProdConf>(burst(3, true), 1, true, &dropped);
+  const auto off = prod_polls<ProdConf>(burst(3, true), 1, false, &kept);
+  const bool ok = ref[0] == 3 && on[0] == 0 && off[0] == 3 && kept == link.out;
+  std::printf("bad checksums: reference without a NIC %zu RSTs, product %zu (discard on) / %zu (discard off, the "
+              "reference's frames) -> %s\n",
+              ref[0], on[0], off[0], ok ? "as documented" : "UNEXPECTED");
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
   const uint32_t runs = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1;
-  int fail = nic_queue_divergence();
+  int fail = nic_queue_divergence() + rx_batch_divergence() + bad_checksum_divergence();
   for (g_seed = 0; g_seed < runs; g_seed++) {
     for (int chaos = 0; chaos < 2; chaos++) {
       std::printf("== %s population %u ==\n", chaos ? "chaos" : "peer", g_seed);

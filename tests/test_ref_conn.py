@@ -46,6 +46,8 @@ def test_server_twin_equals_reference_server():
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("vs reference:") == 8, p.stdout
     assert "DIFFERENT" not in p.stdout and p.stdout.rstrip().endswith("PASS"), p.stdout
+    # the intended differences, each shown: NIC-queue buffers (2 cases), frames per poll, bad checksums
+    assert p.stdout.count("-> as documented") == 4, p.stdout
 
 
 @pytest.mark.gpu
