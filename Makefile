@@ -42,6 +42,7 @@ CLISRVTEST = tests/cpp/test_tcp_client_server
 TXHOSTTEST = tests/cpp/test_tx_host
 REFSERVERTEST = tests/cpp/test_ref_server
 REFCONNTEST = tests/cpp/test_ref_conn
+REFCLIENTTEST = tests/cpp/test_ref_client
 
 # Host programs that include HIP headers: compiled by hipcc with the device pass pinned to gfx950
 # (without --offload-arch hipcc would add a default-arch device pass for nothing)
@@ -57,7 +58,7 @@ CONN_INCS = $(addprefix oracle/_ref/,conn_tcpconn.inc conn_tcpserver.inc conn_ef
   conn_core_tbl.inc conn_core_timer.inc conn_core_members.inc core_defs.inc conn_tcpclient_head.inc \
   conn_tcpclient_tail.inc conn_efvitcpclient.inc conn_core_autoport.inc)
 HAVE_REF_TEXT = $(or $(wildcard $(REFDIR)/example/tcpserver.cc),$(and $(wildcard oracle/_ref/tcpserver_handler.inc),$(wildcard oracle/_ref/tcpclient_handler.inc)))
-REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST) $(REFSERVERTEST) $(REFCONNTEST))
+REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST) $(REFSERVERTEST) $(REFCONNTEST) $(REFCLIENTTEST))
 
 all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST) $(TXHOSTTEST)
 
@@ -76,6 +77,13 @@ $(REF_INCS) $(CONN_INCS):
 # GpuTcpServer (twin and GPU) vs the reference's own EfviTcpServer / TcpServer / TcpConn (oracle/ref_server.hpp)
 $(REFSERVERTEST): tests/cpp/test_ref_server.cpp tests/cpp/peer_population.hpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp \
   oracle/ref_server.hpp include/pollnet_amd/tcp_server.hpp include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp \
+  include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) $(CONN_INCS)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -Wno-unused-result -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
+
+# GpuTcpClient (twin and GPU) vs the reference's own EfviTcpClient / TcpClient against a scripted server
+$(REFCLIENTTEST): tests/cpp/test_ref_client.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp oracle/ref_server.hpp \
+  include/pollnet_amd/tcp_client.hpp include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp \
   include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) $(CONN_INCS)
 	$(HOSTHIP) -O2 -std=c++17 -Wall -Wno-unused-result -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../../oracle'
@@ -182,6 +190,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST) $(REFSERVERTEST) $(REFCONNTEST)
+	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST) $(REFSERVERTEST) $(REFCONNTEST) $(REFCLIENTTEST)
 
 .PHONY: all ref clean

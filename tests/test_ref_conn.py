@@ -56,3 +56,22 @@ def test_gpu_server_equals_reference_server():
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("GpuTcpServer (GPU backend) vs reference") == 6, p.stdout
     assert "DIFFERENT" not in p.stdout and p.stdout.rstrip().endswith("PASS"), p.stdout
+
+
+def test_client_twin_equals_reference_client():
+    """GpuTcpClient vs the reference EfviTcpClient (tests/cpp/test_ref_client.cpp) against a scripted,
+    adversarial server: SYN answered by a SYN-ACK, a wrong-ack SYN-ACK, RST|ACK, a bare RST, a bare SYN or
+    silence; reconnects; adversarial data streams and FINs.  Every client frame and the handler log identical
+    over 24 scripts (sequential backend)."""
+    p = subprocess.run([_bin("test_ref_client"), "twin", "24"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.count("twin vs reference: ") == 24 and "DIFFERENT" not in p.stdout, p.stdout
+    assert p.stdout.rstrip().endswith("PASS"), p.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_client_equals_reference_client():
+    p = subprocess.run([_bin("test_ref_client"), "gpu", "8"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.count("GpuTcpClient (GPU) vs reference") == 8 and "DIFFERENT" not in p.stdout, p.stdout
+    assert p.stdout.rstrip().endswith("PASS"), p.stdout
