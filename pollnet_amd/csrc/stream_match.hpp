@@ -159,6 +159,8 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 //     1 select per frame, no branch, last to first so the first passing filter wins.
 // WPW waves per workgroup, each with its own 4-KiB tile.
 // OPT & 2 (tuning): the loads and the tile round trip alone, no compare or store (its ceiling).
+// OPT & 4 (tuning): raise the wave's priority once its loads are in (s_setprio 2), so the compare and store
+// finish ahead of waves still issuing loads.  OPT & 8 (tuning): only the needed chunks written to the tile.
 template <int MIS, int G, int LAUX, int OPT = 0, int WPW = 4>
 __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs a) {
   constexpr uint32_t kWaveFrames = 64 * G;
@@ -189,7 +191,10 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const uint32_t r = 16 * i + (lane >> 2);
-      wt[r * 4 + (c ^ (r & 3))] = v[g][i];
+      if (!(OPT & 8) || need) wt[r * 4 + (c ^ (r & 3))] = v[g][i];
+    }
+    if constexpr ((OPT & 4) != 0) {
+      if (g == 0) __builtin_amdgcn_s_setprio(2);
     }
     Win<16> h;
 #pragma unroll
