@@ -161,6 +161,7 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 // OPT & 2 (tuning): the loads and the tile round trip alone, no compare or store (its ceiling).
 // OPT & 4 (tuning): raise the wave's priority once its loads are in (s_setprio 2), so the compare and store
 // finish ahead of waves still issuing loads.  OPT & 8 (tuning): only the needed chunks written to the tile.
+// OPT & 16: the filter test as (field & mask) == value per word instead of xor/and/or.
 template <int MIS, int G, int LAUX, int OPT = 0, int WPW = 4>
 __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs a) {
   constexpr uint32_t kWaveFrames = 64 * G;
@@ -225,8 +226,13 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
       for (int j = 0; j < (int)kMaskBlock; ++j) q[j] = a.m[b * kMaskBlock + j];
 #pragma unroll
       for (int j = kMaskBlock - 1; j >= 0; --j) {
-        const uint32_t t = ((sip ^ q[j].vs) & q[j].ms) | ((dip ^ q[j].vd) & q[j].md) | ((ports ^ q[j].vp) & q[j].mp);
-        id = t == 0 ? min((uint32_t)(b * kMaskBlock + j), last) : id;
+        bool pass;
+        if constexpr ((OPT & 16) != 0) { // and-compare form: 3 ands, 3 compares (a wildcard's value is 0 = its mask)
+          pass = (sip & q[j].ms) == q[j].vs && (dip & q[j].md) == q[j].vd && (ports & q[j].mp) == q[j].vp;
+        } else {
+          pass = (((sip ^ q[j].vs) & q[j].ms) | ((dip ^ q[j].vd) & q[j].md) | ((ports ^ q[j].vp) & q[j].mp)) == 0;
+        }
+        id = pass ? min((uint32_t)(b * kMaskBlock + j), last) : id;
       }
     }
     if (h.template u16<IP - 2>() != 0x0008 || h.template b8<IP + 9>() != 6) id = PN_NO_STREAM;
