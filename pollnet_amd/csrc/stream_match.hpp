@@ -218,13 +218,11 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
     constexpr int IP = kPre + MIS;
     const uint32_t sip = h.template u32<IP + 12>(), dip = h.template u32<IP + 16>(), ports = h.template u32<IP + 20>();
     uint32_t id = PN_NO_STREAM;
-    if constexpr ((OPT & 32) != 0) { // timing only: no compare (the ids are the frames' own loads)
-      id = sip ^ dip ^ ports;
-    } else
     // blocks of kMaskBlock filters, last block first: each block's scalar loads go out together
     // (padding entries repeat the last filter; their index clamps to it, so they change nothing)
     const uint32_t last = a.n_filters - 1;
-    for (int b = (int)a.n_blocks - 1; b >= 0; --b) {
+    if constexpr ((OPT & 32) != 0) id = sip ^ dip ^ ports; // timing only: no compare
+    for (int b = (OPT & 32) ? -1 : (int)a.n_blocks - 1; b >= 0; --b) {
       MatchMask q[kMaskBlock];
 #pragma unroll
       for (int j = 0; j < (int)kMaskBlock; ++j) q[j] = a.m[b * kMaskBlock + j];
