@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 // OPT & 4 (tuning): raise the wave's priority once its loads are in (s_setprio 2), so the compare and store
 // finish ahead of waves still issuing loads.  OPT & 8 (tuning): only the needed chunks written to the tile.
 // OPT & 16: the filter test as (field & mask) == value per word instead of xor/and/or.
-// OPT & 32 / 64 (tuning, timing only): no filter compare / no id store.
+// OPT & 32 / 64 (tuning, timing only): no filter compare / no id store.  OPT & 128 (tuning): nt id stores.
 template <int MIS, int G, int LAUX, int OPT = 0, int WPW = 4>
 __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs a) {
   constexpr uint32_t kWaveFrames = 64 * G;
@@ -242,7 +242,11 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
       if (id == 0x9E3779B9u && f < a.n) a.out[f] = id;
       continue;
     }
-    if (f < a.n) a.out[f] = id;
+    if constexpr ((OPT & 128) != 0) { // tuning: non-temporal id store
+      if (f < a.n) __builtin_nontemporal_store(id, a.out + f);
+    } else {
+      if (f < a.n) a.out[f] = id;
+    }
   }
 }
 
