@@ -469,11 +469,13 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
         torch.cuda.synchronize()
         return ev[0].elapsed_time(ev[1]) / 20
 
-    ts, tg = [], []
-    for _ in range(5):  # the product and its loads + tile round trip alone (tuning variant 18), alternately
+    ts, tg, tw = [], [], []
+    for _ in range(5):  # the product, its loads + tile round trip alone (tuning variant 18), and the same with the
+        # required id stores but no filter compare (variant 34), alternately
         ts.append(timed(lambda d: ctx.match_streams(d, STRIDE, FRAME_OFF, n, flt, ids, stream)))
         tg.append(timed(lambda d: tn.match_streams_variant(ctx, d, STRIDE, FRAME_OFF, n, flt, sink, 18, stream)))
-    ms, mg = statistics.median(ts), statistics.median(tg)
+        tw.append(timed(lambda d: tn.match_streams_variant(ctx, d, STRIDE, FRAME_OFF, n, flt, sink, 34, stream)))
+    ms, mg, mw = statistics.median(ts), statistics.median(tg), statistics.median(tw)
     pmc = load_pmc(f"match_streams_c2_n{n}")
     return {"kernel": "match_streams_mask_kernel", "frames": n, "resident_batches": R, "filters": 8, "kernel_ms": round(ms, 5),
             "mframes_per_s": round(n / (ms * 1e-3) / 1e6, 1),
@@ -483,9 +485,11 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
             "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
             "traffic_gbs": None if pmc is None else round(pmc["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1),
             "gather_loads_only_ms": round(mg, 5), "kernel_vs_gather_ceiling": round(mg / ms, 4),
+            "loads_and_id_stores_ms": round(mw, 5), "kernel_vs_loads_and_stores_ceiling": round(mw / ms, 4),
             "first_65536_ids_vs_numpy": ok,
-            "note": "one 128-B line per 2-KiB slot (PMC: every request 128 B); the ceiling is the same kernel's loads "
-                    "and LDS tile round trip alone, no compare or store (tuning variant 18, DESIGN §11)"}
+            "note": "one 128-B line per 2-KiB slot (PMC: every request 128 B); ceilings: the same kernel's loads and LDS "
+                    "tile round trip alone, no compare or store (tuning variant 18), and the same with the 4-B id "
+                    "stores the output needs but no filter compare (variant 34) (DESIGN §11)"}
 
 
 def server_poll():
