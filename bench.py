@@ -486,6 +486,9 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
             "traffic_gbs": None if pmc is None else round(pmc["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1),
             "gather_loads_only_ms": round(mg, 5), "kernel_vs_gather_ceiling": round(mg / ms, 4),
             "loads_and_id_stores_ms": round(mw, 5), "kernel_vs_loads_and_stores_ceiling": round(mw / ms, 4),
+            # HBM rate against the gather's: the kernel moves one 128-B line per frame AND its 4-B id, the
+            # gather only the line (the ids are 3 % of the traffic)
+            "kernel_vs_gather_hbm_rate": round(mg / ms * (128 + 4) / 128, 4),
             "first_65536_ids_vs_numpy": ok,
             "note": "one 128-B line per 2-KiB slot (PMC: every request 128 B); ceilings: the same kernel's loads and LDS "
                     "tile round trip alone, no compare or store (tuning variant 18), and the same with the 4-B id "

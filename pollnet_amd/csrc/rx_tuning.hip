@@ -378,7 +378,7 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant) {
-  if (n == 0 || variant < 0 || variant > 36) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  if (n == 0 || variant < 0 || variant > 38) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
   MatchArgs a;
   int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
   if (rc) return rc;
@@ -422,6 +422,8 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
     case 34: launch_match_mask<1, kMatchLoadAux, 32, 1>(a, frame_off, s); break; // timing only: no compare
     case 35: launch_match_mask<1, kMatchLoadAux, 64, 1>(a, frame_off, s); break; // timing only: no id store
     case 36: launch_match_mask<1, kMatchLoadAux, 128, 1>(a, frame_off, s); break; // production, nt id stores
+    case 37: launch_match_mask<1, kMatchLoadAux, 256, 1>(a, frame_off, s); break; // production, masks loaded first
+    case 38: launch_match_mask<1, kMatchLoadAux, 512, 1>(a, frame_off, s); break; // timing only: stores into 4 KiB
     default: launch_match<0>(a, frame_off, s);
   }
   hipError_t e = hipGetLastError();

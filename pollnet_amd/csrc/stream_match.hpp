@@ -163,6 +163,9 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 // finish ahead of waves still issuing loads.  OPT & 8 (tuning): only the needed chunks written to the tile.
 // OPT & 16: the filter test as (field & mask) == value per word instead of xor/and/or.
 // OPT & 32 / 64 (tuning, timing only): no filter compare / no id store.  OPT & 128 (tuning): nt id stores.
+// OPT & 256: the last filter block's masks loaded right after the frame loads, not at the compare (below).
+// OPT & 512 (timing only): the id stores all land in the first 4 KiB of the output (store issue without the
+// write volume).
 template <int MIS, int G, int LAUX, int OPT = 0, int WPW = 4>
 __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs a) {
   constexpr uint32_t kWaveFrames = 64 * G;
@@ -178,6 +181,9 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
   const uint32_t c = lane & 3;
   const bool need = (c == 0 && chunk_needed<MIS>(0)) || (c == 1 && chunk_needed<MIS>(1)) ||
                     (c == 2 && chunk_needed<MIS>(2)) || (c == 3 && chunk_needed<MIS>(3));
+  const int b_last = (int)a.n_blocks - 1;
+  const uint32_t last = a.n_filters - 1;
+  MatchMask q0[kMaskBlock];
   // instruction (g, i): lane l loads chunk l & 3 of frame 64 g + 16 i + (l >> 2); rows past n_here
   // read zeros (the descriptor's range), unneeded chunks fetch nothing
   u32x4 v[G][4];
@@ -188,6 +194,20 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
       const uint32_t r = 64 * g + 16 * i + (lane >> 2);
       v[g][i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (r * a.stride + 16 * c) | (need ? 0u : kNoFetch), 0, LAUX);
     }
+  // OPT & 256: the last filter block's kernel-argument loads go out right after the frame loads and are in
+  // registers while the frames are still on their way (a.m always holds kMaskBlock entries, so block 0 is
+  // read even without filters; it is used only when n_blocks > 0).  The empty asm statements use the values
+  // here, so the compiler cannot sink the loads to the compare, after the frames' wait.
+  if constexpr ((OPT & 256) != 0) {
+    __builtin_amdgcn_sched_barrier(0);
+    const int b0 = b_last > 0 ? b_last : 0;
+    asm volatile("" : : "s"(last));
+#pragma unroll
+    for (int j = 0; j < (int)kMaskBlock; ++j) {
+      q0[j] = a.m[b0 * kMaskBlock + j];
+      asm volatile("" : : "s"(q0[j].vs), "s"(q0[j].vd), "s"(q0[j].vp), "s"(q0[j].ms), "s"(q0[j].md), "s"(q0[j].mp));
+    }
+  }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
 #pragma unroll
@@ -220,12 +240,11 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
     uint32_t id = PN_NO_STREAM;
     // blocks of kMaskBlock filters, last block first: each block's scalar loads go out together
     // (padding entries repeat the last filter; their index clamps to it, so they change nothing)
-    const uint32_t last = a.n_filters - 1;
     if constexpr ((OPT & 32) != 0) id = sip ^ dip ^ ports; // timing only: no compare
-    for (int b = (OPT & 32) ? -1 : (int)a.n_blocks - 1; b >= 0; --b) {
+    for (int b = (OPT & 32) ? -1 : b_last; b >= 0; --b) {
       MatchMask q[kMaskBlock];
 #pragma unroll
-      for (int j = 0; j < (int)kMaskBlock; ++j) q[j] = a.m[b * kMaskBlock + j];
+      for (int j = 0; j < (int)kMaskBlock; ++j) q[j] = ((OPT & 256) != 0 && b == b_last) ? q0[j] : a.m[b * kMaskBlock + j];
 #pragma unroll
       for (int j = kMaskBlock - 1; j >= 0; --j) {
         bool pass;
@@ -240,6 +259,10 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
     if (h.template u16<IP - 2>() != 0x0008 || h.template b8<IP + 9>() != 6) id = PN_NO_STREAM;
     if constexpr ((OPT & 64) != 0) { // timing only: (almost) no id store
       if (id == 0x9E3779B9u && f < a.n) a.out[f] = id;
+      continue;
+    }
+    if constexpr ((OPT & 512) != 0) { // timing only: every store, into 4 KiB of lines (no HBM write volume)
+      if (f < a.n) a.out[(blockIdx.x & 15) * 64 + lane] = id;
       continue;
     }
     if constexpr ((OPT & 128) != 0) { // tuning: non-temporal id store
