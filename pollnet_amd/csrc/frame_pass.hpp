@@ -77,6 +77,9 @@ enum : int { kPipeStream = 1 << 21 };
 // ahead, 65536 probe pipelined into phase 2, 262144 home entries through the scalar cache (code: commit 229bb94);
 // 524288 a run-length hint in the device table's pad word sending long runs straight to the group walk (c3575ae).
 // The production RX configuration.
+// timing only: every wave's records into the first 16 KiB of the output (the stores issued, almost no
+// write-back volume)
+enum : int { kAblSmallStore = 1 << 22 };
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate | kPipeStream;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at

@@ -321,6 +321,10 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
     *lds_rec = rec;
   } else if constexpr (ABL & kAblNoStore) {
     if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
+  } else if constexpr (ABL & kAblSmallStore) { // timing only: 16 blocks of 64 records, rewritten by every wave
+    const uint32_t blk = __builtin_amdgcn_readfirstlane((f & ~63u) & 0x3C0u);
+    const __amdgpu_buffer_rsrc_t rs = frame_rsrc((const uint8_t*)(a.out + blk), 64 * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(rec, rs, (f & 63u) * 16, 0, SAUX);
   } else if constexpr (ABL & kAblStore8) { // timing only: half the record bytes
     reinterpret_cast<uint2*>(a.out)[f] = uint2{rec.x ^ rec.y, rec.z ^ rec.w};
   } else if constexpr (ABL & kAblGlobalStore) { // the record through a plain global store (SAUX ignored)
@@ -533,6 +537,12 @@ constexpr int kProdGopt = (2 << 4) | kXcdOrder;
 // Bit 12: completion word (pn_classify_notify; signal_done in frame_pass.hpp).  Above the LDS-padding
 // field (bits 4-11).
 constexpr int kSignalDone = 1 << 12;
+// Bit 13 (tuning): GRP consecutive groups per workgroup in XCD order, each group's records stored as it
+// finishes, so a group's store is in flight while the next group loads (only the last store is waited for at the
+// wave's end).  Bit 14: the lane index made opaque per group, so the compiler cannot hoist lane-derived values
+// out of the group loop (live across it they cost registers: 128-147 VGPRs in the GRP > 1 variants above).
+constexpr int kGroupLoopXcd = 1 << 13;
+constexpr int kOpaqueLane = 1 << 14;
 template <int MIS, int COOP, int ABL = kProdAbl, int LAUX = kLoadAux, int SAUX = kStoreAux, int IDX = 0, int LWIN = LAUX,
           int GRP = 1, int GOPT = kProdGopt>
 __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : 4) void rx_classify_kernel(KArgs a) {
@@ -546,7 +556,15 @@ __global__ __launch_bounds__(kWave, (GOPT & 4) ? 2 : (GOPT & 2) ? 3 : 4) void rx
     // then wrapped each buffer load in a waterfall loop and serialized the window loads.
     if (__builtin_amdgcn_readfirstlane(pad_lds[(lane + 1) & 63]) == 0x7fffffffu) a.n = 0;
   }
-  if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
+  if constexpr (GOPT & kGroupLoopXcd) {
+    const uint32_t g0 = xcd_group(blockIdx.x, gridDim.x) * GRP;
+#pragma nounroll
+    for (int g = 0; g < GRP; ++g) {
+      int l = lane;
+      if constexpr (GOPT & kOpaqueLane) asm volatile("" : "+v"(l));
+      classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, (g0 + g) * a.fpw, l, nullptr);
+    }
+  } else if constexpr (GOPT & 8) { // XCD-aware order (tuning): workgroup b runs on XCD b % 8; give each XCD a
     // contiguous eighth of the batch instead of every eighth group
     classify_group<MIS, COOP, ABL, LAUX, SAUX, IDX, LWIN>(a, xcd_group(blockIdx.x, gridDim.x) * a.fpw, lane, nullptr);
     if constexpr (GOPT & kSignalDone) signal_done(a.sig_count, a.sig_flag, a.sig_token, lane);

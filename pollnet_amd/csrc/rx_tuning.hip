@@ -293,6 +293,16 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 12: launch_one<0, 1, kAblNoReduce | kProdAbl>(a, s); break;
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
     case 18: launch_one<0, 1, kAblNoStore | kProdAbl>(a, s); break;
+    case 49: launch_one<0, 1, kAblSmallStore | kProdAbl>(a, s); break;   // stores into 16 KiB
+    case 50: launch_one<0, 1, kProdAbl, kLoadAux, 1>(a, s); break;   // record stores sc0
+    case 51: launch_one<0, 1, kProdAbl, kLoadAux, 3>(a, s); break;   // sc0 nt
+    case 52: launch_one<0, 1, kProdAbl, kLoadAux, 17>(a, s); break;  // sc0 sc1
+    case 53: launch_one<0, 1, kProdAbl, kLoadAux, 18>(a, s); break;  // sc1 nt
+    case 54: launch_one<0, 1, kProdAbl, kLoadAux, 19>(a, s); break;  // sc0 sc1 nt
+    case 56: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, kProdGopt | kGroupLoopXcd | kOpaqueLane>(a, s); break;
+    case 57: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 4, kProdGopt | kGroupLoopXcd | kOpaqueLane>(a, s); break;
+    case 58: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 2, kProdGopt | kGroupLoopXcd>(a, s); break;
+    case 59: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 8, kProdGopt | kGroupLoopXcd | kOpaqueLane>(a, s); break;
     default: return set_err(ctx, PN_EINVAL, "variant: unknown");
   }
   hipError_t e = hipGetLastError();
