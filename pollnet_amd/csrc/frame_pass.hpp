@@ -80,6 +80,8 @@ enum : int { kPipeStream = 1 << 21 };
 // timing only: every wave's records into the first 16 KiB of the output (the stores issued, almost no
 // write-back volume)
 enum : int { kAblSmallStore = 1 << 22 };
+// timing only: the wave's record store issued before its loads (dummy records), none at its end
+enum : int { kAblEarlyStore = 1 << 23 };
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate | kPipeStream;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at

@@ -319,7 +319,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   if (bad_off) rec = u32x4{PN_MISS, 0, 0, PN_F_BADOFF}; // outside the launch's alignment class: not parsed
   if (lds_rec) { // grouped launches write the workgroup's records in one burst at its end
     *lds_rec = rec;
-  } else if constexpr (ABL & kAblNoStore) {
+  } else if constexpr (ABL & (kAblNoStore | kAblEarlyStore)) {
     if (rec.x == 0x7eadbeefu && rec.y == 0x12345678u) *reinterpret_cast<u32x4*>(a.out + f) = rec; // ~never
   } else if constexpr (ABL & kAblSmallStore) { // timing only: 16 blocks of 64 records, rewritten by every wave
     const uint32_t blk = __builtin_amdgcn_readfirstlane((f & ~63u) & 0x3C0u);
@@ -359,6 +359,11 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
   const uint8_t* wave_slot = a.frames + (uint64_t)wave_base * a.stride;
   // one wave-uniform descriptor over the wave's slots; lanes past n read zeros
   const __amdgpu_buffer_rsrc_t rs = frame_rsrc(wave_slot, n_here * a.stride);
+  if constexpr (ABL & kAblEarlyStore) {
+    const uint32_t blk = __builtin_amdgcn_readfirstlane(f & ~63u);
+    const __amdgpu_buffer_rsrc_t ro = frame_rsrc((const uint8_t*)(a.out + blk), 64 * 16);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{f, 0u, 0u, 0u}, ro, (f & 63u) * 16, 0, SAUX);
+  }
 
   Window h;
   uint32_t ether_type;

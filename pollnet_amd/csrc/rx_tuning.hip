@@ -294,6 +294,7 @@ int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_strid
     case 14: launch_one<0, 1, kAblNoMask>(a, s); break;
     case 18: launch_one<0, 1, kAblNoStore | kProdAbl>(a, s); break;
     case 49: launch_one<0, 1, kAblSmallStore | kProdAbl>(a, s); break;   // stores into 16 KiB
+    case 55: launch_one<0, 1, kAblEarlyStore | kProdAbl>(a, s); break;   // store issued first, none at the end
     case 50: launch_one<0, 1, kProdAbl, kLoadAux, 1>(a, s); break;   // record stores sc0
     case 51: launch_one<0, 1, kProdAbl, kLoadAux, 3>(a, s); break;   // sc0 nt
     case 52: launch_one<0, 1, kProdAbl, kLoadAux, 17>(a, s); break;  // sc0 sc1

@@ -16,8 +16,8 @@ NAMES = {0: "perlane_window", 1: "coop_window", 2: "perlane_defaultpolicy", 3: "
          22: "scalar_probe_walk", 23: "grp2_burst_records", 24: "grp4_burst_records", 25: "grp8_burst_records",
          26: "grp16_burst_records", 27: "grp8_records_each", 28: "grp1_lds10k", 29: "grp1_lds14k", 30: "grp8_each_lds10k",
          31: "grp1_vgpr3w", 32: "grp1_vgpr2w", 33: "grp2_burst_vgpr2w", 34: "nopad_5waves", 35: "xcd_contiguous", 36: "blockidx_order", 37: "no_skip_empty_loads", 38: "group_probe", 39: "per_lane_probe", 42: "late_probe", 43: "ABL_home_slot_only", 45: "ABL_home_slot_one_line", 47: "serial_window", 48: "no_pipe_stream",
-         11: "ABL_noprobe", 12: "ABL_noreduce", 14: "ABL_nomask", 18: "ABL_nostore", 49: "ABL_store_16KiB", 50: "store_sc0", 51: "store_sc0_nt", 52: "store_sc0_sc1", 53: "store_sc1_nt", 54: "store_sc0_sc1_nt", 56: "grp2_loop_xcd_opaque", 57: "grp4_loop_xcd_opaque", 58: "grp2_loop_xcd", 59: "grp8_loop_xcd_opaque"}
-TIMING_ONLY = {11, 12, 14, 18, 19, 43, 45, 49}
+         11: "ABL_noprobe", 12: "ABL_noreduce", 14: "ABL_nomask", 18: "ABL_nostore", 49: "ABL_store_16KiB", 50: "store_sc0", 55: "ABL_early_store", 51: "store_sc0_nt", 52: "store_sc0_sc1", 53: "store_sc1_nt", 54: "store_sc0_sc1_nt", 56: "grp2_loop_xcd_opaque", 57: "grp4_loop_xcd_opaque", 58: "grp2_loop_xcd", 59: "grp8_loop_xcd_opaque"}
+TIMING_ONLY = {11, 12, 14, 18, 19, 43, 45, 49, 55}
 
 
 def main():
