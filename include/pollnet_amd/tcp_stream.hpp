@@ -13,8 +13,11 @@
 //      TcpStream::initFilter's 4-tuple (0 = wildcard).  poll() matches a batch of ring
 //      slots against every filter in one pn_match_streams launch (one header line per
 //      frame; zero-copy from a pinned ring), then hands each matching frame, in ring
-//      order, to its stream's reassembler — the frames of no stream are never touched
-//      by the host.  A frame goes to the first stream whose filter it passes.
+//      order, to its streams' reassemblers — the frames of no stream are never touched
+//      by the host.  As with independent TcpStreams (each running its own filterPacket),
+//      a frame goes to every stream whose filter it passes, in stream order: the kernel
+//      names the first, the host tests the later filters on that frame only.
+//      setFirstMatchOnly(true): the first stream only (overlapping filters as priorities).
 // Handler: uint32_t h(int stream, const uint8_t* data, uint32_t size) -> bytes not consumed.
 #pragma once
 
@@ -173,6 +176,24 @@ class GpuTcpStreams {
   }
   Stream& stream(int i) { return *streams_[i]; }
   uint32_t streamCount() const { return (uint32_t)filters_.size(); }
+  // true: a frame goes to the first stream it passes only (default false: every stream it passes)
+  void setFirstMatchOnly(bool v) { first_only_ = v; }
+
+  // TcpStream::filterPacket (TcpStream.h:39-52) on the host, for the filters after a frame's first
+  // match: IPv4 (etherType read little-endian, 0x0008) and TCP, IHL assumed 5 (TcpStream.h:213-214),
+  // each non-zero field equal to the frame's, all in network order as stored
+  static bool filterPacket(const pn_stream_filter& f, const uint8_t* eth) {
+    uint16_t ether_type, src_port, dst_port;
+    uint32_t src_ip, dst_ip;
+    std::memcpy(&ether_type, eth + 12, 2);
+    std::memcpy(&src_ip, eth + 26, 4);
+    std::memcpy(&dst_ip, eth + 30, 4);
+    std::memcpy(&src_port, eth + 34, 2);
+    std::memcpy(&dst_port, eth + 36, 2);
+    return ether_type == 0x0008 && eth[23] == 6 && (!f.src_ip || f.src_ip == src_ip) &&
+           (!f.dst_ip || f.dst_ip == dst_ip) && (!f.src_port || f.src_port == src_port) &&
+           (!f.dst_port || f.dst_port == dst_port);
+  }
 
   // Match n ring slots on the GPU (chunks of max_batch, chunk k+1 on the GPU while
   // chunk k is reassembled) and feed every matching frame to its stream in ring order.
@@ -184,7 +205,7 @@ class GpuTcpStreams {
       if (hipPointerGetAttributes(&attr, slots) != hipSuccess || attr.type != hipMemoryTypeHost)
         return "zero-copy ring must be pinned host memory (hipHostMalloc / hipHostRegister)";
     }
-    const uint32_t chunks = (n + cap_ - 1) / cap_;
+    const uint32_t chunks = (n + cap_ - 1) / cap_, nf = (uint32_t)filters_.size();
     if (const char* e = launch(slots, n, 0)) return e;
     for (uint32_t k = 0; k < chunks; k++) {
       if (k + 1 < chunks)
@@ -197,6 +218,10 @@ class GpuTcpStreams {
         if (s == PN_NO_STREAM) continue;
         const uint8_t* eth = slots + (size_t)(base + i) * stride_ + off_;
         streams_[s]->handlePacket(eth, [&](const uint8_t* d, uint32_t size) { return h((int)s, d, size); });
+        if (first_only_) continue;
+        for (uint32_t t = s + 1; t < nf; t++)
+          if (filterPacket(filters_[t], eth))
+            streams_[t]->handlePacket(eth, [&](const uint8_t* d, uint32_t size) { return h((int)t, d, size); });
       }
     }
     return nullptr;
@@ -241,6 +266,7 @@ class GpuTcpStreams {
   pn_ctx* ctx_ = nullptr;
   hipStream_t stream_ = nullptr;
   GpuRx::Mode mode_ = GpuRx::Mode::ZeroCopy;
+  bool first_only_ = false;
   void* d_frames_[2] = {nullptr, nullptr};
   uint32_t* d_ids_[2] = {nullptr, nullptr};
   uint32_t* h_ids_[2] = {nullptr, nullptr};

@@ -3,12 +3,13 @@
 //
 // A captured ring of ~12,000 frames: 8 sniffed TCP streams (reordered, duplicated,
 // with SYNs), other TCP flows, UDP, ARP and IPv6 frames, IHL=6 frames.  8 filters with
-// wildcards that overlap (a frame goes to the first it passes; the last filter is
-// all-wildcard).  Checks:
+// wildcards that overlap (the last filter is all-wildcard).  Checks:
 //   1. every frame's stream id == the index of the first filter the reference's
 //      TcpStream::filterPacket accepts it for (copy and zero-copy, several chunk sizes);
 //   2. GpuTcpStreams::poll's handler log per stream (sizes and bytes) == feeding each
-//      frame, in ring order, to the reference TcpStream of its first matching filter.
+//      frame, in ring order, to the reference TcpStream of every filter that accepts it
+//      (independent TcpStreams, the default), and with setFirstMatchOnly(true) to that of
+//      its first accepting filter only.
 // argv[1] = libref_tcpstream.so.  Exit 0 = pass.
 #include <dlfcn.h>
 
@@ -158,17 +159,21 @@ int main(int argc, char** argv) {
       {"0.0.0.0", 0, "0.0.0.0", 1234},                        // shadowed by filter 4
       {"0.0.0.0", 0, "0.0.0.0", 0},                           // everything TCP/IPv4
   };
-  // reference: first accepting filter per frame
-  std::vector<uint32_t> want(n, PN_NO_STREAM);
+  // reference: the filters accepting each frame, and the first of them
+  std::vector<uint32_t> want(n, PN_NO_STREAM), accept(n, 0);
+  uint32_t multi = 0;
   for (uint32_t i = 0; i < n; i++) {
     const uint8_t* eth = ring + (size_t)i * stride + off;
     for (uint32_t k = 0; k < fs.size(); k++)
       if (ref_filter(eth, flen[i], fs[k].src_ip.c_str(), fs[k].src_port, fs[k].dst_ip.c_str(), fs[k].dst_port)) {
-        want[i] = k;
-        break;
+        accept[i] |= 1u << k;
+        if (want[i] == PN_NO_STREAM) want[i] = k;
       }
+    multi += __builtin_popcount(accept[i]) > 1;
   }
-  int fail = 0;
+  std::printf("frames accepted by more than one filter: %u\n", multi);
+  int fail_overlap = multi == 0;
+  int fail = fail_overlap;
   uint32_t per_id[9] = {};
   for (uint32_t i = 0; i < n; i++) per_id[want[i] == PN_NO_STREAM ? 8 : want[i]]++;
 
@@ -225,8 +230,10 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> calls;
     std::vector<uint8_t> bytes;
   };
-  std::vector<Log> ref_log(8);
-  {
+  std::vector<Log> ref_logs[2]; // [first-match only, every accepting stream]
+  for (int all = 0; all < 2; all++) {
+    std::vector<Log>& ref_log = ref_logs[all];
+    ref_log.resize(8);
     std::vector<void*> rs(8);
     for (auto& r : rs) r = ref_new(1, 0);
     std::vector<uint8_t> rb(16u << 20);
@@ -234,19 +241,23 @@ int main(int argc, char** argv) {
     for (uint32_t k = 0; k < 8; k++) {
       RefLog rl{rb.data(), 0, rb.size(), rc.data(), 0, (uint32_t)rc.size()};
       for (uint32_t i = 0; i < n; i++)
-        if (want[i] == k) ref_handle(rs[k], ring + (size_t)i * stride + off, flen[i], msg_len[k], &rl);
+        if (all ? (accept[i] >> k) & 1 : want[i] == k)
+          ref_handle(rs[k], ring + (size_t)i * stride + off, flen[i], msg_len[k], &rl);
       ref_log[k].calls.assign(rc.begin(), rc.begin() + rl.n_calls);
       ref_log[k].bytes.assign(rb.begin(), rb.begin() + rl.n_bytes);
     }
     for (auto r : rs) ref_free(r);
   }
+  for (int all = 0; all < 2; all++)
   for (int zc = 0; zc < 2; zc++)
     for (uint32_t chunk : {1000u, 4096u, 257u}) {
+      const std::vector<Log>& ref_log = ref_logs[all];
       auto g = std::make_unique<GpuTcpStreams<>>();
       if (const char* e = g->init(0, stride, off, chunk, zc ? GpuRx::Mode::ZeroCopy : GpuRx::Mode::Copy)) {
         std::printf("init: %s\n", e);
         return 5;
       }
+      g->setFirstMatchOnly(!all);
       for (auto& f : fs)
         if (g->addStream(f.src_ip.c_str(), f.src_port, f.dst_ip.c_str(), f.dst_port) < 0) return 6;
       std::vector<Log> got(8);
@@ -267,13 +278,14 @@ int main(int argc, char** argv) {
         bytes += got[k].bytes.size();
         calls += got[k].calls.size();
       }
-      std::printf("GpuTcpStreams (%s, chunk %u): %u/8 streams identical to the reference (%llu calls, %llu bytes)\n",
-                  zc ? "zero-copy" : "copy", chunk, same, (unsigned long long)calls, (unsigned long long)bytes);
+      std::printf("GpuTcpStreams (%s, chunk %u, %s): %u/8 streams identical to the reference (%llu calls, %llu bytes)\n",
+                  zc ? "zero-copy" : "copy", chunk, all ? "every matching stream" : "first match only", same,
+                  (unsigned long long)calls, (unsigned long long)bytes);
       fail += same != 8;
     }
   // the sniffed streams whose filter selects them alone are delivered intact
   for (int k : {0, 3}) {
-    const auto& b = ref_log[k].bytes;
+    const auto& b = ref_logs[1][k].bytes;
     const bool whole = b.size() == sn[k].data.size() && std::equal(b.begin(), b.end(), sn[k].data.begin());
     std::printf("stream %d: %zu of %zu bytes, %s\n", k, b.size(), sn[k].data.size(), whole ? "intact" : "NOT intact");
     fail += !whole;

@@ -38,3 +38,6 @@ def test_gpu_match_and_streams_vs_reference():
     p = subprocess.run([_bin("test_gpu_tcp_stream"), REF], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "PASS" in p.stdout and " 0 ids differ" in p.stdout, p.stdout
+    # both delivery modes (every accepting stream, as independent TcpStreams; first match only), 2 x 3 chunkings each
+    assert p.stdout.count("8/8 streams identical") == 12, p.stdout
+    assert p.stdout.count("every matching stream): 8/8") == 6, p.stdout
