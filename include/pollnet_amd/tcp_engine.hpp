@@ -31,6 +31,7 @@
 #include <netinet/in.h>
 #include <sys/ioctl.h>
 #include <sys/socket.h>
+#include <sys/uio.h>
 #include <cstdio>
 #include <time.h>
 #include <unistd.h>
@@ -517,6 +518,22 @@ class TcpEngine {
     uint32_t getSendable() const { // TcpConn.h:47-50
       if (fin_sent_) return 0;
       return (send_una_ + kSendBufCnt - 1 - data_next_) * smss_ - data_next_size_;
+    }
+    // TcpConn::getImmediatelySendable (TcpConn.h:52-56): what fits the peer's window now.  pollnet's wrappers
+    // run without a congestion window (CongestionControlAlgo = 0, EfviTcp.h:48, 206), so both_wnd_seq is the
+    // peer's window edge (TcpConn.h:189-192).
+    uint32_t getImmediatelySendable() const {
+      if (data_next_ != send_next_) return 0;
+      const int32_t wnd = (int32_t)(send_wnd_seq_ - segs_[send_next_ & (kSendBufCnt - 1)].seq - data_next_size_);
+      return std::min((uint32_t)std::max(0, wnd), getSendable());
+    }
+    // TcpConn::sendv (TcpConn.h:63-70): the pieces appended in order, the last one pushed.
+    uint32_t sendv(const iovec* iov, int iovcnt) {
+      if (fin_sent_) return 0;
+      uint32_t total = 0;
+      for (int i = 0; i < iovcnt; i++)
+        total += eng_->sendPartial(*this, (const uint8_t*)iov[i].iov_base, (uint32_t)iov[i].iov_len, i + 1 == iovcnt);
+      return total;
     }
     void sendFin() { eng_->sendFin(*this); }
     void setUserTimer(uint32_t timer_id, uint32_t duration_ms) { eng_->setUserTimer(*this, timer_id, duration_ms); }

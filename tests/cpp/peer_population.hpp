@@ -4,6 +4,7 @@
 // reference's own efvitcp server, oracle/ref_server.hpp).
 #pragma once
 
+#include <sys/uio.h>
 #include <arpa/inet.h>
 
 #include <algorithm>
@@ -320,6 +321,17 @@ struct PeerHandler {
     c.getPeername(a);
     const uint16_t port = ntohs(a.sin_port);
     if (port >= 30000 && port % 13 == 0) return n; // a chaos client's handler that consumes nothing: window fills
+    if (port % 4 == 1) { // the send side's state as the handler sees it (TcpConn.h:47-56)
+      char b[96];
+      std::snprintf(b, sizeof b, "data %u id=%u n=%u sendable=%u now=%u\n", port, c.getConnId(), n, c.getSendable(),
+                    c.getImmediatelySendable());
+      *log += b;
+    }
+    if (port % 8 == 3 && !c.fin_asked) { // echo in two pieces through sendv (TcpConn.h:63-70); what does not fit is dropped
+      iovec iov[2] = {{(void*)d, n / 2}, {(void*)(d + n / 2), n - n / 2}};
+      c.echoed += c.sendv(iov, 2);
+      return 0;
+    }
     if (port % 5 == 0 && n > 7) { // consume only whole 8-byte words: the rest is re-presented
       const uint32_t take = n & ~7u;
       if (!c.fin_asked && c.writeNonblock(d, take)) c.echoed += take;

@@ -11,6 +11,7 @@
 // The script is a deterministic function of what it receives, so any difference in the clients' behaviour
 // shows up as a different frame sequence: every frame the client sends (byte for byte) and the handler log
 // must be identical.   argv: twin | gpu [scripts]     exit 0 = pass
+#include <sys/uio.h>
 #include <arpa/inet.h>
 
 #include <cstdio>
@@ -254,10 +255,21 @@ struct CliHandler {
   }
   uint32_t onTcpData(Conn& c, const uint8_t* d, uint32_t n) {
     line("data", c, n);
-    char b[32];
-    std::snprintf(b, sizeof b, "  first %02x last %02x\n", d[0], d[n - 1]);
+    char b[96];
+    std::snprintf(b, sizeof b, "  first %02x last %02x sendable=%u now=%u\n", d[0], d[n - 1], c.getSendable(),
+                  c.getImmediatelySendable());
     *log += b;
-    if (++c.deliveries % 3 == 0) c.writeNonblock(d, std::min<uint32_t>(n, 700));
+    const uint32_t k = ++c.deliveries % 3, m = std::min<uint32_t>(n, 700);
+    if (k == 0) {
+      c.writeNonblock(d, m);
+    } else if (k == 1) { // two pieces through sendv (TcpConn.h:63-70)
+      iovec iov[2] = {{(void*)d, m / 2}, {(void*)(d + m / 2), m - m / 2}};
+      std::snprintf(b, sizeof b, "  sendv %u\n", c.sendv(iov, 2));
+      *log += b;
+    } else { // writeSome: what fits, and the send timeout re-armed (EfviTcp.h:66-70)
+      std::snprintf(b, sizeof b, "  writeSome %d\n", c.writeSome(d, std::min<uint32_t>(n, 300)));
+      *log += b;
+    }
     return n & 7; // whole 8-byte words consumed
   }
   void onTcpDisconnect(Conn& c) { line("disconnect", c); }

@@ -179,8 +179,20 @@ static int coverage(const Transcript& t) {
               "%zu send buffer full\n",
               disc("connection reset"), disc("remote close"), disc("timeout"), disc("connection closed"),
               disc("send buffer full"));
+  // send-side samples (getSendable / getImmediatelySendable, logged by the handler): how many, and how many
+  // limited by the peer's window rather than by free send buffers
+  uint32_t samples = 0, wnd_limited = 0, zero_now = 0;
+  for (size_t p = 0; (p = t.log.find("data ", p)) != std::string::npos; p++) {
+    unsigned sendable = 0, now = 0;
+    if (std::sscanf(t.log.c_str() + t.log.find("sendable=", p), "sendable=%u now=%u", &sendable, &now) != 2) continue;
+    samples++;
+    wnd_limited += now < sendable;
+    zero_now += now == 0;
+  }
+  std::printf("  send side: %u getSendable/getImmediatelySendable samples, %u window-limited (%u zero)\n", samples,
+              wnd_limited, zero_now);
   return (synacks && data && fins && rsts && est && count("recv timeout") && count("sendFin") &&
-          disc("connection reset") && disc("remote close"))
+          disc("connection reset") && disc("remote close") && samples && wnd_limited)
              ? 0
              : 1;
 }
