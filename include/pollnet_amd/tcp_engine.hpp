@@ -537,6 +537,23 @@ class TcpEngine {
     }
     void sendFin() { eng_->sendFin(*this); }
     void setUserTimer(uint32_t timer_id, uint32_t duration_ms) { eng_->setUserTimer(*this, timer_id, duration_ms); }
+#ifdef EFVITCP_DEBUG
+    // TcpConn::dump / shortDump (TcpConn.h:107-128, debug builds): the connection's state on stdout, the
+    // congestion fields as pollnet's wrappers leave them (no congestion window)
+    void dump(const char* note) const {
+      std::printf("%s: conn_id: %u, key: %llu, established: %d, fin_sent: %d, fin_received: %d, fast_re: %d, "
+                  "dup_ack_cnt: %u, send_una: %u, send_next: %u, data_next: %u, data_next_size: %u, "
+                  "send_next_seq: %u, both_wnd_seq: %u, rto: %u, srtt: %u, rttvar: %u, recent_ts: %u, in_recover: %d, "
+                  "recover: %u, retries: %u, src port: %u, dst port: %u\n",
+                  note, id_, (unsigned long long)key_, established_, fin_sent_, fin_received_, fast_re_, dup_ack_cnt_,
+                  send_una_, send_next_, data_next_, data_next_size_, segs_[send_next_ & (kSendBufCnt - 1)].seq,
+                  send_wnd_seq_, rto_, srtt_, rttvar_, rx_.recentTs(), in_recover_, recover_, retries_,
+                  ntohs(local_port_), ntohs(peer_port_));
+    }
+    void shortDump(const char* note = "") const {
+      std::printf("%s, src port: %u, dst port: %u\n", note, ntohs(local_port_), ntohs(peer_port_));
+    }
+#endif
 
    private:
     friend class TcpEngine;
