@@ -516,6 +516,26 @@ def server_poll():
         return {"error": repr(ex)}
 
 
+def sniffer_streams():
+    """The sniffer path end to end (bench/bench_streams): 1 Mi captured frames in pinned host
+    memory, 8 watched TCP streams (every 16th frame) among other TCP traffic; GpuTcpStreams::poll
+    (pn_match_streams over PCIe, host reassembly of the watched frames) against every stream's
+    filterPacket + handlePacket on one core; per-stream bytes and a checksum of them must agree."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "bench", "bench_streams")
+    if not os.path.exists(exe):
+        return {"error": "bench/bench_streams not built"}
+    try:
+        r = subprocess.run([exe, str(1 << 20), "8", "16", "3"], capture_output=True, text=True, timeout=90)
+        line = json.loads(r.stdout.strip().splitlines()[-1])
+        if r.returncode != 0:
+            line["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
+        return line
+    except Exception as ex:  # measured extra; never blocks the bench line
+        return {"error": repr(ex)}
+
+
 def small_batch_latency():
     """Host-visible round trip of one small batch (bench/bench_signal): pn_classify +
     stream sync against pn_classify_notify + a spin on the pinned completion word, 64 / 512 / 1024
@@ -871,6 +891,7 @@ def run_rank(rank, world, local_rank, args):
         except Exception as ex:  # measured extras; never block the bench line
             sec["error"] = repr(ex)
         sec["tcp_server_poll"] = server_poll()
+        sec["sniffer_streams"] = sniffer_streams()
         sec["small_batch_latency"] = small_batch_latency()
         sec["seconds"] = round(time.perf_counter() - t_sec, 1)
         out["secondary"] = sec
