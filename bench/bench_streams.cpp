@@ -9,7 +9,7 @@
 //         PCIe (zero copy), the host reassembling only the frames of a watched stream.
 // Both deliver every stream's bytes to the same handler; the per-stream byte counts and a checksum of the
 // delivered bytes must agree.  One JSON line on stdout.
-//   bench_streams [frames=1048576] [streams=8] [watched_every=16] [reps=5]
+//   bench_streams [frames=1048576] [streams=8] [watched_every=16] [reps=5] [chunk=262144]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -83,7 +83,8 @@ int main(int argc, char** argv) {
   const uint32_t S = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 8;
   const uint32_t every = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 16;
   const int reps = argc > 4 ? std::atoi(argv[4]) : 5;
-  if (!n || !S || S > PN_MAX_STREAM_FILTERS || !every || reps < 1) return 2;
+  const uint32_t chunk = argc > 5 ? (uint32_t)std::atoi(argv[5]) : (1u << 18);
+  if (!n || !S || S > PN_MAX_STREAM_FILTERS || !every || reps < 1 || !chunk) return 2;
 
   uint8_t* ring = nullptr;
   if (hipHostMalloc((void**)&ring, (size_t)n * kStride, hipHostMallocDefault) != hipSuccess) return 3;
@@ -144,7 +145,7 @@ int main(int argc, char** argv) {
   const char* err = nullptr;
   for (int r = 0; r < reps && !err; r++) {
     auto g = std::make_unique<GpuTcpStreams<>>();
-    if ((err = g->init(0, kStride, kOff, 1u << 18, GpuRx::Mode::ZeroCopy))) break;
+    if ((err = g->init(0, kStride, kOff, chunk, GpuRx::Mode::ZeroCopy))) break;
     for (uint32_t k = 0; k < S; k++)
       if (g->addStream(src[k].c_str(), (uint16_t)(5000 + k), "10.0.0.1", 1234) < 0) err = "addStream failed";
     if (err) break;
@@ -169,12 +170,12 @@ int main(int argc, char** argv) {
   std::printf("{\"bench\": \"sniffer_streams\", \"frames\": %u, \"streams\": %u, \"watched_every\": %u, "
               "\"watched_frames\": %llu, \"delivered_bytes\": %llu, \"cpu_one_core\": {\"ms\": %.3f, \"mframes_per_s\": %.2f, "
               "\"gbit_per_s\": %.1f}, \"gpu_zero_copy\": {\"ms\": %.3f, \"mframes_per_s\": %.2f, \"gbit_per_s\": %.1f}, "
-              "\"gpu_over_cpu\": %.2f, \"delivery_equal\": %s, \"reps\": %d, \"note\": \"capture in pinned host "
+              "\"gpu_over_cpu\": %.2f, \"delivery_equal\": %s, \"reps\": %d, \"chunk\": %u, \"note\": \"capture in pinned host "
               "memory (2-KiB slots); CPU: every stream's filterPacket per frame + handlePacket (restated, held equal to "
               "the reference TcpStream by the tests); GPU: GpuTcpStreams::poll (pn_match_streams over PCIe + host "
               "reassembly of the watched frames)\"}\n",
               n, S, every, (unsigned long long)watched, (unsigned long long)delivered, c * 1e3, n / c / 1e6,
-              wire * 8 / c / 1e9, g * 1e3, n / g / 1e6, wire * 8 / g / 1e9, c / g, equal ? "true" : "false", reps);
+              wire * 8 / c / 1e9, g * 1e3, n / g / 1e6, wire * 8 / g / 1e9, c / g, equal ? "true" : "false", reps, chunk);
   (void)hipHostFree(ring);
   return equal ? 0 : 1;
 }

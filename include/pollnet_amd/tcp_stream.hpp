@@ -213,9 +213,22 @@ class GpuTcpStreams {
       if (hipEventSynchronize(done_[k & 1]) != hipSuccess) return "hipEventSynchronize failed";
       const uint32_t base = k * cap_, m = std::min(cap_, n - base);
       const uint32_t* ids = h_ids_[k & 1];
+      // The host touches only the matched frames, spread over the ring, so each is a run of cold lines:
+      // prefetch the next kPrefetchAhead matched frames (the first 1536 B of each slot's frame: reading its
+      // length first would stall on that line) while this one is reassembled.
+      const uint32_t span = std::min<uint32_t>(1536u, stride_ - off_);
+      uint32_t ahead = 0, inflight = 0; // next index to look at for a prefetch; matched frames prefetched past i
       for (uint32_t i = 0; i < m; i++) {
         const uint32_t s = ids[i];
         if (s == PN_NO_STREAM) continue;
+        if (ahead <= i) ahead = i + 1, inflight = 0;
+        else if (inflight) inflight--;
+        for (; inflight < kPrefetchAhead && ahead < m; ahead++) {
+          if (ids[ahead] == PN_NO_STREAM) continue;
+          const uint8_t* e = slots + (size_t)(base + ahead) * stride_ + off_;
+          for (uint32_t o = 0; o < span; o += 64) __builtin_prefetch(e + o);
+          inflight++;
+        }
         const uint8_t* eth = slots + (size_t)(base + i) * stride_ + off_;
         streams_[s]->handlePacket(eth, [&](const uint8_t* d, uint32_t size) { return h((int)s, d, size); });
         if (first_only_) continue;
@@ -267,6 +280,10 @@ class GpuTcpStreams {
   hipStream_t stream_ = nullptr;
   GpuRx::Mode mode_ = GpuRx::Mode::ZeroCopy;
   bool first_only_ = false;
+#ifndef PN_STREAM_PREFETCH_AHEAD
+#define PN_STREAM_PREFETCH_AHEAD 4
+#endif
+  static constexpr uint32_t kPrefetchAhead = PN_STREAM_PREFETCH_AHEAD;
   void* d_frames_[2] = {nullptr, nullptr};
   uint32_t* d_ids_[2] = {nullptr, nullptr};
   uint32_t* h_ids_[2] = {nullptr, nullptr};
