@@ -498,16 +498,17 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
 def server_poll():
     """The drop-in server itself (bench/bench_tcp_server quick, DESIGN §14): GpuTcpServer::poll over
     256 connections receiving in-order 1514-B segments from a pinned host ring (handshake, RX, the
-    server's ACKs), GPU backend at RxBatch 512 and pipelined at 16384, and the same server on the
-    sequential CPU backend (the oracle classifying each frame on one core).  PCIe-bound: every frame
-    crosses it for its checksums."""
+    server's ACKs), GPU backend at RxBatch 512 and pipelined at 16384, the same two with the checksum
+    discard off (the reference's release path: the kernel reads each frame's header lines only,
+    pn_set_verify), and the same server on the sequential CPU backend (the oracle classifying each frame
+    on one core).  PCIe-bound: with checksums verified every frame crosses it whole."""
     import subprocess
 
     exe = os.path.join(ROOT, "bench", "bench_tcp_server")
     if not os.path.exists(exe):
         return {"error": "bench/bench_tcp_server not built"}
     try:
-        r = subprocess.run([exe, "256", "400", "quick"], capture_output=True, text=True, timeout=90)
+        r = subprocess.run([exe, "256", "400", "quick"], capture_output=True, text=True, timeout=120)
         line = json.loads(r.stdout.strip().splitlines()[-1])
         if r.returncode != 0:
             line["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
@@ -617,6 +618,37 @@ def secondary_tx(torch, pa, n, steps, stream):
         torch.cuda.empty_cache()
     ctx.close()
     return out
+
+
+def secondary_release_path(torch, pa, ctx, frames_b, res, n, steps, stream):
+    """C2 through the release path (pn_set_verify(ctx, 0): Core::checksum is debug-only in the reference,
+    Core.h:448-478): the kernel reads each frame's 128-B header line instead of the whole frame.  Same rotating
+    resident batches; batch 0's records must equal the full path's (already oracle-gated) with the TCP verdict
+    taken out.  Algorithmic bytes per frame: the 64-B header window read + the 16-B record."""
+    F = pa.rx.F
+    ctx.classify(frames_b[0], STRIDE, FRAME_OFF, n, res, stream)
+    torch.cuda.synchronize()
+    full = res.cpu().numpy().view(pa.RESULT_DTYPE).copy()
+    ctx.set_verify(False)
+    try:
+        ctx.classify(frames_b[0], STRIDE, FRAME_OFF, n, res, stream)
+        torch.cuda.synchronize()
+        got = res.cpu().numpy().view(pa.RESULT_DTYPE)
+        exp = full.copy()
+        exp["flags"] = (exp["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
+        exp["tcp_fold"] = 0
+        ok = bool(np.array_equal(got, exp))
+        kern = time_launches(torch, lambda d: ctx.classify(d, STRIDE, FRAME_OFF, n, res, stream), frames_b, steps, stream)
+    finally:
+        ctx.set_verify(True)
+    algo = n * (64 + 16)
+    return {"kernel_ms": round(kern, 5), "mframes_per_s": round(n / (kern * 1e-3) / 1e6, 1),
+            "algorithmic_bytes_per_launch": algo, "achieved_gbs": round(algo / (kern * 1e-3) / 1e9, 1),
+            "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "line_traffic_gbs": round(n * (128 + 16) / (kern * 1e-3) / 1e9, 1),
+            "records_equal_full_path_less_tcp_verdict": ok,
+            "note": "pn_set_verify(ctx, 0) on the rotating C2 batches: one 128-B header line read per frame (the "
+                    "64-B window block inside it), no TCP checksum; DESIGN §4"}
 
 
 def secondary_c4_shard(torch, pa, ctx_dev, steps, R, stream):
@@ -878,6 +910,10 @@ def run_rank(rank, world, local_rank, args):
             sec["match_streams"] = secondary_streams(torch, pa, ctx, frames_b, slots, n, stream)
         except Exception as ex:  # measured extra; never blocks the bench line
             sec["match_streams"] = {"error": repr(ex)}
+        try:
+            sec["c2_release_path"] = secondary_release_path(torch, pa, ctx, frames_b, res, n, args.steps, stream)
+        except Exception as ex:  # measured extra; never blocks the bench line
+            sec["c2_release_path"] = {"error": repr(ex)}
         del frames_b[1:]  # the C2 batches rotated above are done; make room for the others
         torch.cuda.empty_cache()
         try:

@@ -178,8 +178,10 @@ struct Run {
   std::string err;
 };
 
+// verify = false: the checksum discard off, as the reference's release build runs (no checksum verified);
+// the GPU backend then classifies from each frame's header lines only (pn_set_verify)
 template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false>
-static Run runOne(uint32_t n_flows, uint32_t polls) {
+static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   Run out;
   using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe>, BenchLink, Backend>;
   auto srv = std::make_unique<Server>();
@@ -188,6 +190,7 @@ static Run runOne(uint32_t n_flows, uint32_t polls) {
     out.err = srv->getLastError();
     return out;
   }
+  srv->setDropBadChecksum(verify);
   Handler h;
   BenchLink& link = srv->link();
   link.phase = BenchLink::Syn;
@@ -275,9 +278,11 @@ int main(int argc, char** argv) {
     ok = ok && r.ok;
   };
   const bool cpu_only = argc > 3 && std::strcmp(argv[3], "cpu") == 0;
-  if (argc > 3 && std::strcmp(argv[3], "quick") == 0) { // bench.py's secondary leg: three lines
+  if (argc > 3 && std::strcmp(argv[3], "quick") == 0) { // bench.py's secondary leg
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
+    leg("gpu_rxbatch_512_release_path", runOne<512, GpuBackend>(n_flows, polls, false));
+    leg("gpu_rxbatch_16384_pipelined_release_path", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4, false));
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
   } else if (!cpu_only) {
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));

@@ -80,6 +80,9 @@ typedef struct pn_result {
                                    the frame (undefined); TCP_OK/RFC_TCP_OK cleared, tcp_fold=0xFFFF */
 #define PN_F_BADOFF 0x4000u     /* pn_classify_indexed: offset outside the call's eth_mod16 class; the
                                    frame was not read and the record is {PN_MISS, 0, 0, 0, BADOFF, 0} */
+#define PN_F_TCP_UNCHECKED 0x8000u /* pn_set_verify(ctx, 0): the reference's release path, which verifies no
+                                   checksum (Core::checksum is debug-only, Core.h:448-478): only the frame's
+                                   header lines were read; TCP_OK / RFC_TCP_OK never set, tcp_fold = 0 */
 
 /* ---- 16-byte conn-table entry, identical layout to ConnHashEntry (Core.h:178-182) ---- */
 typedef struct pn_conn_entry {
@@ -147,6 +150,14 @@ int pn_device_count(int* n);
  * nothing. */
 int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entries, uint64_t tbl_mask,
                       uint32_t max_conn_cnt);
+
+/* What the classify entry points verify on this ctx (default 1: both checksums, as the reference's debug
+ * build does before every frame it sends or receives, Core.h:448-478).  verify_tcp = 0: the reference's
+ * release path — the TCP checksum is neither computed nor read for (the kernel reads only each frame's
+ * header lines: one 128-B line in the default layout instead of the whole frame); every other record field,
+ * PN_F_IP_OK and PN_F_RFC_IP_OK included, is the same, and PN_F_TCP_UNCHECKED marks the record.  Applies to
+ * launches issued after the call. */
+int pn_set_verify(pn_ctx* ctx, int verify_tcp);
 
 /* Classify n frames resident in device memory (asynchronous on `stream`).
  *   frames_dev : base of n slots, 16-byte aligned; frame i's Ethernet header is at

@@ -354,6 +354,7 @@ class GpuBackend {
     rx_ring_ = tx_ring_ = nullptr;
     const uint32_t chunk = rx_chunk && rx_chunk < rx_cap ? rx_chunk : rx_cap;
     if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy)) return e;
+    if (pn_set_verify(rx_.ctx(), verify_ ? 1 : 0)) return pn_last_error(rx_.ctx());
     // the TX fill has a stream of its own: pipelined, it runs beside the next batch's classify
     if (!tx_stream_ && hipStreamCreateWithFlags(&tx_stream_, hipStreamNonBlocking) != hipSuccess)
       return "hipStreamCreate(tx) failed";
@@ -373,6 +374,12 @@ class GpuBackend {
     return nullptr;
   }
   uint8_t* rxSlots(uint32_t half = 0) { return rx_ring_ + (size_t)half * rx_cap_ * kStride; }
+  // Whether classify verifies the TCP checksum (pn_set_verify).  Off, the kernel reads only each frame's
+  // header lines over PCIe instead of the whole frame: the engine turns it off with its checksum discard.
+  void setVerify(bool v) {
+    verify_ = v;
+    if (rx_.ctx()) (void)pn_set_verify(rx_.ctx(), v ? 1 : 0);
+  }
   // Pipelined RX: launch classifies the first n slots of one half against the snapshot on the
   // device (syncTable); collect waits for it and calls f(key, rec, eth) in ring order.
   const char* launch(uint32_t half, uint32_t n, const ConnTable&) { return rx_.submit(rxSlots(half), n, half); }
@@ -426,6 +433,7 @@ class GpuBackend {
   }
 
   GpuRx rx_;
+  bool verify_ = true;
   hipStream_t tx_stream_ = nullptr;
   uint8_t* rx_ring_ = nullptr;
   uint8_t* tx_ring_ = nullptr;
@@ -594,8 +602,14 @@ class TcpEngine {
   // Records re-resolved on the host because the table changed after their snapshot.
   uint64_t reResolved() const { return re_resolved_; }
   // Drop checksum-failed frames before they touch any state (what the NIC's RX checksum
-  // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.
-  void setDropBadChecksum(bool drop) { drop_bad_ = drop; }
+  // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.  Off, the frames
+  // are trusted as the reference's release build trusts them (Core::checksum is debug-only,
+  // Core.h:448-478), and the GPU backend stops verifying the TCP checksum: its classify reads
+  // only each frame's header lines (pn_set_verify).
+  void setDropBadChecksum(bool drop) {
+    drop_bad_ = drop;
+    be_.setVerify(drop);
+  }
   const ConnTable& table() const { return table_; }
   uint32_t nowTs() const { return wheel_.now(); }
   // Frames built since the last flush (checksums not yet filled), plus (pipelined) those whose

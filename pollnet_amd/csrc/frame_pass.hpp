@@ -82,6 +82,9 @@ enum : int { kPipeStream = 1 << 21 };
 enum : int { kAblSmallStore = 1 << 22 };
 // timing only: the wave's record store issued before its loads (dummy records), none at its end
 enum : int { kAblEarlyStore = 1 << 23 };
+// product (pn_set_verify(ctx, 0)): no segment stream and no TCP verdict -- the header lines only, as the
+// reference's release path reads them (Core::checksum is debug-only, Core.h:448-478)
+enum : int { kHeaderOnly = 1 << 24 };
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate | kPipeStream;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at

@@ -31,6 +31,7 @@ struct pn_ctx {
   uint32_t n_entries = 0;
   uint64_t mask = 0;
   uint32_t max_conn = 0;
+  bool verify_tcp = true; // pn_set_verify: false = header lines only (the reference's release path)
   std::vector<hipStream_t> streams; // distinct streams launched on since the last set / sync
   std::vector<hipEvent_t> retired;  // recorded on those streams at the last set (pooled)
   size_t n_retired = 0;

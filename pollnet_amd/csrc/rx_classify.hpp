@@ -289,7 +289,12 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
                                        u32x4* lds_rec) {
   uint32_t flags = st.flags;
   uint32_t tcp_fold = 0xffff;
-  if (!st.trunc) {
+  if constexpr ((ABL & kHeaderOnly) != 0) { // the release path: no TCP sum (the IP header is in the window)
+    flags |= PN_F_TCP_UNCHECKED;
+    tcp_fold = 0;
+    if (!st.trunc && st.ihl >= 5 && 4 * st.ihl <= st.tot_len && csum_fold(st.s_ip20 + st.s_opt) == 0)
+      flags |= PN_F_RFC_IP_OK;
+  } else if (!st.trunc) {
     const uint32_t s_seg = st.t_all - st.s_ip20; // exact: both are exact word sums
     const uint32_t s_addr = (st.src_ip >> 16) + (st.src_ip & 0xffff) + (st.dst_ip >> 16) + (st.dst_ip & 0xffff);
     // sum.add(ntohs(0x6)) ; sum.add(htons(tcp_len))  (Core.h:462-464)
@@ -492,6 +497,8 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
       }
     }
     st.t_all += sum;
+  } else if constexpr ((ABL & kHeaderOnly) != 0) {
+    // no segment stream: the record needs only the header lines
   } else {
     if constexpr ((ABL & kSkipWaveGate) && (ABL & kSkipEmptyLoads)) {
       // a frame whose extent ends before its second stream KiB: take the skipping form
@@ -618,10 +625,11 @@ void launch_one(const KArgs& a, hipStream_t s) {
 }
 
 
-template <int MIS, bool SIG = false>
+template <int MIS, bool SIG = false, bool HO = false>
 void launch(const KArgs& a, hipStream_t s) {
   constexpr int G = SIG ? (kProdGopt | kSignalDone) : kProdGopt;
-  if (coop_layout(a)) return launch_one<MIS, 1, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, G>(a, s);
-  launch_one<MIS, 0, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux, 1, G>(a, s);
+  constexpr int A = HO ? (kProdAbl | kHeaderOnly) : kProdAbl;
+  if (coop_layout(a)) return launch_one<MIS, 1, A, kLoadAux, kStoreAux, 0, kLoadAux, 1, G>(a, s);
+  launch_one<MIS, 0, A, kLoadAux, kStoreAux, 0, kLoadAux, 1, G>(a, s);
 }
 } // namespace

@@ -34,17 +34,38 @@ int strided_args(pn_ctx* ctx, const char* fn, const void* frames_dev, uint32_t s
   return PN_OK;
 }
 
-template <bool SIG>
-void launch_strided(const KArgs& a, uint32_t frame_off, hipStream_t s) {
+template <bool SIG, bool HO>
+void launch_strided_as(const KArgs& a, uint32_t frame_off, hipStream_t s) {
   switch ((frame_off + 14) & 15) {
-    case 0: launch<0, SIG>(a, s); break;
-    case 2: launch<2, SIG>(a, s); break;
-    case 4: launch<4, SIG>(a, s); break;
-    case 6: launch<6, SIG>(a, s); break;
-    case 8: launch<8, SIG>(a, s); break;
-    case 10: launch<10, SIG>(a, s); break;
-    case 12: launch<12, SIG>(a, s); break;
-    default: launch<14, SIG>(a, s); break;
+    case 0: launch<0, SIG, HO>(a, s); break;
+    case 2: launch<2, SIG, HO>(a, s); break;
+    case 4: launch<4, SIG, HO>(a, s); break;
+    case 6: launch<6, SIG, HO>(a, s); break;
+    case 8: launch<8, SIG, HO>(a, s); break;
+    case 10: launch<10, SIG, HO>(a, s); break;
+    case 12: launch<12, SIG, HO>(a, s); break;
+    default: launch<14, SIG, HO>(a, s); break;
+  }
+}
+
+// the ctx's verify setting picks the full kernel or the header-only one (pn_set_verify)
+template <bool SIG>
+void launch_strided(const pn_ctx* ctx, const KArgs& a, uint32_t frame_off, hipStream_t s) {
+  if (ctx->verify_tcp) launch_strided_as<SIG, false>(a, frame_off, s);
+  else launch_strided_as<SIG, true>(a, frame_off, s);
+}
+
+template <int A>
+void launch_indexed(const KArgs& a, uint32_t eth_mod16, hipStream_t s) {
+  switch ((eth_mod16 + 14) & 15) {
+    case 0: launch_one<0, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 2: launch_one<2, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 4: launch_one<4, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 6: launch_one<6, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 8: launch_one<8, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 10: launch_one<10, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    case 12: launch_one<12, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
+    default: launch_one<14, 1, A, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
   }
 }
 
@@ -146,7 +167,7 @@ int pn_classify(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint3
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  launch_strided<false>(a, frame_off, s);
+  launch_strided<false>(ctx, a, frame_off, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify launch");
   pn_internal::note_stream(ctx, s);
@@ -167,7 +188,7 @@ int pn_classify_notify(pn_ctx* ctx, const void* frames, uint32_t slot_stride, ui
   if (rc) return rc;
   a.sig_flag = done_word;
   a.sig_token = token;
-  launch_strided<true>(a, frame_off, s);
+  launch_strided<true>(ctx, a, frame_off, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (notify) launch");
   pn_internal::note_stream(ctx, s);
@@ -201,19 +222,17 @@ int pn_classify_indexed(pn_ctx* ctx, const void* base, const uint64_t* offsets, 
   hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
-  switch ((eth_mod16 + 14) & 15) {
-    case 0: launch_one<0, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    case 2: launch_one<2, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    case 4: launch_one<4, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    case 6: launch_one<6, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    case 8: launch_one<8, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    case 10: launch_one<10, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    case 12: launch_one<12, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-    default: launch_one<14, 1, kProdAbl, kLoadAux, kStoreAux, 1, kIdxWin, 1, kXcdOrder>(a, s); break;
-  }
+  if (ctx->verify_tcp) launch_indexed<kProdAbl>(a, eth_mod16, s);
+  else launch_indexed<kProdAbl | kHeaderOnly>(a, eth_mod16, s);
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "rx_classify (indexed) launch");
   pn_internal::note_stream(ctx, s);
+  return PN_OK;
+}
+
+int pn_set_verify(pn_ctx* ctx, int verify_tcp) {
+  if (!ctx) return set_err(nullptr, PN_EINVAL, "pn_set_verify: ctx is NULL");
+  ctx->verify_tcp = verify_tcp != 0;
   return PN_OK;
 }
 

@@ -44,6 +44,7 @@ class F:
     NOT_TCP = 0x1000
     TRUNC = 0x2000
     BADOFF = 0x4000
+    TCP_UNCHECKED = 0x8000  # pn_set_verify(ctx, 0): the release path, no TCP checksum
 
 
 RESULT_DTYPE = np.dtype(
@@ -118,6 +119,7 @@ _pn_tx_fill = _sig("pn_tx_fill", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _v
 _pn_classify_notify = _sig("pn_classify_notify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _vp, _vp, _u32)
 _pn_tx_fill_notify = _sig("pn_tx_fill_notify", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp, _u32)
 _pn_sync = _sig("pn_sync", _i32, _vp)
+_pn_set_verify = _sig("pn_set_verify", _i32, _vp, _i32)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 
 # The seeded workload generator lives in its own library (include/pollnet_amd_gen.h), outside
@@ -278,6 +280,11 @@ class RxContext:
         )
         self.max_conn_cnt = max_conn_cnt
         self._held.clear()
+
+    def set_verify(self, verify_tcp: bool):
+        """pn_set_verify: False = the reference's release path (header lines only, no TCP checksum;
+        records carry PN_F_TCP_UNCHECKED); True (default) = both checksums verified."""
+        _check(_pn_set_verify(self._h, 1 if verify_tcp else 0), self._h, "pn_set_verify")
 
     def classify(self, frames_dev, slot_stride: int, frame_off: int, n: int, results_dev, stream=None):
         """Asynchronous launch on `stream` (torch.cuda.Stream, raw handle, or None = null stream)."""

@@ -91,7 +91,7 @@ static Transcript runRef(const std::vector<Client>& pop) {
 }
 
 template <class Backend>
-static Transcript runProd(const std::vector<Client>& pop) {
+static Transcript runProd(const std::vector<Client>& pop, bool drop_bad = true) {
   using Srv = GpuTcpServer<ProdConf, PeerLink, Backend>;
   auto srv = std::make_unique<Srv>();
   Transcript t;
@@ -101,6 +101,7 @@ static Transcript runProd(const std::vector<Client>& pop) {
   }
   srv->link().defer = true;
   srv->link().clients = pop;
+  srv->setDropBadChecksum(drop_bad); // off: the GPU backend classifies from the header lines only (pn_set_verify)
   PeerHandler<typename Srv::Conn> h{&t.log};
   for (t.polls = 1; t.polls < kMaxPolls; t.polls++) {
     srv->poll(h, kT0 + ((int64_t)t.polls << 20));
@@ -302,10 +303,10 @@ static std::vector<size_t> ref_polls(std::vector<std::vector<uint8_t>> frames, i
   }
   return out;
 }
-template <class Conf>
+template <class Conf, class Backend = OracleBackend>
 static std::vector<size_t> prod_polls(std::vector<std::vector<uint8_t>> frames, int polls, bool drop_bad,
                                       std::vector<std::vector<uint8_t>>* sent) {
-  using P = GpuTcpServer<Conf, BurstLink, OracleBackend>;
+  using P = GpuTcpServer<Conf, BurstLink, Backend>;
   auto p = std::make_unique<P>();
   p->initWithLink("10.0.0.1", 1234, kT0);
   p->setDropBadChecksum(drop_bad);
@@ -342,16 +343,18 @@ static int rx_batch_divergence() {
 // Bad checksums: the reference relies on the NIC to discard them (an ef_vi RX_DISCARD event); run without a
 // NIC it answers a corrupted unknown-flow segment with an RST.  The engine discards it after pn_classify
 // (setDropBadChecksum, default on); with the discard off it sends the reference's RST, byte for byte.
-static int bad_checksum_divergence() {
+// On the GPU backend the discard off also switches the kernel to the header lines only (pn_set_verify(ctx, 0)).
+template <class Backend = OracleBackend>
+static int bad_checksum_divergence(const char* backend = "") {
   BurstLink link;
   const auto ref = ref_polls(burst(3, true), 1, link);
   std::vector<std::vector<uint8_t>> dropped, kept;
-  const auto on = prod_polls<ProdConf>(burst(3, true), 1, true, &dropped);
-  const auto off = prod_polls<ProdConf>(burst(3, true), 1, false, &kept);
+  const auto on = prod_polls<ProdConf, Backend>(burst(3, true), 1, true, &dropped);
+  const auto off = prod_polls<ProdConf, Backend>(burst(3, true), 1, false, &kept);
   const bool ok = ref[0] == 3 && on[0] == 0 && off[0] == 3 && kept == link.out;
-  std::printf("bad checksums: reference without a NIC %zu RSTs, product %zu (discard on) / %zu (discard off, the "
+  std::printf("bad checksums%s: reference without a NIC %zu RSTs, product %zu (discard on) / %zu (discard off, the "
               "reference's frames) -> %s\n",
-              ref[0], on[0], off[0], ok ? "as documented" : "UNEXPECTED");
+              backend, ref[0], on[0], off[0], ok ? "as documented" : "UNEXPECTED");
   return ok ? 0 : 1;
 }
 
@@ -359,6 +362,7 @@ int main(int argc, char** argv) {
   const bool gpu = argc > 1 && std::strcmp(argv[1], "gpu") == 0;
   const uint32_t runs = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1;
   int fail = nic_queue_divergence() + rx_batch_divergence() + bad_checksum_divergence();
+  if (gpu) fail += bad_checksum_divergence<GpuBackend>(" (GPU backend)");
   for (g_seed = 0; g_seed < runs; g_seed++) {
     for (int chaos = 0; chaos < 2; chaos++) {
       std::printf("== %s population %u ==\n", chaos ? "chaos" : "peer", g_seed);
@@ -367,7 +371,11 @@ int main(int argc, char** argv) {
       if (ref.out.empty()) return 2;
       fail += coverage(ref);
       fail += compare("twin (sequential oracle backend) vs reference", ref, runProd<OracleBackend>(pop));
-      if (gpu) fail += compare("GpuTcpServer (GPU backend) vs reference", ref, runProd<GpuBackend>(pop));
+      if (gpu) {
+        fail += compare("GpuTcpServer (GPU backend) vs reference", ref, runProd<GpuBackend>(pop));
+        fail += compare("GpuTcpServer (GPU backend, release path: no checksum verification) vs reference", ref,
+                        runProd<GpuBackend>(pop, false));
+      }
     }
   }
   std::printf("%s\n", fail ? "FAIL" : "PASS");

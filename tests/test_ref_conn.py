@@ -55,6 +55,9 @@ def test_gpu_server_equals_reference_server():
     p = subprocess.run([_bin("test_ref_server"), "gpu", "3"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("GpuTcpServer (GPU backend) vs reference") == 6, p.stdout
+    # and with the checksum discard off: the header-only kernel (pn_set_verify(ctx, 0)), the reference's release path
+    assert p.stdout.count("GpuTcpServer (GPU backend, release path: no checksum verification) vs reference") == 6, p.stdout
+    assert "bad checksums (GPU backend):" in p.stdout and p.stdout.count("-> as documented") == 5, p.stdout
     assert "DIFFERENT" not in p.stdout and p.stdout.rstrip().endswith("PASS"), p.stdout
 
 
