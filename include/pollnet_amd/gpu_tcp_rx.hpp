@@ -75,6 +75,10 @@ class GpuTcpRx {
     return nullptr;
   }
   void setDropBadChecksum(bool drop) { drop_bad_ = drop; }
+  // Whether classify verifies the TCP checksum (pn_set_verify; default on).  Off, the records carry no TCP
+  // verdict and the kernel reads only each frame's header lines — the reference's release path; then
+  // setDropBadChecksum(true) has no TCP verdict to act on.
+  const char* setVerify(bool v) { return pn_set_verify(rx_.ctx(), v ? 1 : 0) ? pn_last_error(rx_.ctx()) : nullptr; }
 
   // Control plane: a SYN from `key` was accepted (TcpServer.h:85-96 + TcpConn::onSyn).
   Conn* accept(uint64_t key, uint32_t syn_seq, bool has_ts = false, uint32_t ts_val = 0) {
