@@ -28,6 +28,13 @@
 
 namespace pollnet_amd {
 
+// A record's checksum verdicts: both OK, or the IP one OK where the TCP sum was not computed (the release
+// path, pn_set_verify(ctx, 0): PN_F_TCP_UNCHECKED).
+inline bool checksums_ok(uint16_t flags) {
+  const uint16_t need = PN_F_IP_OK | ((flags & PN_F_TCP_UNCHECKED) ? 0 : PN_F_TCP_OK);
+  return (flags & need) == need;
+}
+
 // Wait for a pn_*_notify launch: spin on its host-visible word (an acquire load, the
 // reference's busy-poll style).  Every 4096 polls the stream is queried; if it has drained (or
 // failed) without the token, that is an error -- the caller synchronises the stream to report it.

@@ -189,7 +189,7 @@ class GpuTcpRx {
       // a frame cut at its slot (or outside the indexed call's class) has no trustworthy
       // payload extent: never delivered, whatever drop_bad_ says
       if (rec.flags & (PN_F_TRUNC | PN_F_BADOFF)) return;
-      if (self->drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
+      if (self->drop_bad_ && !checksums_ok(rec.flags)) return;
       pn_result r = rec;
       if (self->dirty_) { // the table changed earlier in this poll: resolve on the host, fix the record
         uint32_t conn_id = PN_MISS;

@@ -834,7 +834,7 @@ class TcpEngine {
   void onFrame(HH& h, uint64_t key, const pn_result& rec, const uint8_t* eth) {
     if (rec.flags & (PN_F_NOT_TCP | PN_F_TRUNC | PN_F_BADOFF)) return;
     if (!self().accepts(eth)) return; // the NIC filter (Core.h:335-383)
-    if (drop_bad_ && (rec.flags & (PN_F_IP_OK | PN_F_TCP_OK)) != (PN_F_IP_OK | PN_F_TCP_OK)) return;
+    if (drop_bad_ && !checksums_ok(rec.flags)) return;
     pn_result r = rec;
     // the record came from a table snapshot that has changed since (earlier in this batch, or,
     // pipelined, after the launch): probe the live table
