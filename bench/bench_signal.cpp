@@ -57,7 +57,10 @@ int main(int argc, char** argv) {
   uint32_t token = 0;
   bool ok = true;
   std::string out = "{\"bench\": \"completion_word_vs_stream_sync\", \"frames\": \"C2 1514-B\"";
+  // both checksums verified, then the release path (pn_set_verify(ctx, 0): header lines only)
+  for (int verify = 1; verify >= 0 && ok; verify--)
   for (int zc = 0; zc < 2; zc++) {
+    if (pn_set_verify(ctx, verify)) return 4;
     const uint8_t* fr = zc ? h_frames : d_frames;
     pn_result* rec = zc ? h_rec : d_rec;
     auto sync_once = [&](uint32_t n) {
@@ -107,7 +110,7 @@ int main(int argc, char** argv) {
                     legs.empty() ? "" : ", ", n, median(ts), median(tg), same ? "true" : "false");
       legs += buf;
     }
-    out += std::string(", \"") + (zc ? "zero_copy" : "resident") + "\": {" + legs + "}";
+    out += std::string(", \"") + (zc ? "zero_copy" : "resident") + (verify ? "" : "_release_path") + "\": {" + legs + "}";
   }
   out += std::string(", \"ok\": ") + (ok ? "true" : "false") + "}";
   std::printf("%s\n", out.c_str());
