@@ -941,6 +941,20 @@ def run_rank(rank, world, local_rank, args):
             torch.cuda.synchronize()
             if not torch.equal(zres, res.cpu()):
                 out["e2e_zero_copy_pinned_host"]["error"] = "records differ from the device-resident run"
+            # the release path (pn_set_verify(ctx, 0)): only each frame's header line crosses PCIe
+            ctx.set_verify(False)
+            try:
+                rel, rres = e2e_zero_copy(torch, ctx, slots, n)
+            finally:
+                ctx.set_verify(True)
+            F = pa.rx.F
+            exp = res.cpu().numpy().view(pa.RESULT_DTYPE).copy()
+            exp["flags"] = (exp["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
+            exp["tcp_fold"] = 0
+            rel["records_equal_full_path_less_tcp_verdict"] = bool(np.array_equal(rres.numpy().view(pa.RESULT_DTYPE), exp))
+            rel["note"] = ("pn_set_verify(ctx, 0), the reference's release path: pn_classify reads one header line per "
+                           "pinned host slot over PCIe, records to pinned host memory")
+            out["e2e_zero_copy_pinned_host_release_path"] = rel
         except Exception as ex:  # measured extra; never blocks the bench line
             out["e2e_pinned_host"] = {"error": str(ex)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
