@@ -96,6 +96,17 @@ def test_errors_follow_reference_convention():
         t.add(1000, 9)  # MaxConn + MaxTW full
 
 
+def test_set_verify_without_ctx_is_an_error():
+    lib = ctypes.CDLL(pa.LIB_PATH)
+    lib.pn_set_verify.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.pn_set_verify.restype = ctypes.c_int
+    lib.pn_last_error.argtypes = [ctypes.c_void_p]
+    lib.pn_last_error.restype = ctypes.c_char_p
+    assert lib.pn_set_verify(None, 0) == -1  # PN_EINVAL
+    assert b"pn_set_verify" in lib.pn_last_error(None)
+    assert pa.rx.F.TCP_UNCHECKED == 0x8000  # PN_F_TCP_UNCHECKED, the flag the release path sets
+
+
 def test_no_device_open_fails_loudly():
     import torch
 
