@@ -324,7 +324,7 @@ static Run runRef(uint64_t seed) {
 }
 
 template <class Backend>
-static Run runProd(uint64_t seed) {
+static Run runProd(uint64_t seed, bool drop_bad = true) {
   using Cli = GpuTcpClient<ProdCliConf, ScriptServer, Backend>;
   auto cli = std::make_unique<Cli>();
   Run r;
@@ -334,6 +334,7 @@ static Run runProd(uint64_t seed) {
     std::printf("init: %s\n", cli->getLastError());
     return r;
   }
+  cli->setDropBadChecksum(drop_bad); // off: the GPU backend classifies from the header lines only (pn_set_verify)
   CliHandler<typename Cli::Conn> h{&r.log};
   for (int t = 1; t <= kPolls; t++) {
     cli->poll(h, kT0 + ((int64_t)t << 20));
@@ -382,6 +383,8 @@ int main(int argc, char** argv) {
     if (gpu) {
       std::snprintf(what, sizeof what, "script %u: GpuTcpClient (GPU) vs reference", k);
       fail += compare(what, ref, runProd<GpuBackend>(seed));
+      std::snprintf(what, sizeof what, "script %u: GpuTcpClient (GPU, release path) vs reference", k);
+      fail += compare(what, ref, runProd<GpuBackend>(seed, false));
     }
   }
   std::printf("exercised (reference side): %zu connections, %zu connect failures, %zu client RSTs, %zu data frames\n",

@@ -77,4 +77,5 @@ def test_gpu_client_equals_reference_client():
     p = subprocess.run([_bin("test_ref_client"), "gpu", "8"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("GpuTcpClient (GPU) vs reference") == 8 and "DIFFERENT" not in p.stdout, p.stdout
+    assert p.stdout.count("GpuTcpClient (GPU, release path) vs reference") == 8, p.stdout
     assert p.stdout.rstrip().endswith("PASS"), p.stdout
