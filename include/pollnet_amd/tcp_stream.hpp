@@ -31,6 +31,12 @@
 
 #include "gpu_rx.hpp"
 
+// GpuTcpStreams::poll prefetches this many matched frames ahead of the one it reassembles (4 measured best of
+// 0/1/2/4/8, profiles/r04/sniffer/prefetch_pf*.jsonl); overridable for A/B builds.
+#ifndef PN_STREAM_PREFETCH_AHEAD
+#define PN_STREAM_PREFETCH_AHEAD 4
+#endif
+
 namespace pollnet_amd {
 
 template <bool WaitForResend = true, uint32_t BUFSIZE = (1u << 20)>
@@ -280,9 +286,6 @@ class GpuTcpStreams {
   hipStream_t stream_ = nullptr;
   GpuRx::Mode mode_ = GpuRx::Mode::ZeroCopy;
   bool first_only_ = false;
-#ifndef PN_STREAM_PREFETCH_AHEAD
-#define PN_STREAM_PREFETCH_AHEAD 4
-#endif
   static constexpr uint32_t kPrefetchAhead = PN_STREAM_PREFETCH_AHEAD;
   void* d_frames_[2] = {nullptr, nullptr};
   uint32_t* d_ids_[2] = {nullptr, nullptr};
