@@ -157,5 +157,44 @@ int main(int argc, char** argv) {
                 (unsigned long long)st[k].packets, (unsigned long long)st[k].taken, (unsigned long long)st[k].calls,
                 (unsigned long long)st[k].bytes);
   std::printf("%d/%d streams identical to the reference TcpStream\n", 4 * n - bad, 4 * n);
-  return bad ? 1 : 0;
+
+  // GpuTcpStreams::filterPacket (the host filter for a frame's later streams) vs the reference's filterPacket:
+  // random headers drawn from small pools (so filters hit), non-IPv4 / non-TCP frames, wildcard filters
+  auto ref_filter = (int (*)(const uint8_t*, uint32_t, const char*, uint16_t, const char*, uint16_t))dlsym(
+      h, "ref_filter_packet");
+  if (!ref_filter) {
+    std::printf("missing ref_filter_packet\n");
+    return 1;
+  }
+  std::mt19937_64 rng(0xF117E4);
+  const uint32_t hosts[4] = {0x0a000001, 0x0a000002, 0xc0a80105, 0x7f000001};
+  const uint16_t ports[4] = {1234, 40000, 80, 5000};
+  uint32_t fdiff = 0, fpass = 0, fcases = 0;
+  uint8_t fr[64];
+  for (int i = 0; i < 200000; i++) {
+    for (auto& b : fr) b = (uint8_t)rng();
+    fr[12] = 0x08, fr[13] = rng() % 8 ? 0x00 : 0x06;
+    fr[23] = rng() % 8 ? 6 : 17;
+    const uint32_t sip = hosts[rng() % 4], dip = hosts[rng() % 4];
+    const uint16_t sp = ports[rng() % 4], dp = ports[rng() % 4];
+    for (int k = 0; k < 4; k++) fr[26 + k] = (uint8_t)(sip >> (24 - 8 * k)), fr[30 + k] = (uint8_t)(dip >> (24 - 8 * k));
+    fr[34] = sp >> 8, fr[35] = sp & 255, fr[36] = dp >> 8, fr[37] = dp & 255;
+    const uint32_t fs = rng() % 2 ? hosts[rng() % 4] : 0, fd = rng() % 2 ? hosts[rng() % 4] : 0;
+    const uint16_t fsp = rng() % 2 ? ports[rng() % 4] : 0, fdp = rng() % 2 ? ports[rng() % 4] : 0;
+    char s_ip[32], d_ip[32];
+    std::snprintf(s_ip, sizeof s_ip, "%u.%u.%u.%u", fs >> 24, (fs >> 16) & 255, (fs >> 8) & 255, fs & 255);
+    std::snprintf(d_ip, sizeof d_ip, "%u.%u.%u.%u", fd >> 24, (fd >> 16) & 255, (fd >> 8) & 255, fd & 255);
+    pn_stream_filter f{};
+    inet_pton(AF_INET, s_ip, &f.src_ip);
+    inet_pton(AF_INET, d_ip, &f.dst_ip);
+    f.src_port = htons(fsp);
+    f.dst_port = htons(fdp);
+    const bool want = ref_filter(fr, 64, s_ip, fsp, d_ip, fdp) != 0;
+    const bool got = pollnet_amd::GpuTcpStreams<>::filterPacket(f, fr);
+    fdiff += want != got;
+    fpass += want;
+    fcases++;
+  }
+  std::printf("filterPacket: %u frames, %u pass, %u differ from the reference\n", fcases, fpass, fdiff);
+  return bad || fdiff ? 1 : 0;
 }

@@ -30,6 +30,8 @@ def test_reassembler_vs_reference_tcpstream():
     p = subprocess.run([_bin("test_tcp_stream"), REF, "200"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert "800/800 streams identical" in p.stdout, p.stdout
+    # GpuTcpStreams' host filter (later streams of a frame) equals the reference's filterPacket
+    assert "filterPacket: 200000 frames" in p.stdout and " 0 differ from the reference" in p.stdout, p.stdout
 
 
 @pytest.mark.gpu
