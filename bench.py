@@ -642,7 +642,9 @@ def secondary_release_path(torch, pa, ctx, frames_b, res, n, steps, stream):
     finally:
         ctx.set_verify(True)
     algo = n * (64 + 16)
+    pmc = load_pmc(f"c2_release_path_n{n}")
     return {"kernel_ms": round(kern, 5), "mframes_per_s": round(n / (kern * 1e-3) / 1e6, 1),
+            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
             "algorithmic_bytes_per_launch": algo, "achieved_gbs": round(algo / (kern * 1e-3) / 1e9, 1),
             "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "line_traffic_gbs": round(n * (128 + 16) / (kern * 1e-3) / 1e9, 1),
