@@ -172,3 +172,20 @@ def test_verify_switches_back(torch_cuda, ctx):
     same(classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, n, t), release(exp))
     ctx.set_verify(True)
     same(classify(torch_cuda, ctx, s, STRIDE, FRAME_OFF, n, t), exp)
+
+
+def test_zero_copy_pinned_host(torch_cuda, ctx):
+    """Frames and records in pinned host memory (the kernel reads the header lines over PCIe)."""
+    torch = torch_cuda
+    p = pa.rx.GenParams.for_config(5)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    ctx.set_conn_table(t)
+    n = 5000
+    s = pa.gen_frames(p, n)
+    exp = release(orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, t.max_conn_cnt, threads=8))
+    host = torch.from_numpy(s.reshape(-1)).pin_memory()
+    res = torch.zeros(n * 16, dtype=torch.uint8).pin_memory()
+    ctx.classify(host, STRIDE, FRAME_OFF, n, res, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    same(res.numpy().view(pa.RESULT_DTYPE), exp)
