@@ -389,7 +389,7 @@ int pn_calib_slot_read_var(pn_ctx* ctx, const void* src_dev, uint32_t n_slots, u
 int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                              const pn_stream_filter* filters, uint32_t n_filters, uint32_t* stream_ids, void* stream,
                              int variant) {
-  if (n == 0 || variant < 0 || variant > 38) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
+  if (n == 0 || variant < 0 || variant > 40) return set_err(ctx, PN_EINVAL, "match variant: bad arguments");
   MatchArgs a;
   int rc = match_args(ctx, frames, slot_stride, frame_off, n, filters, n_filters, stream_ids, a);
   if (rc) return rc;
@@ -435,6 +435,8 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
     case 36: launch_match_mask<1, kMatchLoadAux, 128, 1>(a, frame_off, s); break; // production, nt id stores
     case 37: launch_match_mask<1, kMatchLoadAux, 256, 1>(a, frame_off, s); break; // production, masks loaded first
     case 38: launch_match_mask<1, kMatchLoadAux, 512, 1>(a, frame_off, s); break; // timing only: stores into 4 KiB
+    case 39: launch_match_mask<1, kMatchLoadAux, 1024, 1>(a, frame_off, s); break; // no tile: quad DPP exchange
+    case 40: launch_match_mask<1, kMatchLoadAux, 1024 | 2, 1>(a, frame_off, s); break; // 39's loads + exchange alone
     default: launch_match<0>(a, frame_off, s);
   }
   hipError_t e = hipGetLastError();

@@ -150,6 +150,16 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
   }
 }
 
+// lane j of each quad's value, to all four lanes of the quad (DPP quad_perm [j, j, j, j]); j folds to a constant
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v, int j) {
+  switch (j) {
+    case 0: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x00, 0xF, 0xF, false);
+    case 1: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x55, 0xF, 0xF, false);
+    case 2: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xAA, 0xF, 0xF, false);
+    default: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xFF, 0xF, 0xF, false);
+  }
+}
+
 // Round 4 form: the same cooperative 64-B loads (4 lanes per frame, one line request per frame), then
 //   - each wave orders its own LDS tile round trip by itself: the DS instructions of one wave execute
 //     in order, so a wave reads its tile right after writing it, without waiting at a workgroup barrier
@@ -165,7 +175,7 @@ __global__ __launch_bounds__(256) void match_streams_kernel(MatchArgs a) {
 // OPT & 32 / 64 (tuning, timing only): no filter compare / no id store.  OPT & 128 (tuning): nt id stores.
 // OPT & 256: the last filter block's masks loaded right after the frame loads, not at the compare (below).
 // OPT & 512 (timing only): the id stores all land in the first 4 KiB of the output (store issue without the
-// write volume).
+// write volume).  OPT & 1024 (tuning): no LDS tile, the header words exchanged within each quad by DPP.
 template <int MIS, int G, int LAUX, int OPT = 0, int WPW = 4>
 __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs a) {
   constexpr uint32_t kWaveFrames = 64 * G;
@@ -210,24 +220,46 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
   }
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t r = 16 * i + (lane >> 2);
-      if (!(OPT & 8) || need) wt[r * 4 + (c ^ (r & 3))] = v[g][i];
-    }
-    if constexpr ((OPT & 4) != 0) {
-      if (g == 0) __builtin_amdgcn_s_setprio(2);
-    }
     Win<16> h;
+    uint32_t f;
+    if constexpr ((OPT & 1024) != 0) {
+      // tuning: no tile.  Lane 4q + c takes frame 16c + q; each header word k of it is in lane 4q + k / 4 of its
+      // quad, component k % 4 of load c: four quad broadcasts (DPP) of that component, one per load, and the
+      // lane keeps the one of its own load
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const u32x4 x = wt[lane * 4 + (q ^ (lane & 3))];
-      h.d[4 * q + 0] = x.x;
-      h.d[4 * q + 1] = x.y;
-      h.d[4 * q + 2] = x.z;
-      h.d[4 * q + 3] = x.w;
+      for (int k = 0; k < 16; ++k) h.d[k] = 0;
+      constexpr int kLo = (kPre + MIS - 2) / 4, kHi = (kPre + MIS + 23) / 4;
+#pragma unroll
+      for (int k = kLo; k <= kHi; ++k) {
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const u32x4 vv = v[g][i];
+          const uint32_t comp = (k & 3) == 0 ? vv.x : (k & 3) == 1 ? vv.y : (k & 3) == 2 ? vv.z : vv.w;
+          x[i] = quad_bcast(comp, k >> 2);
+        }
+        h.d[k] = c == 0 ? x[0] : c == 1 ? x[1] : c == 2 ? x[2] : x[3];
+      }
+      f = f0 + 64 * g + 16 * c + (lane >> 2);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t r = 16 * i + (lane >> 2);
+        if (!(OPT & 8) || need) wt[r * 4 + (c ^ (r & 3))] = v[g][i];
+      }
+      if constexpr ((OPT & 4) != 0) {
+        if (g == 0) __builtin_amdgcn_s_setprio(2);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x4 x = wt[lane * 4 + (q ^ (lane & 3))];
+        h.d[4 * q + 0] = x.x;
+        h.d[4 * q + 1] = x.y;
+        h.d[4 * q + 2] = x.z;
+        h.d[4 * q + 3] = x.w;
+      }
+      f = f0 + 64 * g + lane;
     }
-    const uint32_t f = f0 + 64 * g + lane;
     if constexpr (OPT & 2) { // timing only
       uint32_t x = 0;
 #pragma unroll

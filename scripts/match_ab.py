@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
-TIMING_ONLY = {5, 15, 16, 17, 18, 19, 21, 23, 25, 27, 29, 34, 35, 38}
+TIMING_ONLY = {5, 15, 16, 17, 18, 19, 21, 23, 25, 27, 29, 34, 35, 38, 40}
 
 
 def main():

@@ -99,7 +99,7 @@ def test_match_streams_layouts(frame_off, stride, n):
 # The round-4 kernel forms (match_streams_mask_kernel, tuning variants 10-14: wave-ordered tile, mask
 # compare in blocks of 8 filters, 1-4 groups of 64 frames per wave, 1 or 4 waves per workgroup) on
 # the same layouts and 0, 1, 7, 8, 9 and 64 filters (padded blocks), against numpy.
-@pytest.mark.parametrize("variant", [10, 11, 12, 13, 14, 20, 22, 24, 26, 28, 30, 31, 32, 33, 36, 37])
+@pytest.mark.parametrize("variant", [10, 11, 12, 13, 14, 20, 22, 24, 26, 28, 30, 31, 32, 33, 36, 37, 39])
 @pytest.mark.parametrize("frame_off,stride,n", [(2, 112, 1), (4, 2048, 700), (14, 128, 257), (16, 65536, 200),
                                                 (26, 2048, 4097)])
 def test_match_streams_mask_variants(variant, frame_off, stride, n):
