@@ -636,7 +636,7 @@ def secondary_release_path(torch, pa, ctx, frames_b, res, n, steps, stream):
         got = res.cpu().numpy().view(pa.RESULT_DTYPE)
         exp = full.copy()
         exp["flags"] = (exp["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
-        exp["tcp_fold"] = 0
+        exp["tcp_fold"] = 0xFFFF
         ok = bool(np.array_equal(got, exp))
         kern = time_launches(torch, lambda d: ctx.classify(d, STRIDE, FRAME_OFF, n, res, stream), frames_b, steps, stream)
     finally:
@@ -952,7 +952,7 @@ def run_rank(rank, world, local_rank, args):
             F = pa.rx.F
             exp = res.cpu().numpy().view(pa.RESULT_DTYPE).copy()
             exp["flags"] = (exp["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
-            exp["tcp_fold"] = 0
+            exp["tcp_fold"] = 0xFFFF
             rel["records_equal_full_path_less_tcp_verdict"] = bool(np.array_equal(rres.numpy().view(pa.RESULT_DTYPE), exp))
             rel["note"] = ("pn_set_verify(ctx, 0), the reference's release path: pn_classify reads one header line per "
                            "pinned host slot over PCIe, records to pinned host memory")

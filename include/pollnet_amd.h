@@ -58,7 +58,8 @@ typedef struct pn_result {
   int16_t payload_len;  /* ip + min(tot_len,1500) - (tcp + doff*4)        (TcpConn.h:472, signed) */
   uint16_t flags;       /* PN_F_* below */
   uint16_t tcp_fold;    /* CSum::fold() of the reference TCP sum (Core.h:459-466); 0 <=> valid.
-                           0xFFFF when PN_F_TRUNC (segment runs past the slot). */
+                           0xFFFF = no fold computed: PN_F_TRUNC (segment runs past the slot) or
+                           PN_F_TCP_UNCHECKED (release path).  A real fold is never 0xFFFF (~r, r >= 1). */
 } pn_result;
 
 /* flags */
@@ -82,7 +83,7 @@ typedef struct pn_result {
                                    frame was not read and the record is {PN_MISS, 0, 0, 0, BADOFF, 0} */
 #define PN_F_TCP_UNCHECKED 0x8000u /* pn_set_verify(ctx, 0): the reference's release path, which verifies no
                                    checksum (Core::checksum is debug-only, Core.h:448-478): only the frame's
-                                   header lines were read; TCP_OK / RFC_TCP_OK never set, tcp_fold = 0 */
+                                   header lines were read; TCP_OK / RFC_TCP_OK never set, tcp_fold = 0xFFFF */
 
 /* ---- 16-byte conn-table entry, identical layout to ConnHashEntry (Core.h:178-182) ---- */
 typedef struct pn_conn_entry {

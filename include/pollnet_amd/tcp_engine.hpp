@@ -376,9 +376,10 @@ class GpuBackend {
   uint8_t* rxSlots(uint32_t half = 0) { return rx_ring_ + (size_t)half * rx_cap_ * kStride; }
   // Whether classify verifies the TCP checksum (pn_set_verify).  Off, the kernel reads only each frame's
   // header lines over PCIe instead of the whole frame: the engine turns it off with its checksum discard.
-  void setVerify(bool v) {
+  const char* setVerify(bool v) {
     verify_ = v;
-    if (rx_.ctx()) (void)pn_set_verify(rx_.ctx(), v ? 1 : 0);
+    if (rx_.ctx() && pn_set_verify(rx_.ctx(), v ? 1 : 0)) return pn_last_error(rx_.ctx());
+    return nullptr;
   }
   // Pipelined RX: launch classifies the first n slots of one half against the snapshot on the
   // device (syncTable); collect waits for it and calls f(key, rec, eth) in ring order.
@@ -546,17 +547,24 @@ class TcpEngine {
     void sendFin() { eng_->sendFin(*this); }
     void setUserTimer(uint32_t timer_id, uint32_t duration_ms) { eng_->setUserTimer(*this, timer_id, duration_ms); }
 #ifdef EFVITCP_DEBUG
-    // TcpConn::dump / shortDump (TcpConn.h:107-128, debug builds): the connection's state on stdout, the
-    // congestion fields as pollnet's wrappers leave them (no congestion window)
+    // TcpConn::dump / shortDump (TcpConn.h:107-128, debug builds): the reference's fields in the reference's
+    // order.  cwnd, ssthresh and cong_av print 0: with pollnet's wrappers (CongestionControlAlgo = 0,
+    // EfviTcp.h:48, 206) the reference never writes them (TcpConn.h:418-421, 583-664, 788-791, 816-824), so
+    // its zero-initialised server prints 0.  ack_seq / ack_end_seq are recv_buf_seq plus the first / last
+    // reassembly extent's end (TcpConn.h:115-116), from the receive half.
     void dump(const char* note) const {
-      std::printf("%s: conn_id: %u, key: %llu, established: %d, fin_sent: %d, fin_received: %d, fast_re: %d, "
-                  "dup_ack_cnt: %u, send_una: %u, send_next: %u, data_next: %u, data_next_size: %u, "
-                  "send_next_seq: %u, both_wnd_seq: %u, rto: %u, srtt: %u, rttvar: %u, recent_ts: %u, in_recover: %d, "
-                  "recover: %u, retries: %u, src port: %u, dst port: %u\n",
-                  note, id_, (unsigned long long)key_, established_, fin_sent_, fin_received_, fast_re_, dup_ack_cnt_,
-                  send_una_, send_next_, data_next_, data_next_size_, segs_[send_next_ & (kSendBufCnt - 1)].seq,
-                  send_wnd_seq_, rto_, srtt_, rttvar_, rx_.recentTs(), in_recover_, recover_, retries_,
-                  ntohs(local_port_), ntohs(peer_port_));
+      const uint32_t cwnd = 0, ssthresh = 0, cong_av = 0;
+      const uint32_t ack_seq = rx_.recvBufSeq() + rx_.segs()[0].second;
+      const uint32_t ack_end_seq = rx_.recvBufSeq() + rx_.segs()[rx_.segCount() ? rx_.segCount() - 1 : 0].second;
+      std::printf("%s: conn_id: %u, key: %llu, established: %d, fin_sent: %d, fin_received: %d, cwnd: %u, "
+                  "ssthresh: %u, cong_av: %u, fast_re: %d, dup_ack_cnt: %u, send_una: %u, send_next: %u, "
+                  "data_next: %u, data_next_size: %u, ack_seq: %u, ack_end_seq: %u, send_next_seq: %u, "
+                  "both_wnd_seq: %u, rto: %u, srtt: %u, rttvar: %u, recent_ts: %u, in_recover: %d, recover: %u, "
+                  "retries: %u, src port: %u, dst port: %u\n",
+                  note, id_, (unsigned long long)key_, established_, fin_sent_, fin_received_, cwnd, ssthresh, cong_av,
+                  fast_re_, dup_ack_cnt_, send_una_, send_next_, data_next_, data_next_size_, ack_seq, ack_end_seq,
+                  segs_[send_next_ & (kSendBufCnt - 1)].seq, send_wnd_seq_, rto_, srtt_, rttvar_, rx_.recentTs(),
+                  in_recover_, recover_, retries_, ntohs(local_port_), ntohs(peer_port_));
     }
     void shortDump(const char* note = "") const {
       std::printf("%s, src port: %u, dst port: %u\n", note, ntohs(local_port_), ntohs(peer_port_));
@@ -604,11 +612,20 @@ class TcpEngine {
   // Drop checksum-failed frames before they touch any state (what the NIC's RX checksum
   // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.  Off, the frames
   // are trusted as the reference's release build trusts them (Core::checksum is debug-only,
-  // Core.h:448-478), and the GPU backend stops verifying the TCP checksum: its classify reads
-  // only each frame's header lines (pn_set_verify).
-  void setDropBadChecksum(bool drop) {
+  // Core.h:448-478), and the GPU backend also stops verifying the TCP checksum: its classify
+  // reads only each frame's header lines (pn_set_verify), so the records a hook sees carry no
+  // TCP verdict (PN_F_TCP_UNCHECKED set, PN_F_TCP_OK / PN_F_RFC_TCP_OK clear, tcp_fold 0xFFFF).
+  // To keep the verdict in the records with the discard off, call setVerify(true) after this.
+  // Returns the backend's error (pn_set_verify), nullptr on success.
+  const char* setDropBadChecksum(bool drop) {
     drop_bad_ = drop;
-    be_.setVerify(drop);
+    return be_.setVerify(drop);
+  }
+  // Whether the backend computes the TCP verdict (pn_set_verify), on its own.  The discard needs it:
+  // setVerify(false) while setDropBadChecksum(true) is in force is refused.
+  const char* setVerify(bool verify) {
+    if (!verify && drop_bad_) return "setVerify(false): the checksum discard (setDropBadChecksum(true)) needs the TCP verdict";
+    return be_.setVerify(verify);
   }
   const ConnTable& table() const { return table_; }
   uint32_t nowTs() const { return wheel_.now(); }

@@ -264,7 +264,7 @@ static void release_frame(const uint8_t* eth, const pn_conn_entry* tbl, uint32_t
   out->payload_off = (uint16_t)data_off;
   out->payload_len = (int16_t)(14 + (int)(tot_len < 1500 ? tot_len : 1500) - data_off);
   out->flags = (uint16_t)flags;
-  out->tcp_fold = 0;
+  out->tcp_fold = 0xFFFF; /* not computed (the GPU release path's sentinel) */
 }
 
 typedef struct job {

@@ -31,6 +31,16 @@ __device__ __forceinline__ uint32_t dpp(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP, 0xf, 0xf, false);
 }
 
+// Between a wave's writes to its own LDS tile and other lanes' reads of them (and back): a
+// wavefront-scope release, the wave barrier, a wavefront-scope acquire.  LDS ops of one wave
+// execute in order on the hardware, so this costs at most an lgkmcnt wait; what it buys is the
+// ordering under the memory model, so the compiler may not move a read above the write it needs.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // A buffer-load offset past every descriptor's range (at most a few MiB here): the load returns zeros and
 // fetches nothing.  Used instead of a branch around a load, so that loads stay in flight together.
 constexpr uint32_t kNoFetch = 0x80000000u;

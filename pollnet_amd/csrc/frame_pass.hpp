@@ -123,6 +123,7 @@ __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t r
     static_assert(MIS + 64 <= kWinBytes, "window must cover ip .. ip+64");
     u32x4* tile = coop_tile();
     const uint32_t blk = coop_block(ipa_off);
+    wave_lds_sync(); // a previous window's tile reads (a grouped kernel's last group) before these writes
     // All 8 loads in flight before the first LDS write: a part that is not needed gets an offset past
     // the descriptor's range (returns zeros, fetches nothing) instead of a branch around its load --
     // with the branches the compiler waited for each load before issuing the next (8 round trips).
@@ -149,6 +150,7 @@ __device__ __forceinline__ uint32_t load_window_strided(__amdgpu_buffer_rsrc_t r
       const uint32_t r = 8 * i + (lane >> 3), part = lane & 7;
       tile[r * 8 + (part ^ (r & 7))] = v[i];
     }
+    wave_lds_sync(); // each lane reads the rows other lanes wrote (the tile is this wave's own)
     constexpr uint32_t p0 = 1; // the window starts at the block's second chunk
 #pragma unroll
     for (int c = 0; c < kWinChunks; ++c) {

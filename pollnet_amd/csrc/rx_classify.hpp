@@ -290,8 +290,7 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   uint32_t flags = st.flags;
   uint32_t tcp_fold = 0xffff;
   if constexpr ((ABL & kHeaderOnly) != 0) { // the release path: no TCP sum (the IP header is in the window)
-    flags |= PN_F_TCP_UNCHECKED;
-    tcp_fold = 0;
+    flags |= PN_F_TCP_UNCHECKED; // tcp_fold stays 0xFFFF: no fold was computed (never a fold value)
     if (!st.trunc && st.ihl >= 5 && 4 * st.ihl <= st.tot_len && csum_fold(st.s_ip20 + st.s_opt) == 0)
       flags |= PN_F_RFC_IP_OK;
   } else if (!st.trunc) {

@@ -247,6 +247,10 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
         const uint32_t r = 16 * i + (lane >> 2);
         if (!(OPT & 8) || need) wt[r * 4 + (c ^ (r & 3))] = v[g][i];
       }
+      // other lanes of this wave read what these lanes wrote: order the tile writes before the reads
+      // for the compiler and the memory model (the tile is the wave's own, so a wavefront-scope
+      // release/acquire pair around a wave barrier is the whole synchronisation)
+      wave_lds_sync();
       if constexpr ((OPT & 4) != 0) {
         if (g == 0) __builtin_amdgcn_s_setprio(2);
       }
@@ -258,6 +262,7 @@ __global__ __launch_bounds__(64 * WPW) void match_streams_mask_kernel(MatchArgs 
         h.d[4 * q + 2] = x.z;
         h.d[4 * q + 3] = x.w;
       }
+      if constexpr (G > 1) wave_lds_sync(); // group g's reads before group g + 1's writes
       f = f0 + 64 * g + lane;
     }
     if constexpr (OPT & 2) { // timing only

@@ -42,7 +42,7 @@ struct ScriptLink {
 struct OracleBackend {
   static constexpr bool kSnapshot = false;
   static constexpr uint32_t kStride = 2048, kFrameOff = 2;
-  void setVerify(bool) {} // the oracle always computes both verdicts; the engine reads them only when dropping
+  const char* setVerify(bool) { return nullptr; } // the oracle always computes both verdicts; the engine reads them only when dropping
   std::vector<uint8_t> rx, tx;
   std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
   uint32_t cap = 0;

@@ -81,3 +81,26 @@ def test_generator_is_compiler_independent(tmp_path):
     for cfg in (3, 5):
         a, b = (_gen(so, cfg, 1 << 18, first=1 << 20) for so in libs.values())
         assert np.array_equal(a, b), cfg
+
+
+def test_debug_dump_compiles(tmp_path):
+    """Conn::dump / shortDump exist only under EFVITCP_DEBUG (as TcpConn.h:107-128): the debug build of a server
+    and a client that call them compiles (hipcc, host and gfx950 device passes, syntax only)."""
+    tu = tmp_path / "dump.cpp"
+    tu.write_text("""#define EFVITCP_DEBUG
+#include "pollnet_amd/tcp_server.hpp"
+#include "pollnet_amd/tcp_client.hpp"
+struct C {
+  static const uint32_t RecvBufSize = 4096;
+  static const uint32_t MaxConns = 4;
+  static const uint32_t SendTimeoutSec = 0;
+  static const uint32_t RecvTimeoutSec = 0;
+  static const uint32_t ConnSendBufCnt = 8;
+  struct UserData {};
+};
+void f(const pollnet_amd::GpuTcpServer<C>::Conn& c) { c.dump("x"); c.shortDump("y"); }
+void g(const pollnet_amd::GpuTcpClient<C>::Conn& c) { c.dump("x"); c.shortDump(); }
+""")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
+                        "-fsyntax-only", "-x", "hip", str(tu)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]

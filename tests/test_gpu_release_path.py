@@ -1,6 +1,6 @@
 """GPU: pn_set_verify(ctx, 0) — the reference's release path (Core::checksum is debug-only, Core.h:448-478), so
 the kernel reads only each frame's header lines.  Every record must equal the oracle's full record with its TCP
-verdict taken out: TCP_OK and RFC_TCP_OK cleared, PN_F_TCP_UNCHECKED set, tcp_fold 0; every other field (conn id,
+verdict taken out: TCP_OK and RFC_TCP_OK cleared, PN_F_TCP_UNCHECKED set, tcp_fold 0xFFFF (no fold computed); every other field (conn id,
 seq, payload offset/length, the IP verdicts, TRUNC, NOT_TCP, IHL_NE_5, the flags) bit-exact.  Strided (all 8
 alignment classes, strides 112 B..64 KiB, every frames-per-wave split), notify, indexed/packed, random bytes."""
 import numpy as np
@@ -35,7 +35,7 @@ def release(exp):
     """The oracle's full records as the release path reports them."""
     r = exp.copy()
     r["flags"] = (r["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
-    r["tcp_fold"] = 0
+    r["tcp_fold"] = 0xFFFF
     return r
 
 

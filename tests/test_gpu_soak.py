@@ -18,7 +18,7 @@ F = pa.rx.F
 def release(exp):
     r = exp.copy()
     r["flags"] = (r["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
-    r["tcp_fold"] = 0
+    r["tcp_fold"] = 0xFFFF
     return r
 
 
