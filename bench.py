@@ -112,11 +112,18 @@ def cpu_threads():
 
 def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
     """The reference's own per-frame code, compiled from /root/reference into oracle/_ref/libref_core.so
-    (kind "reference": Core::checksum + connHashKey + findConnEntry + the TIME_WAIT test + TcpConn::onPack's
-    head, oracle/ref_core.cc ref_bench_batch), on this host's cores; the oracle's C port of the same path
-    ("port", oracle/pn_oracle.c orc_refsum_batch) and the release path (no checksum) beside it.  Falls back
-    to the port as the headline when libref_core.so is absent.  The reference's digest over the sample is
-    compared with the same digest of the GPU's records for those frames."""
+    (kind "reference"), on this host's cores:
+      - the headline: the debug build's work per frame (Core::checksum + connHashKey + findConnEntry + the
+        TIME_WAIT test + TcpConn::onPack's head, oracle/ref_core.cc ref_bench_batch), beside the GPU's
+        verified classify;
+      - release_path: the release build's (the same without Core::checksum, ref_release_batch), beside the
+        GPU's pn_set_verify(ctx, 0) figures;
+    each at the fastest thread count of its own sweep, and one thread.  Every figure is the median of 5
+    timed passes with their min / max; a headline that disagrees with its own sweep point at the same
+    thread count by more than 15 % is re-measured (both) instead of published as is.  The oracle's C port
+    of the same paths ("port", oracle/pn_oracle.c) is timed beside it and is the headline only when
+    libref_core.so is absent.  The reference's digests over the sample are compared with the same digests
+    of the GPU's records for those frames."""
     import pollnet_amd as pa
     from oracle import pyoracle as orc
 
@@ -136,7 +143,10 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
     def reference(th):
         ref.batch(slots, STRIDE, FRAME_OFF, sample, th)
 
-    def rate(fn, th, secs):
+    def reference_release(th):
+        ref.release(slots, STRIDE, FRAME_OFF, sample, th)
+
+    def one_pass(fn, th, secs):
         t0 = time.perf_counter()
         passes = 0
         while True:
@@ -146,50 +156,79 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
             if el >= secs:
                 return passes * sample / el, passes * wire * 8 / el / 1e9, passes
 
-    head = reference if ref is not None else port
+    def measure(fn, th, secs, reps=5):
+        """median of `reps` timed passes of >= secs each (Gbit/s), with min / max"""
+        runs = [one_pass(fn, th, secs) for _ in range(reps)]
+        gb = sorted(r[1] for r in runs)
+        fr = sorted(r[0] for r in runs)
+        return {"value": round(statistics.median(gb), 2), "unit": "Gbit/s",
+                "mframes_per_s": round(statistics.median(fr) / 1e6, 3), "cores": th,
+                "min": round(gb[0], 2), "max": round(gb[-1], 2), "reps": reps, "passes": sum(r[2] for r in runs)}
+
+    counts = sorted({c for c in (8, 16, 32, 64, threads) if c <= threads})
+
+    def swept(fn, sweep_s, head_s):
+        # the box's share of a large host can be smaller than its affinity mask: probe a few thread counts up to
+        # the available cores and measure at the fastest (stated in the line)
+        sweep = {t: measure(fn, t, sweep_s, reps=3)["value"] for t in counts}
+        best = max(sweep, key=sweep.get)
+        head = measure(fn, best, head_s)
+        remeasured = False
+        if abs(head["value"] - sweep[best]) > 0.15 * max(head["value"], sweep[best]):
+            remeasured = True
+            sweep[best] = measure(fn, best, sweep_s, reps=3)["value"]
+            head = measure(fn, best, head_s)
+        head["thread_sweep_gbit_per_s"] = sweep
+        head["sweep_point_at_cores"] = sweep[best]
+        head["consistent_with_sweep"] = abs(head["value"] - sweep[best]) <= 0.15 * max(head["value"], sweep[best])
+        head["remeasured"] = remeasured
+        return head
+
+    head_fn = reference if ref is not None else port
+    kind = "reference" if ref is not None else "port"
     c1 = c1_socket_loopback()
-    # the box's share of a large host can be smaller than its affinity mask: probe a few thread
-    # counts up to the available cores and measure at the fastest (stated in the line)
-    sweep = {}
-    for t in sorted({c for c in (8, 16, 32, 64, threads) if c <= threads}):
-        sweep[t] = round(rate(head, t, budget_s * 0.05)[1], 1)
-    best = max(sweep, key=sweep.get)
-    fr_mt, gb_mt, p_mt = rate(head, best, budget_s * 0.3)
-    fr_1, gb_1, _ = rate(head, 1, budget_s * 0.2)
-    fr_rel, gb_rel, _ = rate(lambda th: port(th, True), 1, budget_s * 0.1)
+    head = swept(head_fn, budget_s * 0.02, budget_s * 0.06)
+    single = measure(head_fn, 1, budget_s * 0.025)
+    rel_fn = reference_release if ref is not None else (lambda th: port(th, True))
+    rel = swept(rel_fn, budget_s * 0.01, budget_s * 0.04)
+    rel_1 = measure(rel_fn, 1, budget_s * 0.02)
     code = ("the reference's own Core.h / TcpConn.h code (oracle/ref_core.cc ref_bench_batch, compiled from "
             "/root/reference by oracle/ref.mk, g++ -O3 -march=x86-64-v3)" if ref is not None else
             "'ref parse + checksum' port (oracle/pn_oracle.c orc_refsum_batch, -O3 -march=x86-64-v3)")
-    out = {
-        "value": round(gb_mt, 2),
-        "unit": "Gbit/s",
-        "cores": best,
-        "kind": "reference" if ref is not None else "port",
+    out = dict(head)
+    out.update({
+        "kind": kind,
         "sample": f"Core::checksum + pollNet's key/probe/TIME_WAIT test + onPack's payload head per frame, {code}, "
-                  f"over {sample} frames of the same workload, {p_mt} passes; contiguous index shards over {best} "
-                  f"threads, the fastest of a sweep up to this process's {cpu_threads()} available cores (CPU "
-                  f"affinity {len(os.sched_getaffinity(0))}, cgroup CPU quota {cgroup_cpu_quota()}, machine "
-                  f"{os.cpu_count()})",
-        "mframes_per_s": round(fr_mt / 1e6, 3),
-        "thread_sweep_gbit_per_s": sweep,
-        "single_thread": {"value": round(gb_1, 2), "unit": "Gbit/s", "mframes_per_s": round(fr_1 / 1e6, 3),
-                          "cores": 1},
-        "release_path_no_checksum_1t": {"value": round(gb_rel, 2), "unit": "Gbit/s",
-                                        "mframes_per_s": round(fr_rel / 1e6, 3), "cores": 1, "kind": "port"},
+                  f"over {sample} frames of the same workload; median of {head['reps']} timed passes (min/max beside "
+                  f"it); contiguous index shards over {head['cores']} threads, the fastest of a sweep up to this "
+                  f"process's {cpu_threads()} available cores (CPU affinity {len(os.sched_getaffinity(0))}, cgroup "
+                  f"CPU quota {cgroup_cpu_quota()}, machine {os.cpu_count()})",
+        "single_thread": single,
+        "release_path": dict(rel, kind=kind, single_thread=rel_1,
+                             code=("the reference's release build per frame: the same lines without Core::checksum "
+                                   "(oracle/ref_core.cc ref_release_batch)" if ref is not None else
+                                   "oracle/pn_oracle.c orc_release_batch"),
+                             note="beside the GPU's release-path figures (pn_set_verify(ctx, 0): c2_release_path, "
+                                  "e2e_zero_copy_pinned_host_release_path)"),
         "host_cpu": _cpu_model(),
         "c1_socket_loopback_ref": c1,
-    }
+    })
     if ref is not None:
-        fr_p, gb_p, _ = rate(port, best, budget_s * 0.15)
-        fr_p1, gb_p1, _ = rate(port, 1, budget_s * 0.1)
-        out["port"] = {"value": round(gb_p, 2), "unit": "Gbit/s", "mframes_per_s": round(fr_p / 1e6, 3),
-                       "cores": best, "single_thread_gbit_per_s": round(gb_p1, 2),
-                       "code": "oracle/pn_oracle.c orc_refsum_batch (the oracle's restatement of the same path)"}
+        p_mt = measure(port, head["cores"], budget_s * 0.012)
+        p_1 = measure(port, 1, budget_s * 0.012)
+        p_rel1 = measure(lambda th: port(th, True), 1, budget_s * 0.01)
+        out["port"] = {"value": p_mt["value"], "min": p_mt["min"], "max": p_mt["max"], "unit": "Gbit/s",
+                       "mframes_per_s": p_mt["mframes_per_s"], "cores": head["cores"],
+                       "single_thread_gbit_per_s": p_1["value"], "release_path_single_thread_gbit_per_s": p_rel1["value"],
+                       "code": "oracle/pn_oracle.c orc_refsum_batch / orc_release_batch (the oracle's restatement of "
+                               "the same paths)"}
         if gpu_records is not None:
-            digest, n_valid = ref.batch(slots, STRIDE, FRAME_OFF, sample, best)
+            digest, n_valid = ref.batch(slots, STRIDE, FRAME_OFF, sample, head["cores"])
             rec = np.ascontiguousarray(gpu_records[: sample * 16]).view(pa.RESULT_DTYPE)
             out["reference_agrees_with_gpu_records"] = digest == orc.records_digest(rec)
             out["reference_frames_verified"] = n_valid
+            out["release_path"]["reference_agrees_with_gpu_records"] = (
+                ref.release(slots, STRIDE, FRAME_OFF, sample, rel["cores"]) == orc.records_digest(rec, release=True))
     return out
 
 

@@ -13,7 +13,8 @@
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
 //   argv: n_flows (256)  polls (400)  [cpu|quick]   prints one JSON line; exit 0 = all data delivered
 //         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512, GPU
-//         pipelined 16384 and CPU 512 only — bench.py's secondary.tcp_server_poll)
+//         pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
+//         checksum summed) — bench.py's secondary.tcp_server_poll)
 #include <arpa/inet.h>
 
 #include <chrono>
@@ -284,6 +285,8 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_512_release_path", runOne<512, GpuBackend>(n_flows, polls, false));
     leg("gpu_rxbatch_16384_pipelined_release_path", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4, false));
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
+    // the same sequential server with the discard off: the reference's release build (no checksum summed per frame)
+    leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
   } else if (!cpu_only) {
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_4096", runOne<4096, GpuBackend>(n_flows, polls));
@@ -300,6 +303,7 @@ int main(int argc, char** argv) {
   }
   if (argc <= 3 || std::strcmp(argv[3], "quick") != 0) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
+    leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
     leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
     leg("cpu_rxbatch_4096_pipelined", runOne<4096, OracleBackend, 0, true>(n_flows, polls / 4));
   }

@@ -152,8 +152,10 @@ int orc_table_del(orc_table* t, uint64_t key) { /* Core.h:578-605 */
 }
 
 /* ---------------- per-frame transform ---------------- */
+/* verify_tcp = 0: the record pn_classify writes under pn_set_verify(ctx, 0) -- everything but the TCP
+ * verdict (no segment sum: PN_F_TCP_UNCHECKED, tcp_fold 0xFFFF), the IP verdicts from the header alone */
 static void classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
-                           uint64_t mask, uint32_t max_conn, pn_result* out, int with_rfc) {
+                           uint64_t mask, uint32_t max_conn, pn_result* out, int with_rfc, int verify_tcp) {
   const uint8_t* ip = eth + 14;  /* Core.h:506 */
   const uint8_t* tcp = ip + 20;  /* Core.h:507: IHL assumed 5 */
   uint32_t flags = 0;
@@ -187,6 +189,15 @@ static void classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_ent
   int trunc = (14u + 20u + tcp_len_even) > avail;
   if (trunc) {
     flags |= PN_F_TRUNC;
+    if (!verify_tcp) flags |= PN_F_TCP_UNCHECKED;
+  } else if (!verify_tcp) {
+    flags |= PN_F_TCP_UNCHECKED;
+    uint32_t hl = ihl * 4;
+    if (with_rfc && ihl >= 5 && hl <= tot_len) {
+      orc_csum r = {0};
+      orc_csum_add_bytes(&r, ip, hl);
+      if (orc_csum_fold(r) == 0) flags |= PN_F_RFC_IP_OK;
+    }
   } else {
     orc_csum t = {0};
     orc_csum_add32(&t, ld32(ip + 12)); /* src_ip */
@@ -239,7 +250,11 @@ static void classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_ent
 
 void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
                         uint64_t mask, uint32_t max_conn, pn_result* out) {
-  classify_frame(eth, avail, tbl, n_entries, mask, max_conn, out, 1);
+  classify_frame(eth, avail, tbl, n_entries, mask, max_conn, out, 1, 1);
+}
+void orc_classify_frame_release(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
+                                uint64_t mask, uint32_t max_conn, pn_result* out) {
+  classify_frame(eth, avail, tbl, n_entries, mask, max_conn, out, 1, 0);
 }
 
 static void release_frame(const uint8_t* eth, const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask,
@@ -275,7 +290,7 @@ typedef struct job {
   uint64_t mask;
   uint32_t max_conn;
   pn_result* out;
-  int mode; /* 0 full (REF + RFC), 1 release path, 2 REF checksum path only */
+  int mode; /* 0 full (REF + RFC), 1 release path, 2 REF checksum path only, 3 pn_set_verify(ctx, 0) records */
 } job;
 
 static void* run_job(void* arg) {
@@ -286,7 +301,7 @@ static void* run_job(void* arg) {
     if (j->mode == 1)
       release_frame(eth, j->tbl, j->n_entries, j->mask, j->max_conn, &j->out[i]);
     else
-      classify_frame(eth, avail, j->tbl, j->n_entries, j->mask, j->max_conn, &j->out[i], j->mode == 0);
+      classify_frame(eth, avail, j->tbl, j->n_entries, j->mask, j->max_conn, &j->out[i], j->mode != 2, j->mode != 3);
   }
   return NULL;
 }
@@ -326,4 +341,10 @@ void orc_refsum_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame
                       const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
                       pn_result* out, int n_threads) {
   run_batch(slots, slot_stride, frame_off, n, tbl, n_entries, mask, max_conn, out, n_threads, 2);
+}
+
+void orc_classify_batch_unverified(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                                   const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
+                                   pn_result* out, int n_threads) {
+  run_batch(slots, slot_stride, frame_off, n, tbl, n_entries, mask, max_conn, out, n_threads, 3);
 }

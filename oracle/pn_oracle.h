@@ -56,6 +56,10 @@ int orc_table_del(orc_table* t, uint64_t key);                           /* Core
  * to the end of its slot.  Table may be described by raw entries + mask. */
 void orc_classify_frame(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
                         uint64_t mask, uint32_t max_conn, pn_result* out);
+/* The record pn_classify writes under pn_set_verify(ctx, 0): every field and verdict of
+ * orc_classify_frame but the TCP one (no segment sum; PN_F_TCP_UNCHECKED, tcp_fold 0xFFFF). */
+void orc_classify_frame_release(const uint8_t* eth, uint32_t avail, const pn_conn_entry* tbl, uint32_t n_entries,
+                                uint64_t mask, uint32_t max_conn, pn_result* out);
 
 /* Batch over strided slots; n_threads <= 1 runs single-threaded (pthreads otherwise). */
 void orc_classify_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
@@ -75,6 +79,11 @@ void orc_release_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t fram
 void orc_refsum_batch(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                       const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
                       pn_result* out, int n_threads);
+
+/* orc_classify_frame_release over a batch: the expected records of pn_set_verify(ctx, 0). */
+void orc_classify_batch_unverified(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
+                                   const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
+                                   pn_result* out, int n_threads);
 
 /* ---- TX checksum generation (pn_tx_oracle.c) ---- */
 /* n frames built the way a reference sender builds them (incremental CSum state:

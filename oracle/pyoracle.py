@@ -52,6 +52,7 @@ _frame = _sig("orc_classify_frame", None, _vp, _u32, _vp, _u32, _u64, _u32, _vp)
 _batch = _sig("orc_classify_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 _release = _sig("orc_release_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 _refsum = _sig("orc_refsum_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
+_unverified = _sig("orc_classify_batch_unverified", None, _vp, _u32, _u32, _u32, _vp, _u32, _u64, _u32, _vp, _i32)
 _tx_build = _sig("orc_tx_build_batch", _i32, _u64, _u32, _vp, _u32, _u32, _u32, _vp, _vp)
 _tx_fill_frame = _sig("orc_tx_fill_frame", _i32, _vp, _u32, _i32, C.c_uint16, _u32)
 _tx_fill_batch = _sig("orc_tx_fill_batch", None, _vp, _u32, _u32, _u32, _vp, _u32, _i32)
@@ -137,11 +138,14 @@ def classify_frame(eth: bytes, avail: int, entries: np.ndarray, mask: int, max_c
 
 
 def classify_batch(slots: np.ndarray, stride: int, frame_off: int, n: int, entries: np.ndarray, mask: int,
-                   max_conn: int, threads: int = 1, release: bool = False, ref_only: bool = False) -> np.ndarray:
+                   max_conn: int, threads: int = 1, release: bool = False, ref_only: bool = False,
+                   unverified: bool = False) -> np.ndarray:
+    """release: the minimal release-path record (timing); unverified: the exact record of
+    pn_classify under pn_set_verify(ctx, 0) (orc_classify_batch_unverified)."""
     assert slots.dtype == np.uint8 and slots.flags.c_contiguous and slots.size >= n * stride
     ent = np.ascontiguousarray(entries, dtype=ENTRY_DTYPE)
     out = np.zeros(n, RESULT_DTYPE)
-    fn = _release if release else (_refsum if ref_only else _batch)
+    fn = _unverified if unverified else (_release if release else (_refsum if ref_only else _batch))
     fn(slots.ctypes.data, stride, frame_off, n, ent.ctypes.data, len(ent), mask, max_conn, out.ctypes.data, threads)
     return out
 
@@ -233,6 +237,7 @@ def ref_core():
             ("ref_bench_new", _vp, [_vp, _vp, _u32]),
             ("ref_bench_free", None, [_vp]),
             ("ref_bench_batch", _u64, [_vp, _vp, _u32, _u32, _u32, _i32, _vp]),
+            ("ref_release_batch", _u64, [_vp, _vp, _u32, _u32, _u32, _i32]),
         ):
             f = getattr(lib, name)
             f.restype, f.argtypes = res, args
@@ -306,13 +311,20 @@ class RefBench:
         d = self.lib.ref_bench_batch(self.h, slots.ctypes.data, stride, frame_off, n, threads, C.byref(valid))
         return int(d), int(valid.value)
 
+    def release(self, slots: np.ndarray, stride: int, frame_off: int, n: int, threads: int = 1) -> int:
+        """The release build's per-frame work (ref_release_batch: no Core::checksum); its digest equals
+        records_digest(records, release=True)."""
+        assert slots.dtype == np.uint8 and slots.flags.c_contiguous and slots.size >= n * stride
+        return int(self.lib.ref_release_batch(self.h, slots.ctypes.data, stride, frame_off, n, threads))
 
-def records_digest(rec: np.ndarray) -> int:
+
+def records_digest(rec: np.ndarray, release: bool = False) -> int:
     """ref_bench_batch's digest (oracle/ref_core.cc ref_frame_digest) computed from pn_result
-    records: (IP_OK and TCP_OK, HIT, TW, conn_id on hit, payload_off, payload_len, seq)."""
+    records: (IP_OK and TCP_OK, HIT, TW, conn_id on hit, payload_off, payload_len, seq).
+    release: ref_release_batch's (no checksum verified: the first term is 0)."""
     u = np.uint64
     fl = rec["flags"].astype(u)
-    verified = ((fl & u(3)) == u(3)).astype(u)
+    verified = np.zeros(len(rec), u) if release else ((fl & u(3)) == u(3)).astype(u)
     hit = (fl >> u(2)) & u(1)
     tw = (fl >> u(3)) & u(1)
     conn = np.where(hit == u(1), rec["conn_id"].astype(u), u(0xFFFFFFFF))

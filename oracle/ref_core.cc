@@ -286,7 +286,8 @@ uint32_t ref_table_entries(void* tp, uint64_t* keys, uint32_t* conn_ids, uint64_
 uint32_t ref_table_total_size() { return Ref::TotalTableSize; }
 
 // ---- the CPU baseline: the reference's own per-frame code over a ring of slots ----
-// Per frame, in pollNet's order (Core.h:503-510, debug build): Core::checksum (Core.h:448-472),
+// Per frame, in pollNet's order (Core.h:503-510, debug build; the release build skips the first step):
+// Core::checksum (Core.h:448-472),
 // key = connHashKey(src_ip, src_port), entry = findConnEntry(key), the TIME_WAIT test, and
 // TcpConn::onPack's payload extent and seq (TcpConn.h:469-473).  The table is the bench's
 // (MaxConnCnt = MaxTimeWaitConnCnt = 1024, pollnet_amd.rx.GenParams), one copy per thread.
@@ -308,12 +309,19 @@ void* ref_bench_new(const uint64_t* keys, const uint32_t* conn_ids, uint32_t n) 
 }
 void ref_bench_free(void* t) { delete static_cast<RefBench*>(t); }
 
+// CHECK = false: the release build's per-frame work (Core.h:503-510 without EFVITCP_DEBUG's Core::checksum,
+// then onPack's head): the digest's verified bit is 0, as records_digest(release=True) computes it.
+extern "C++" {
+template <bool CHECK>
 static inline uint64_t ref_frame_digest(RefBench& t, uint8_t* eth) {
   using namespace efvitcp;
   IpHeader* ip_hdr = reinterpret_cast<IpHeader*>(eth + sizeof(EtherHeader));
-  const int exits0 = t.exits;
-  t.checksum(ip_hdr);
-  const bool verified = t.exits == exits0;
+  bool verified = false;
+  if constexpr (CHECK) {
+    const int exits0 = t.exits;
+    t.checksum(ip_hdr);
+    verified = t.exits == exits0;
+  }
   TcpHeader* th = reinterpret_cast<TcpHeader*>(ip_hdr + 1);
   const uint64_t key = connHashKey(ip_hdr->src_ip, th->src_port);
   ConnHashEntry* entry = t.findConnEntry(key);
@@ -330,9 +338,10 @@ static inline uint64_t ref_frame_digest(RefBench& t, uint8_t* eth) {
 
 // Frames [0, n) of the slot ring, split into contiguous shards over `threads` threads (each
 // with its own copy of the table).  Returns the digest (sum over frames, order-free); *n_valid
-// = frames whose checksums verified.
-uint64_t ref_bench_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off, uint32_t n, int threads,
-                         uint32_t* n_valid) {
+// = frames whose checksums verified (CHECK; 0 on the release path).
+template <bool CHECK>
+static uint64_t ref_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off, uint32_t n, int threads,
+                          uint32_t* n_valid) {
   RefBench* proto = static_cast<RefBench*>(tp);
   if (threads < 1) threads = 1;
   std::vector<uint64_t> dig(threads, 0);
@@ -349,12 +358,14 @@ uint64_t ref_bench_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off
     int exits_cleared = 0;
     for (uint32_t i = b; i < e; i++) {
       const int exits0 = t->exits;
-      d += ref_frame_digest(*t, slots + (size_t)i * stride + off);
-      if (t->exits == exits0) {
-        v++;
-      } else if (t->exits - exits_cleared > 256) { // drop the debug build's prints now and then
-        t->cout.os.str(std::string());
-        exits_cleared = t->exits;
+      d += ref_frame_digest<CHECK>(*t, slots + (size_t)i * stride + off);
+      if constexpr (CHECK) {
+        if (t->exits == exits0) {
+          v++;
+        } else if (t->exits - exits_cleared > 256) { // drop the debug build's prints now and then
+          t->cout.os.str(std::string());
+          exits_cleared = t->exits;
+        }
       }
     }
     dig[w] = d;
@@ -369,6 +380,16 @@ uint64_t ref_bench_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off
   for (int w = 0; w < threads; w++) d += dig[w], v += valid[w];
   if (n_valid) *n_valid = v;
   return d;
+}
+} // extern "C++"
+// The debug build's per-frame work (Core::checksum included): bench.py's cpu_baseline headline.
+uint64_t ref_bench_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off, uint32_t n, int threads,
+                         uint32_t* n_valid) {
+  return ref_batch<true>(tp, slots, stride, off, n, threads, n_valid);
+}
+// The release build's (no checksum): cpu_baseline.release_path, beside pn_set_verify(ctx, 0).
+uint64_t ref_release_batch(void* tp, uint8_t* slots, uint32_t stride, uint32_t off, uint32_t n, int threads) {
+  return ref_batch<false>(tp, slots, stride, off, n, threads, nullptr);
 }
 // how many times the debug build's rehash check fired (Core.h:665-669: it would have exited)
 int ref_table_debug_exits(void* tp) { return static_cast<Ref*>(tp)->exits; }

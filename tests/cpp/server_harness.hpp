@@ -42,7 +42,13 @@ struct ScriptLink {
 struct OracleBackend {
   static constexpr bool kSnapshot = false;
   static constexpr uint32_t kStride = 2048, kFrameOff = 2;
-  const char* setVerify(bool) { return nullptr; } // the oracle always computes both verdicts; the engine reads them only when dropping
+  // verify = false: the release path, as the GPU backend's pn_set_verify(ctx, 0) -- no segment sum per frame, the
+  // records pn_classify writes then (orc_classify_frame_release); the reference's release build sums nothing
+  bool verify = true;
+  const char* setVerify(bool v) {
+    verify = v;
+    return nullptr;
+  }
   std::vector<uint8_t> rx, tx;
   std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
   uint32_t cap = 0;
@@ -66,11 +72,12 @@ struct OracleBackend {
     std::memcpy(&port_be, eth + 34, 2);
     return pn_conn_hash_key(ip_be, port_be);
   }
-  static void one(const uint8_t* eth, const pollnet_amd::ConnTable& t, pn_result* r) {
+  void one(const uint8_t* eth, const pollnet_amd::ConnTable& t, pn_result* r) const {
     uint32_t ne = 0;
     uint64_t mask = 0;
     const pn_conn_entry* e = t.entries(&ne, &mask);
-    orc_classify_frame(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), r);
+    if (verify) orc_classify_frame(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), r);
+    else orc_classify_frame_release(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), r);
   }
   // sequential: each frame against the live table, just before its dispatch
   template <class F>

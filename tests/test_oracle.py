@@ -309,3 +309,29 @@ def test_release_path_matches_full_path_fields():
         assert np.array_equal(full[k], rel[k])
     keep = pa.F.HIT | pa.F.TW | 0x1F0
     assert np.array_equal(full["flags"] & keep, rel["flags"])
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_unverified_record_is_full_record_less_tcp_verdict(cfg):
+    """orc_classify_batch_unverified (the expected record of pn_set_verify(ctx, 0)) computes no segment sum, yet equals
+    the full record with the TCP verdict taken out (TCP_OK / RFC_TCP_OK cleared, TCP_UNCHECKED set, tcp_fold 0xFFFF):
+    C3 / C5 frames (options, odd lengths, bad sums, TRUNC) and random bytes at every alignment class."""
+    F = pa.F
+    p = pa.rx.GenParams.for_config(cfg)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    s = pa.gen_frames(p, 4096)
+    rng = np.random.default_rng(cfg)
+    junk = rng.integers(0, 256, (512, STRIDE), dtype=np.uint8)
+    junk[:, FRAME_OFF + 12:FRAME_OFF + 14] = (8, 0)
+    junk[:, FRAME_OFF + 14] = 0x45
+    junk[:, FRAME_OFF + 23] = 6
+    s = np.ascontiguousarray(np.concatenate([s, junk]))
+    n = len(s)
+    full = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, 1024)
+    got = orc.classify_batch(s, STRIDE, FRAME_OFF, n, e, m, 1024, unverified=True)
+    exp = full.copy()
+    exp["flags"] = (exp["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
+    exp["tcp_fold"] = 0xFFFF
+    assert np.array_equal(got, exp)
+    assert (full["flags"] & F.TRUNC).any() or cfg == 3

@@ -203,6 +203,10 @@ def test_reference_batch_digest_equals_oracle_records(cfg):
         digest, n_valid = rb.batch(slots, 2048, 2, n, threads)
         assert digest == orc.records_digest(rec)
         assert n_valid == int(((rec["flags"] & 3) == 3).sum())
+    # the release build's work (ref_release_batch, no Core::checksum) against the records of pn_set_verify(ctx, 0)
+    unv = orc.classify_batch(slots, 2048, 2, n, entries, mask, p.max_conn_cnt, threads=4, unverified=True)
+    for threads in (1, 3):
+        assert rb.release(slots, 2048, 2, n, threads) == orc.records_digest(unv, release=True)
 
 
 @pytest.mark.gpu
