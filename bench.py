@@ -61,7 +61,9 @@ def parse():
                     help="workload (default: C2 at one GPU, C4 = BASELINE configs[3] at N>1)")
     ap.add_argument("--frames", type=int, default=0, help="frames per GPU (default: 1 Mi; C4: 2 Mi)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="no end-to-end legs (host ring in, records out)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="the headline and the end-to-end host-ring leg only (no secondary legs, no CPU baseline)")
     ap.add_argument("--no-secondary", action="store_true", help="skip the C3/C5/packed/TX sub-measurements")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget for the CPU baseline leg")
     ap.add_argument("--stream-ceiling-only", action="store_true",
@@ -361,13 +363,42 @@ def ceilings(torch, ctx, bufs, n, res, stream, steps=20, rounds=7, stream_only=F
             "at_ceiling_within_spread": abs(1 - a_ms / p_ms) <= max(spread, 0.002)}
 
 
-def load_pmc(workload_key):
-    """The committed rocprofv3 --pmc summary for a workload (profiles/pmc_traffic.json)."""
+def load_pmc(workload_key, sub=None):
+    """The committed rocprofv3 --pmc summary for a workload (profiles/pmc_traffic.json, scripts/pmc_refresh.sh), with
+    whether the built library still holds the kernel code the counters were taken on: each entry records the code
+    hash of every kernel it summed over, compared here with the same hash of the library this run loads
+    (pollnet_amd/codehash.py)."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
-            return json.load(f).get(workload_key)
+            e = json.load(f).get(workload_key)
     except (OSError, ValueError):
         return None
+    if e is not None and sub is not None:
+        e = e.get(sub)
+    if e is None:
+        return None
+    from pollnet_amd import codehash
+
+    try:
+        ok, why = codehash.check_entry(e)
+    except Exception as ex:  # a library or tool that cannot be read: never report the bytes as current
+        ok, why = False, f"code identity not checked: {ex!r}"
+    return dict(e, code_current=ok, code_check=why)
+
+
+def pmc_fields(pmc, ms=None):
+    """The traffic keys of a bench object: the committed bytes per launch only while the code is the measured
+    code; otherwise null with traffic_stale true (a changed kernel needs a PMC refresh, scripts/pmc_refresh.sh)."""
+    if pmc is None:
+        return {"traffic": None, "traffic_over_algorithmic": None, "traffic_stale": None,
+                "traffic_code_check": "no committed PMC entry for this workload"}
+    cur = pmc["code_current"]
+    out = {"traffic": pmc["hbm_bytes_per_launch"] if cur else None,
+           "traffic_over_algorithmic": pmc.get("traffic_over_algorithmic") if cur else None,
+           "traffic_stale": not cur, "traffic_code_check": pmc["code_check"]}
+    if ms is not None:
+        out["traffic_gbs"] = round(pmc["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1) if cur else None
+    return out
 
 
 def golden_digest(cfg, first=0, n=None):
@@ -442,9 +473,7 @@ def secondary_rx(torch, pa, cfg, n, steps, stream, packed=False):
            "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "ablated_kernel_ms": c["ablated_kernel_ms"], "kernel_vs_ablated_ceiling": c["kernel_vs_ablated_ceiling"],
            "at_ceiling_within_spread": c["at_ceiling_within_spread"], "stream_read_gbs": c["stream_read_gbs"],
-           "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-           "traffic_over_algorithmic": None if pmc is None else pmc.get("traffic_over_algorithmic"),
-           "records_sha256_matches_golden": bool(sha_ok)}
+           **pmc_fields(pmc), "records_sha256_matches_golden": bool(sha_ok)}
     if packed:
         # packed capture: each frame (+ its pad byte) back to back, every Ethernet header at 2 mod 16
         # (the slots' alignment class): frame i+1 starts ((len_i + 17) & ~15) after frame i
@@ -521,8 +550,7 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
             "algorithmic_bytes_per_launch": n * (64 + 4),
             "achieved_gbs": round(n * (64 + 4) / (ms * 1e-3) / 1e9, 1),
             "frac": round(n * (64 + 4) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-            "traffic_gbs": None if pmc is None else round(pmc["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9, 1),
+            **pmc_fields(pmc, ms),
             "gather_loads_only_ms": round(mg, 5), "kernel_vs_gather_ceiling": round(mg / ms, 4),
             "loads_and_id_stores_ms": round(mw, 5), "kernel_vs_loads_and_stores_ceiling": round(mw / ms, 4),
             # HBM rate against the gather's: the kernel moves one 128-B line per frame AND its 4-B id, the
@@ -606,7 +634,6 @@ def secondary_tx(torch, pa, n, steps, stream):
 
     ctx = pa.RxContext(torch.cuda.current_device())
     out = {}
-    pmc = load_pmc("tx_c2_n1048576")
     p = pa.rx.GenParams.for_config(2)
     host = np.empty((n, STRIDE), dtype=np.uint8)
     for off in (2, 14):
@@ -640,7 +667,7 @@ def secondary_tx(torch, pa, n, steps, stream):
                                      stream))
         kern, kabl = statistics.median(ks), statistics.median(abl)
         algo = 1504 * n
-        tr = None if not pmc else pmc.get(f"frame_off_{off}", {})
+        tr = load_pmc("tx_c2_n1048576", f"frame_off_{off}")
         out[f"frame_off_{off}"] = {
             "kernel": "tx_fill_kernel + tx_patch_kernel (one pn_tx_fill call)", "frames": n, "resident_batches": 2,
             "kernel_ms": round(kern, 5), "gbit_per_s": round(8 * 1514 * n / (kern * 1e-3) / 1e9, 1),
@@ -648,8 +675,9 @@ def secondary_tx(torch, pa, n, steps, stream):
             "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ablated_kernel_ms": round(kabl, 5), "kernel_vs_ablated_ceiling": round(kabl / kern, 4),
             "at_ceiling_within_spread": abs(1 - kabl / kern) <= max((max(ks) - min(ks)) / kern, 0.002),
-            "traffic": None if not tr else tr.get("hbm_bytes_per_launch"),
-            "traffic_over_algorithmic": None if not tr else tr.get("traffic_over_algorithmic"),
+            **pmc_fields(tr),
+            "write_requests_per_frame": None if not (tr and tr["code_current"]) else tr.get("ea_write_requests_per_frame"),
+            "write_64B_per_frame": None if not (tr and tr["code_current"]) else tr.get("ea_write_64B_per_frame"),
             "first_4096_vs_oracle": bool(np.array_equal(got, exp)),
             "frames_changed_vs_valid_original": int(len(bad)),
             "only_corrupted_frames_differ": bool(len(bad) == n // 1024 and np.all(bad % 1024 == bad[0] % 1024))}
@@ -683,7 +711,7 @@ def secondary_release_path(torch, pa, ctx, frames_b, res, n, steps, stream):
     algo = n * (64 + 16)
     pmc = load_pmc(f"c2_release_path_n{n}")
     return {"kernel_ms": round(kern, 5), "mframes_per_s": round(n / (kern * 1e-3) / 1e6, 1),
-            "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
+            **pmc_fields(pmc),
             "algorithmic_bytes_per_launch": algo, "achieved_gbs": round(algo / (kern * 1e-3) / 1e9, 1),
             "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "line_traffic_gbs": round(n * (128 + 16) / (kern * 1e-3) / 1e9, 1),
@@ -729,6 +757,111 @@ def secondary_c4_shard(torch, pa, ctx_dev, steps, R, stream):
             "batches_sha256_gated": f"{len(sha) if gd is not None else 0}/{R}",
             "gated_batches_sha256_match_golden": bool(gd is not None and all(sha)),
             "note": "the per-GPU workload of the N>1 line, on one GPU: N x this value is the ideal N-GPU aggregate"}
+
+
+def e2e_host_ring(torch, pa, ctx, ring, n, got0, stream, dist, barrier, world, rank, numa, passes=5):
+    """The end-to-end leg on every rank: the node's one host ring (pollnet_amd/host_ring.py), each rank's
+    shard first-touched on its GPU's NUMA node and hipHostRegister-ed, classified in place by that rank's GPU
+    (zero copy), the records written into the ring's shared record array.  Both modes: checksums verified (each
+    frame's lines cross PCIe) and the release path (pn_set_verify(ctx, 0): one header line per frame).  Timed over
+    one common window per mode (max over ranks), `passes` launches over the whole shard; value = all ranks' wire
+    bytes / that window.  Every rank's records must equal its device-resident records of the same frames (already
+    gated against the committed digests), with the TCP verdict taken out in release mode."""
+    from pollnet_amd.shard import common_window
+
+    ring.register()
+    shard_ptr, rec_ptr = ring.addresses()
+    wire = float(pa.wire_bytes(ring.shard(), STRIDE, FRAME_OFF, n))
+    F = pa.rx.F
+    out = {"note": "one host ring in POSIX shared memory, rank r's index shard first-touched from its GPU's NUMA node "
+                   "and hipHostRegister-ed; pn_classify reads it in place over PCIe and writes the 16-B records into "
+                   "the ring's shared record array (pollnet_amd/host_ring.py)", "passes": passes,
+           "frames_per_rank": n}
+    try:
+        for mode in ("verified", "release_path"):
+            ctx.set_verify(mode == "verified")
+            ctx.classify(shard_ptr, STRIDE, FRAME_OFF, n, rec_ptr, stream)  # warm: TLB / page-table walk of the range
+            torch.cuda.synchronize()
+            t_own = [0.0]
+
+            def body():
+                t0 = time.perf_counter()
+                for _ in range(passes):
+                    ctx.classify(shard_ptr, STRIDE, FRAME_OFF, n, rec_ptr, stream)
+                torch.cuda.synchronize()
+                t_own[0] = time.perf_counter() - t0
+
+            wall, _ = common_window(body, dist if world > 1 else None, barrier)
+            exp = np.ascontiguousarray(got0).view(pa.RESULT_DTYPE).copy()
+            if mode == "release_path":
+                exp["flags"] = (exp["flags"] & ~np.uint16(F.TCP_OK | F.RFC_TCP_OK)) | np.uint16(F.TCP_UNCHECKED)
+                exp["tcp_fold"] = 0xFFFF
+            ok = bool(np.array_equal(ring.records().view(pa.RESULT_DTYPE), exp))
+            # bytes the path needs across PCIe per frame: the frame + its record (verified), the 64-B header window
+            # + the record (release); the line-granular bytes are up to 1.02x / 1.8x that
+            need = (wire + 16 * n) if mode == "verified" else n * (64 + 16)
+            mine = {"rank": rank, "numa_node": numa, "own_s": round(t_own[0], 5),
+                    "needed_bytes_gb_per_s": round(need * passes / t_own[0] / 1e9, 2), "records_ok": ok}
+            ranks = [mine]
+            total_wire = wire
+            if world > 1:
+                ranks = [None] * world
+                dist.all_gather_object(ranks, mine)
+                w = torch.tensor([wire], dtype=torch.float64)
+                dist.all_reduce(w, op=dist.ReduceOp.SUM)
+                total_wire = float(w[0])
+            out[mode] = {"gbit_per_s": round(total_wire * passes * 8 / wall / 1e9, 2),
+                         "mframes_per_s": round(n * world * passes / wall / 1e6, 2),
+                         "window_s": round(wall, 5), "every_rank_records_ok": all(r["records_ok"] for r in ranks),
+                         "ranks": ranks}
+    finally:
+        ctx.set_verify(True)
+    return out
+
+
+def summary(out):
+    """The line's figures a reader needs first, compact: kernel fractions of the 8 TB/s roofline, the per-GPU
+    workload of the N>1 line, the release-path kernels, the CPU baselines with their spread, the host-ring rates."""
+    def g(d, *path):
+        for k in path:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return d
+
+    sec = out.get("secondary", {})
+    cpu = out.get("cpu_baseline", {})
+    s = {"value": out["value"], "unit": out["unit"], "n_gpus": out["n_gpus"], "frac": g(out, "roofline", "frac"),
+         "kernel_ms": g(out, "roofline", "kernel_ms_avg"), "traffic_stale": g(out, "roofline", "traffic_stale"),
+         "verified": out.get("verified_vs_oracle")}
+    if sec:
+        s.update({
+            "c3_frac": g(sec, "c3", "frac"), "c5_frac": g(sec, "c5", "frac"),
+            "c4_shard_gbit_per_s": g(sec, "c4_shard", "value"), "c4_shard_kernel_ms": g(sec, "c4_shard", "kernel_ms"),
+            "tx_off2_frac": g(sec, "tx_fill", "frame_off_2", "frac"), "tx_off14_frac": g(sec, "tx_fill", "frame_off_14", "frac"),
+            "tx_off2_ms": g(sec, "tx_fill", "frame_off_2", "kernel_ms"),
+            "tx_off14_ms": g(sec, "tx_fill", "frame_off_14", "kernel_ms"),
+            "match_streams_ms": g(sec, "match_streams", "kernel_ms"),
+            "release_path_ms": g(sec, "c2_release_path", "kernel_ms"),
+            "server_512_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512", "mframes_per_s"),
+            "server_512_release_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_release_path", "mframes_per_s"),
+            "server_cpu_512_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512", "mframes_per_s"),
+            "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s")})
+    if cpu:
+        s.update({"cpu_ref_gbit_per_s": cpu.get("value"), "cpu_ref_min_max": [cpu.get("min"), cpu.get("max")],
+                  "cpu_ref_cores": cpu.get("cores"), "cpu_ref_consistent_with_sweep": cpu.get("consistent_with_sweep"),
+                  "cpu_ref_release_gbit_per_s": g(cpu, "release_path", "value"),
+                  "cpu_ref_release_min_max": [g(cpu, "release_path", "min"), g(cpu, "release_path", "max")],
+                  "cpu_ref_release_cores": g(cpu, "release_path", "cores")})
+    for k in ("e2e_pinned_host", "e2e_zero_copy_pinned_host", "e2e_zero_copy_pinned_host_release_path"):
+        if k in out:
+            s[k + "_gbit_per_s"] = g(out, k, "gbit_per_s")
+    if "e2e_host_ring" in out:
+        s["e2e_host_ring_gbit_per_s"] = g(out, "e2e_host_ring", "verified", "gbit_per_s")
+        s["e2e_host_ring_release_gbit_per_s"] = g(out, "e2e_host_ring", "release_path", "gbit_per_s")
+        s["e2e_host_ring_records_ok"] = (g(out, "e2e_host_ring", "verified", "every_rank_records_ok") and
+                                         g(out, "e2e_host_ring", "release_path", "every_rank_records_ok"))
+    return s
 
 
 def device_identity(torch, dev):
@@ -790,21 +923,37 @@ def run_rank(rank, world, local_rank, args):
     # memory-side cache, so a copy is as cold as new content), so every timed batch is the rank's own
     # shard and is gated against that shard's committed digest.
     firsts = [b * n if world == 1 else lo for b in range(R)]
+    # the node's one host ring (pollnet_amd/host_ring.py): rank r's batch 0 is generated straight into its shard,
+    # from CPUs of its GPU's NUMA node (first touch places the pages there), for the end-to-end leg
+    ring, numa_node, numa_cpus = None, -1, []
+    if not args.no_e2e:
+        from pollnet_amd.host_ring import SharedHostRing, device_numa
+
+        pr = torch.cuda.get_device_properties(dev)
+        numa_node, numa_cpus = device_numa(pr.pci_domain_id, pr.pci_bus_id, pr.pci_device_id)
+        ring = SharedHostRing(dist if world > 1 else None, rank, world, n, STRIDE)
     frames_b, wires = [], []
-    host = np.empty((n, STRIDE), dtype=np.uint8)
+    host = np.empty((n, STRIDE), dtype=np.uint8) if (R > 1 and world == 1) or ring is None else None
     slots = None
     for b in range(R):
         if world > 1 and b > 0:
             frames_b.append(frames_b[0].clone())
             wires.append(wires[0])
             continue
-        pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=firsts[b], threads=gen_threads, out=host)
-        wires.append(pa.wire_bytes(host, STRIDE, FRAME_OFF, n))
-        frames_b.append(torch.from_numpy(host.reshape(-1)).to(f"cuda:{dev}"))
+        dst = ring.shard() if (b == 0 and ring is not None) else host
+        from pollnet_amd.host_ring import cpu_affinity
+
+        with cpu_affinity(numa_cpus if dst is not host else []):
+            pa.gen_frames(params, n, STRIDE, FRAME_OFF, first_index=firsts[b], threads=gen_threads, out=dst)
+        wires.append(pa.wire_bytes(dst, STRIDE, FRAME_OFF, n))
+        frames_b.append(torch.from_numpy(dst.reshape(-1)).to(f"cuda:{dev}"))
         if b == 0:
             # N=1 keeps batch 0 on the host (CPU baseline, e2e legs); N>1 ranks keep only the rows
             # the in-run oracle check reads
-            slots = host.copy() if world == 1 else host[: min(n, 4096)].copy()
+            if world == 1:
+                slots = dst if dst is not host else host.copy()
+            else:
+                slots = dst[: min(n, 4096)].copy()
     del host
     frames = frames_b[0]
     log(f"[rank {rank}] device {dev}: C{cfg} shard [{lo}, {lo + n}), {R} x {n} frames "
@@ -874,8 +1023,6 @@ def run_rank(rank, world, local_rank, args):
     if world > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world:
         shm_barrier = ShmBarrier(dist, rank, world)
     wall_max, own_max = common_window(timed_steps, dist if world > 1 else None, shm_barrier)
-    if shm_barrier is not None:
-        shm_barrier.close(dist)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     gate.update(device_identity(torch, dev))
     gate.update({"kernel_ms": round(kern_ms, 5), "setup_s": setup_s, "peak_rss_mib": peak_rss_mib()})
@@ -891,6 +1038,12 @@ def run_rank(rank, world, local_rank, args):
         total_wire = float(w[0])
         gates = [None] * world
         dist.all_gather_object(gates, {"rank": rank, "shard": [lo, lo + n], **gate})
+    e2e = None
+    if ring is not None:
+        try:
+            e2e = e2e_host_ring(torch, pa, ctx, ring, n, got0, stream, dist, shm_barrier, world, rank, numa_node)
+        except Exception as ex:  # measured extra; never blocks the bench line
+            e2e = {"error": repr(ex)}
     total_frames = n * world * args.steps
     gbit = total_wire * 8 / wall_max / 1e9
     mfps = total_frames / wall_max / 1e6
@@ -934,13 +1087,14 @@ def run_rank(rank, world, local_rank, args):
             "rank_own_wall_ms_max": round(own_max * 1e3, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None if pmc is None else pmc.get("hbm_bytes_per_launch"),
-                         "traffic_over_algorithmic": None if pmc is None else pmc.get("traffic_over_algorithmic"),
+                         **pmc_fields(pmc),
                          "kernel": "rx_classify_kernel", "kernel_ms_avg": round(kern_ms, 5),
                          "kernel_ms_avg_max_over_ranks": round(kern_ms_max, 5),
                          "algorithmic_bytes_per_launch": algo_bytes,
                          "bytes_per_frame": round(algo_bytes / n, 2)},
         }
+    if rank == 0 and e2e is not None:
+        out["e2e_host_ring"] = e2e
     if rank == 0 and world == 1:
         out["roofline"]["same_run_ceilings"] = ceilings(torch, ctx, frames_b, n, res, stream,
                                                         stream_only=args.stream_ceiling_only)
@@ -1004,9 +1158,15 @@ def run_rank(rank, world, local_rank, args):
     if rank == 0:
         if "WORLD_SIZE" not in os.environ or os.environ.get("PN_BENCH_SPAWNED") == "1":
             assert out["n_gpus"] == args.gpus, (out["n_gpus"], args.gpus)
+        out["summary"] = summary(out)  # last key: a driver keeping only the line's tail still sees it
         json_out.write(json.dumps(out) + "\n")
         json_out.flush()
     ctx.close()
+    del slots
+    if ring is not None:
+        ring.close(dist if world > 1 else None)
+    if shm_barrier is not None:
+        shm_barrier.close(dist)
     if world > 1:
         dist.destroy_process_group()
 
@@ -1020,6 +1180,9 @@ def _spawned(rank, world, args, port):
 
 def main():
     args = parse()
+    if args.e2e:
+        args.no_secondary = args.no_cpu_baseline = True
+        args.no_e2e = False
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # one process per GPU, started here; the parent never initialises a GPU
         import socket

@@ -298,3 +298,107 @@ def test_bench_under_the_drivers_torchrun_command():
     assert cg["distinct_devices"] == 1 and cg["every_rank_sha256_gated"] is True
     assert cg["setup_s_max"] >= max(g["setup_s"] for g in ranks)
     assert line["value"] > 0 and line["scaling"] == "weak"
+
+
+def _ring_worker(rank, world, port, n, cfg, out_dir):
+    """Each rank generates its index shard straight into the node's shared host ring (the e2e leg's layout,
+    pollnet_amd/host_ring.py), from CPUs of its NUMA node when known, then writes the oracle's records for its
+    shard into its slice of the ring's record array.  No exchange."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import pollnet_amd as pa
+    from oracle import pyoracle as orc
+    from pollnet_amd.host_ring import SharedHostRing, cpu_affinity
+    from pollnet_amd.shard import shard_range
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ring = SharedHostRing(dist, rank, world, n, 2048)
+    p = pa.rx.GenParams.for_config(cfg)
+    lo, hi = shard_range(rank, world, n)
+    cpus = sorted(os.sched_getaffinity(0))[rank::world]  # a stand-in for the GPU's node: a distinct CPU subset
+    with cpu_affinity(cpus):
+        assert set(os.sched_getaffinity(0)) == set(cpus)
+        pa.gen_frames(p, n, first_index=lo, threads=2, out=ring.shard())
+    assert set(os.sched_getaffinity(0)) != set(cpus) or len(cpus) == len(os.sched_getaffinity(0))
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    rec = orc.classify_batch(ring.shard(), 2048, 2, n, e, m, t.max_conn_cnt)
+    ring.records()[:] = rec.view(np.uint8)
+    dist.barrier()
+    if rank == 0:  # the whole ring and record array, as one process on the node sees them
+        np.save(os.path.join(out_dir, "ring.npy"), ring.slots().copy())
+        np.save(os.path.join(out_dir, "records.npy"), np.concatenate([ring.records(r) for r in range(world)]))
+        with open(os.path.join(out_dir, "name.txt"), "w") as f:
+            f.write(ring.shm.name)
+    ring.close(dist)
+    dist.destroy_process_group()
+
+
+def test_shared_host_ring_shards_assemble(tmp_path):
+    """World-size-2 gloo: the ranks' shards of the shared host ring assemble into the global ring the generator
+    makes in one process, the record slices into the single-process records, and the segment is unlinked at close."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import pollnet_amd as pa
+    from oracle import pyoracle as orc
+
+    world, n, cfg = 2, 2048, 4
+    mp.spawn(_ring_worker, args=(world, _free_port(), n, cfg, str(tmp_path)), nprocs=world, join=True)
+    p = pa.rx.GenParams.for_config(cfg)
+    full = pa.gen_frames(p, world * n, threads=4)
+    assert np.array_equal(np.load(tmp_path / "ring.npy"), full)
+    t = pa.gen_conn_table(p)
+    e, m = t.snapshot()
+    exp = orc.classify_batch(full, 2048, 2, world * n, e, m, t.max_conn_cnt)
+    assert np.array_equal(np.load(tmp_path / "records.npy"), exp.view(np.uint8))
+    assert not os.path.exists("/dev/shm/" + open(tmp_path / "name.txt").read().strip())
+
+
+def test_device_numa_lookup():
+    """sysfs lookup of a PCI device's node: an absent device is (-1, []), never an exception."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from pollnet_amd.host_ring import _cpulist, device_numa
+
+    assert device_numa(0xffff, 0xff, 0x1f) == (-1, [])
+    assert _cpulist("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+
+
+@pytest.mark.gpu
+def test_bench_e2e_host_ring_two_ranks():
+    """`bench.py --gpus 2 --e2e` under the driver's torchrun command on this box's one GPU: the end-to-end leg's
+    plumbing (one shared host ring, each rank's C4 shard of 2 Mi frames first-touched on its GPU's NUMA node,
+    hipHostRegister-ed and classified in place, records into the ring) with every shard gated: each rank's batches
+    hash to its shard's committed digest, and its ring records equal its device-resident records, in both modes.
+    Both ranks share one GPU and one PCIe link here, so the aggregate says nothing about 2 GPUs' PCIe."""
+    import json
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+           "--warmup", "1", "--batches", "2", "--e2e"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.strip().splitlines() if ln.startswith("{")]
+    line = json.loads(lines[-1])
+    assert line["verified_vs_oracle"] is True and line["correctness_gate"]["every_rank_sha256_gated"] is True
+    e2e = line["e2e_host_ring"]
+    assert "error" not in e2e, e2e
+    for mode in ("verified", "release_path"):
+        assert e2e[mode]["every_rank_records_ok"] is True, e2e[mode]
+        assert [r["rank"] for r in e2e[mode]["ranks"]] == [0, 1]
+        assert e2e[mode]["gbit_per_s"] > 0
+    assert e2e["frames_per_rank"] == 1 << 21
+    assert line["summary"]["e2e_host_ring_records_ok"] is True
+    assert list(line)[-1] == "summary"
