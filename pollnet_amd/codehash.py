@@ -88,7 +88,9 @@ def product_library() -> str:
 
 def matching(names, path: str = None) -> dict:
     """{name: hash} for rocprofv3 kernel names; a name the library does not hold maps to None."""
-    h = kernel_hashes(path or product_library())
+    h = kernel_hashes(product_library())
+    if path:
+        h.update(kernel_hashes(path))
     return {n: h.get(n) for n in sorted(set(names))}
 
 

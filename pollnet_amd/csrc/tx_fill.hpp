@@ -284,6 +284,63 @@ __global__ __launch_bounds__(256) void tx_patch_sector_kernel(TArgs a) {
   else *reinterpret_cast<u32x4*>(q) = v;
 }
 
+// Phase 2 with write-through stores (tuning, round 5: the offset-14 write pattern).  System-scope
+// stores (sc0 sc1) go through L2 to the memory side at once, so the dirty sectors leave during this short
+// phase instead of being written back while the next call streams its reads.  FORM 0: the 2-byte fields;
+// FORM 1: each 64-B sector holding a field rewritten whole from a re-read (8 lanes per frame, 16 B each), so
+// every write request is a full aligned 64-B one.
+__device__ __forceinline__ void st16_wt(uint8_t* p, uint32_t v) {
+  asm volatile("global_store_short %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st128_wt(uint8_t* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+template <int MODE, int FORM>
+__global__ __launch_bounds__(256) void tx_patch_wt_kernel(TArgs a) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if constexpr (FORM == 0) {
+    const uint32_t f = t;
+    if (f >= a.n) return;
+    const uint2 rec = a.patch[f];
+    if (!(rec.y & kPatchOk)) return;
+    uint8_t* ip = a.frames + (uint64_t)f * a.stride + a.frame_off + 14;
+    if (rec.y & kPatchLen) st16_wt(ip + 2, rec.y & 0xffff);
+    st16_wt(ip + 10, rec.x & 0xffff);
+    if constexpr (MODE == PN_TX_TCP) st16_wt(ip + 36, rec.x >> 16);
+  } else {
+    const uint32_t f = t >> 3, part = t & 7;
+    if (f >= a.n) return;
+    const uint2 rec = a.patch[f];
+    if (!(rec.y & kPatchOk)) return;
+    uint8_t* slot = a.frames + (uint64_t)f * a.stride;
+    const uint64_t ip = (uint64_t)(slot + a.frame_off + 14);
+    const uint64_t sa = (ip + 10) & ~63ull, sb = (ip + 36) & ~63ull;
+    const uint64_t sec = part < 4 ? sa : sb;
+    if (part >= 4 && sb == sa) return;
+    const uint64_t q = sec + 16 * (part & 3);
+    u32x4 v = *reinterpret_cast<const u32x4*>(q);
+    auto patch16 = [&](uint64_t at, uint32_t val) {
+      if (at >= q && at < q + 16) {
+        const uint32_t o = (uint32_t)(at - q), w = o >> 2, sh = (o & 2) * 8;
+        uint32_t* d = reinterpret_cast<uint32_t*>(&v);
+        d[w] = (d[w] & ~(0xffffu << sh)) | ((val & 0xffffu) << sh);
+      }
+    };
+    if (rec.y & kPatchLen) patch16(ip + 2, rec.y);
+    patch16(ip + 10, rec.x);
+    patch16(ip + 36, rec.x >> 16);
+    st128_wt(reinterpret_cast<uint8_t*>(q), v);
+  }
+}
+
+// Tuning: after a phase-2 kernel with ordinary stores, a short launch whose workgroups each end with a
+// system-scope release, which writes the L2's dirty lines back (one workgroup per XCD suffices; 64 cover the
+// round-robin placement), so the patch's dirty sectors leave before the next call's read stream.
+__global__ __launch_bounds__(64) void tx_l2_release_kernel(uint32_t* sink) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (threadIdx.x == 0 && sink[blockIdx.x] == 0x7fffffffu) sink[blockIdx.x] = 0; // never true: keeps the launch
+}
+
 inline bool coop_layout(const TArgs& a) {
   return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }

@@ -124,6 +124,23 @@ extern "C" int pn_tx_fill_variant(pn_ctx* ctx, void* frames, uint32_t slot_strid
         hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
         return 0;
       }
+      // round 5 (the SendBuf layout's write pattern): the product's launch shape with a write-through
+      // phase 2 (50: 2-byte fields, 51: whole 64-B sectors from a re-read), or the production phase 2 followed by
+      // an L2 write-back launch (52)
+      case 50: case 51: case 52: {
+        TArgs b = a;
+        b.fpw = frames_per_wave(n);
+        hipLaunchKernelGGL((tx_fill_kernel<M, 1, T, kWbPatch, 0, 0, 0, true>), dim3((n + b.fpw - 1) / b.fpw), block, 0, s, b);
+        if (variant == 50) {
+          hipLaunchKernelGGL((tx_patch_wt_kernel<T, 0>), pgrid, pblock, 0, s, b);
+        } else if (variant == 51) {
+          hipLaunchKernelGGL((tx_patch_wt_kernel<T, 1>), dim3((8 * n + 255) / 256), pblock, 0, s, b);
+        } else {
+          hipLaunchKernelGGL((tx_patch_kernel<T>), pgrid, pblock, 0, s, b);
+          hipLaunchKernelGGL(tx_l2_release_kernel, dim3(64), dim3(64), 0, s, reinterpret_cast<uint32_t*>(b.patch));
+        }
+        return 0;
+      }
       case 40: case 41: {
         TArgs b = a;
         b.fpw = frames_per_wave(n);

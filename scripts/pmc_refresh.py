@@ -26,8 +26,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+TUNING = os.path.join(ROOT, "pollnet_amd", "libpollnet_amd_tuning.so")
 FAMILIES = ("rx_classify_kernel", "match_streams_mask_kernel", "tx_fill_kernel", "tx_patch_kernel",
-            "calib_stream_read_kernel")
+            "calib_stream_read_kernel", "tx_patch_wt_kernel", "tx_l2_release_kernel", "tx_patch_sector_kernel")
 
 
 def family(name):
@@ -135,7 +136,7 @@ def main():
              "ea_write_requests_per_frame": round(cnt["TCC_EA0_WRREQ_sum"] / n, 4),
              "ea_write_64B_per_frame": round(w64 / n, 4),
              "calls_measured": len(fetch[label]),
-             "kernels": codehash.matching(names)}
+             "kernels": codehash.matching(names, None if not label.startswith("x_") else TUNING)}
         if fam is None:
             algo = w["algorithmic_bytes_per_launch"]
             e["algorithmic_bytes_per_launch"] = algo
@@ -154,9 +155,18 @@ def main():
     d = {}
     if os.path.exists(args.out):
         d = json.load(open(args.out))
-    new = {}
+    new, exper = {}, {}
     for label in plan["workloads"]:
         if label == "calib":
+            continue
+        if label.startswith("x_"):  # experiments (tuning-library kernels): their own file, never pmc_traffic.json
+            key, sub = label.split("/")
+            t = entry(label)
+            t["per_kernel"] = {fam: entry(label, fam) for fam in sorted({family(k) for c in fetch[label] for k, _ in c})}
+            for v in t["per_kernel"].values():
+                v.pop("source", None)
+                v.pop("method", None)
+            exper.setdefault(key, {})[sub] = t
             continue
         if label.startswith("tx_"):
             key, sub = label.split("/")
@@ -179,6 +189,9 @@ def main():
         os.makedirs(args.profiles, exist_ok=True)
         with open(os.path.join(args.profiles, "pmc_entries.json"), "w") as f:
             json.dump(new, f, indent=1)
+        if exper:
+            with open(os.path.join(args.profiles, "experiments.json"), "w") as f:
+                json.dump(exper, f, indent=1)
         with open(os.path.join(args.profiles, "gates.json"), "w") as f:
             json.dump({"lib_sha256": plan["lib_sha256"], "gates": plan["gates"]}, f, indent=1)
         for st in glob.glob(os.path.join(args.root, "trace", "**", "*kernel_stats.csv"), recursive=True):
@@ -187,6 +200,9 @@ def main():
                    if k.startswith("tx_") else (v["hbm_bytes_per_launch"], v["traffic_over_algorithmic"]))
                for k, v in new.items()}
     print(json.dumps(summary, indent=1))
+    if exper:
+        print(json.dumps({k: {s: (e["hbm_bytes_per_launch"], e["ea_write_requests_per_frame"], e["ea_write_64B_per_frame"],
+                                  e.get("trace_kernel_us_median")) for s, e in v.items()} for k, v in exper.items()}, indent=1))
 
 
 if __name__ == "__main__":

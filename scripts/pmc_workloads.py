@@ -7,11 +7,13 @@ counter CSV (Dispatch_Id order) and turns each label's per-call counters into th
 profiles/pmc_traffic.json.  The workloads are bench.py's (same generators, strides, rotating resident batches);
 every batch is gated against the committed digests (or the oracle) so the counters are of a correct run.
 
-  python3 scripts/pmc_workloads.py --out DIR [--uncached] [--only LABEL,...]
+  python3 scripts/pmc_workloads.py --out DIR [--uncached] [--only LABEL,...] [--tx-variants V,...]
 
 --uncached adds the round-5 experiment: the C2 ring in uncached device memory
 (hipExtMallocWithFlags(hipDeviceMallocUncached)), pn_match_streams and the release-path classify on it, records
-compared with the same calls on ordinary memory."""
+compared with the same calls on ordinary memory.  --tx-variants adds the TX fill's tuning variants (the
+measurement-only library, scripts/tx_variants.py's numbering) at both layouts, labels x_tx_v<V>/frame_off_<off>:
+experiments, kept out of profiles/pmc_traffic.json by the summariser."""
 import argparse
 import ctypes
 import hashlib
@@ -64,6 +66,7 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--uncached", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--tx-variants", default="")
     args = ap.parse_args()
     only = set(filter(None, args.only.split(",")))
     import torch
@@ -105,7 +108,7 @@ def main():
     ctx.set_conn_table(pa.gen_conn_table(p2))
     res = torch.empty(N * 16, dtype=torch.uint8, device="cuda")
     sink = torch.zeros(4096, dtype=torch.int32, device="cuda")
-    run("calib", ["calib_stream_read"], lambda d: tn.calib_stream_read(ctx, d, d.numel(), sink, stream), c2[:1], calls=6)
+    run("calib", ["calib_stream_read_kernel"], lambda d: tn.calib_stream_read(ctx, d, d.numel(), sink, stream), c2[:1], calls=6)
     plan["workloads"]["calib"] = {"bytes_per_launch": N * STRIDE}
     if want("c2_n1048576"):
         run("c2_n1048576", ["rx_classify_kernel"], lambda d: ctx.classify(d, STRIDE, FRAME_OFF, N, res, stream), c2)
@@ -275,6 +278,41 @@ def main():
                                                 "scrambled, 2 rotating batches"}
         ctx.close()
         del bufs
+        torch.cuda.empty_cache()
+
+    # ---- experiments: TX fill variants of the tuning library (same frames and rotation as the product's TX legs)
+    TX_FAMS = {40: ["tx_fill_kernel", "tx_patch_kernel"], 50: ["tx_fill_kernel", "tx_patch_wt_kernel"],
+               51: ["tx_fill_kernel", "tx_patch_wt_kernel"], 52: ["tx_fill_kernel", "tx_patch_kernel", "tx_l2_release_kernel"],
+               32: ["tx_fill_kernel", "tx_patch_sector_kernel"], 41: ["tx_fill_kernel"]}
+    tx_vs = [int(v) for v in filter(None, args.tx_variants.split(","))]
+    for off in (2, 14) if tx_vs else ():
+        ctx = pa.RxContext(dev)
+        bufs = []
+        for b in range(2):
+            pa.gen_frames(p2, N, STRIDE, off, first_index=b * N, threads=16, out=host)
+            d = torch.from_numpy(host.reshape(-1)).cuda()
+            v = d.view(N, STRIDE)
+            v[:, off + 24:off + 26] = 0x5A
+            v[:, off + 50:off + 52] = 0xA5
+            bufs.append(d)
+        ref = bufs[0].clone()
+        ctx.tx_fill(ref, STRIDE, off, N, None, pa.PN_TX_TCP, stream)
+        seq.calls.append(["gate", ["tx_fill_kernel", "tx_patch_kernel"]])
+        for var in tx_vs:
+            label = f"x_tx_v{var}/frame_off_{off}"
+            run(label, TX_FAMS[var], lambda d: tn.tx_fill_variant(ctx, d, STRIDE, off, N, None, var, stream), bufs, calls=8)
+            chk = bufs[0].clone()
+            chk.view(N, STRIDE)[:, off + 24:off + 26] = 0x5A
+            chk.view(N, STRIDE)[:, off + 50:off + 52] = 0xA5
+            tn.tx_fill_variant(ctx, chk, STRIDE, off, N, None, var, stream)
+            seq.calls.append(["gate", TX_FAMS[var]])
+            torch.cuda.synchronize()
+            plan["gates"][label] = bool(torch.equal(chk, ref))
+            plan["workloads"][label] = {"algorithmic_bytes_per_launch": 1504 * N,
+                                        "workload": f"TX fill tuning variant {var} at frame_off {off} (experiment)"}
+            del chk
+        ctx.close()
+        del bufs, ref
         torch.cuda.empty_cache()
 
     plan["calls"] = seq.calls

@@ -20,7 +20,8 @@ NAMES = {0: "inplace_u16_stores", 2: "inplace_tile_wb128_sc1", 9: "ABL_nowrite",
          32: "phase2_sector_plain", 33: "phase2_sector_nt",
          35: "PROBE_full64B_write_nofetch", 36: "PROBE_full128B_write_nofetch", 40: "product_shape_twophase",
          41: "product_shape_inplace", 42: "product_shape_twophase_skip_empty_loads",
-         43: "product_shape_twophase_concurrent_window"}
+         43: "product_shape_twophase_concurrent_window", 50: "product_shape_phase2_u16_writethrough",
+         51: "product_shape_phase2_sector64_writethrough", 52: "product_shape_phase2_then_l2_release"}
 TIMING_ONLY = {9, 13, 14, 15, 16, 35, 36}
 
 
