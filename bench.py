@@ -158,42 +158,54 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
             if el >= secs:
                 return passes * sample / el, passes * wire * 8 / el / 1e9, passes
 
-    def measure(fn, th, secs, reps=5):
-        """median of `reps` timed passes of >= secs each (Gbit/s), with min / max"""
-        runs = [one_pass(fn, th, secs) for _ in range(reps)]
+    def stats(runs, th):
         gb = sorted(r[1] for r in runs)
         fr = sorted(r[0] for r in runs)
         return {"value": round(statistics.median(gb), 2), "unit": "Gbit/s",
                 "mframes_per_s": round(statistics.median(fr) / 1e6, 3), "cores": th,
-                "min": round(gb[0], 2), "max": round(gb[-1], 2), "reps": reps, "passes": sum(r[2] for r in runs)}
+                "min": round(gb[0], 2), "max": round(gb[-1], 2), "reps": len(runs), "passes": sum(r[2] for r in runs)}
+
+    def interleaved(legs, reps):
+        """legs: {name: (fn, threads, seconds)}; the reps of all legs round-robin (rep 1 of every leg, then rep 2,
+        ...), so a change in the host's load over the leg lands on every figure alike; median / min / max each"""
+        runs = {k: [] for k in legs}
+        for _ in range(reps):
+            for k, (fn, th, secs) in legs.items():
+                runs[k].append(one_pass(fn, th, secs))
+        return {k: stats(runs[k], legs[k][1]) for k in legs}
 
     counts = sorted({c for c in (8, 16, 32, 64, threads) if c <= threads})
-
-    def swept(fn, sweep_s, head_s):
-        # the box's share of a large host can be smaller than its affinity mask: probe a few thread counts up to
-        # the available cores and measure at the fastest (stated in the line)
-        sweep = {t: measure(fn, t, sweep_s, reps=3)["value"] for t in counts}
-        best = max(sweep, key=sweep.get)
-        head = measure(fn, best, head_s)
-        remeasured = False
-        if abs(head["value"] - sweep[best]) > 0.15 * max(head["value"], sweep[best]):
-            remeasured = True
-            sweep[best] = measure(fn, best, sweep_s, reps=3)["value"]
-            head = measure(fn, best, head_s)
-        head["thread_sweep_gbit_per_s"] = sweep
-        head["sweep_point_at_cores"] = sweep[best]
-        head["consistent_with_sweep"] = abs(head["value"] - sweep[best]) <= 0.15 * max(head["value"], sweep[best])
-        head["remeasured"] = remeasured
-        return head
-
     head_fn = reference if ref is not None else port
     kind = "reference" if ref is not None else "port"
-    c1 = c1_socket_loopback()
-    head = swept(head_fn, budget_s * 0.02, budget_s * 0.06)
-    single = measure(head_fn, 1, budget_s * 0.025)
     rel_fn = reference_release if ref is not None else (lambda th: port(th, True))
-    rel = swept(rel_fn, budget_s * 0.01, budget_s * 0.04)
-    rel_1 = measure(rel_fn, 1, budget_s * 0.02)
+    c1 = c1_socket_loopback()
+
+    def sweep_of(fn, secs):
+        # the box's share of a large host can be smaller than its affinity mask: probe a few thread counts up to
+        # the available cores and measure at the fastest (stated in the line)
+        r = interleaved({t: (fn, t, secs) for t in counts}, 3)
+        return {t: v["value"] for t, v in r.items()}
+
+    sweep, sweep_rel = sweep_of(head_fn, budget_s * 0.02), sweep_of(rel_fn, budget_s * 0.01)
+    best, best_rel = max(sweep, key=sweep.get), max(sweep_rel, key=sweep_rel.get)
+    legs = {"head": (head_fn, best, budget_s * 0.06), "single": (head_fn, 1, budget_s * 0.025),
+            "rel": (rel_fn, best_rel, budget_s * 0.04), "rel_1": (rel_fn, 1, budget_s * 0.02)}
+    if ref is not None:
+        legs.update({"port": (port, best, budget_s * 0.012), "port_1": (port, 1, budget_s * 0.012),
+                     "port_rel_1": (lambda th: port(th, True), 1, budget_s * 0.01)})
+    m = interleaved(legs, 5)
+    remeasured = False
+    for key, sw, b, fn, secs in (("head", sweep, best, head_fn, budget_s * 0.06),
+                                 ("rel", sweep_rel, best_rel, rel_fn, budget_s * 0.04)):
+        if abs(m[key]["value"] - sw[b]) > 0.15 * max(m[key]["value"], sw[b]):  # re-measure both, once
+            remeasured = True
+            r = interleaved({"sweep_point": (fn, b, secs / 3), key: (fn, b, secs)}, 5)
+            sw[b] = r["sweep_point"]["value"]
+            m[key] = r[key]
+    for key, sw, b in (("head", sweep, best), ("rel", sweep_rel, best_rel)):
+        m[key].update({"thread_sweep_gbit_per_s": sw, "sweep_point_at_cores": sw[b], "remeasured": remeasured,
+                       "consistent_with_sweep": abs(m[key]["value"] - sw[b]) <= 0.15 * max(m[key]["value"], sw[b])})
+    head, single, rel, rel_1 = m["head"], m["single"], m["rel"], m["rel_1"]
     code = ("the reference's own Core.h / TcpConn.h code (oracle/ref_core.cc ref_bench_batch, compiled from "
             "/root/reference by oracle/ref.mk, g++ -O3 -march=x86-64-v3)" if ref is not None else
             "'ref parse + checksum' port (oracle/pn_oracle.c orc_refsum_batch, -O3 -march=x86-64-v3)")
@@ -202,7 +214,7 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
         "kind": kind,
         "sample": f"Core::checksum + pollNet's key/probe/TIME_WAIT test + onPack's payload head per frame, {code}, "
                   f"over {sample} frames of the same workload; median of {head['reps']} timed passes (min/max beside "
-                  f"it); contiguous index shards over {head['cores']} threads, the fastest of a sweep up to this "
+                  f"it), the passes of every CPU figure interleaved round-robin; contiguous index shards over {head['cores']} threads, the fastest of a sweep up to this "
                   f"process's {cpu_threads()} available cores (CPU affinity {len(os.sched_getaffinity(0))}, cgroup "
                   f"CPU quota {cgroup_cpu_quota()}, machine {os.cpu_count()})",
         "single_thread": single,
@@ -216,9 +228,7 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
         "c1_socket_loopback_ref": c1,
     })
     if ref is not None:
-        p_mt = measure(port, head["cores"], budget_s * 0.012)
-        p_1 = measure(port, 1, budget_s * 0.012)
-        p_rel1 = measure(lambda th: port(th, True), 1, budget_s * 0.01)
+        p_mt, p_1, p_rel1 = m["port"], m["port_1"], m["port_rel_1"]
         out["port"] = {"value": p_mt["value"], "min": p_mt["min"], "max": p_mt["max"], "unit": "Gbit/s",
                        "mframes_per_s": p_mt["mframes_per_s"], "cores": head["cores"],
                        "single_thread_gbit_per_s": p_1["value"], "release_path_single_thread_gbit_per_s": p_rel1["value"],
