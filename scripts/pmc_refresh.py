@@ -136,7 +136,7 @@ def main():
              "ea_write_requests_per_frame": round(cnt["TCC_EA0_WRREQ_sum"] / n, 4),
              "ea_write_64B_per_frame": round(w64 / n, 4),
              "calls_measured": len(fetch[label]),
-             "kernels": codehash.matching(names, None if not label.startswith("x_") else TUNING)}
+             "kernels": codehash.matching(names, TUNING if label.startswith("x_") else None)}
         if fam is None:
             algo = w["algorithmic_bytes_per_launch"]
             e["algorithmic_bytes_per_launch"] = algo
@@ -159,8 +159,8 @@ def main():
     for label in plan["workloads"]:
         if label == "calib":
             continue
-        if label.startswith("x_"):  # experiments (tuning-library kernels): their own file, never pmc_traffic.json
-            key, sub = label.split("/")
+        if label.startswith(("x_", "uncached_")):  # experiments: their own file, never pmc_traffic.json
+            key, sub = label.split("/") if "/" in label else (label, "all")
             t = entry(label)
             t["per_kernel"] = {fam: entry(label, fam) for fam in sorted({family(k) for c in fetch[label] for k, _ in c})}
             for v in t["per_kernel"].values():
