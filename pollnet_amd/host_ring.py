@@ -66,10 +66,32 @@ def cpu_affinity(cpus):
         os.sched_setaffinity(0, old)
 
 
+def room_for(nbytes: int, shm_dir: str = "/dev/shm"):
+    """None if a shared segment of nbytes fits both the shared-memory filesystem's free space and half the host's
+    available memory, else the reason.  A tmpfs that fills up under a mapping kills the writer with SIGBUS, which
+    no handler turns into an error, so the size is checked before anything is created."""
+    try:
+        st = os.statvfs(shm_dir)
+        free = st.f_bavail * st.f_frsize
+    except OSError as ex:
+        return f"{shm_dir}: {ex}"
+    if nbytes > free:
+        return f"{shm_dir} has {free / 2**30:.1f} GiB free, the ring needs {nbytes / 2**30:.1f} GiB"
+    try:
+        with open("/proc/meminfo") as f:
+            avail = next(int(ln.split()[1]) * 1024 for ln in f if ln.startswith("MemAvailable:"))
+        if nbytes > avail // 2:
+            return f"the ring ({nbytes / 2**30:.1f} GiB) exceeds half the host's available memory ({avail / 2**30:.1f} GiB)"
+    except (OSError, StopIteration, ValueError):
+        pass
+    return None
+
+
 class SharedHostRing:
     """world * n_per_rank slots of `stride` bytes, then world * n_per_rank 16-B records, in one POSIX
     shared-memory segment.  Collective over `dist` (torch.distributed or None for one process): rank 0
-    creates the segment and broadcasts its name; every rank maps all of it."""
+    checks the room (room_for), creates the segment and broadcasts its name; every rank maps all of it.  When
+    there is no room every rank raises the same RuntimeError (nobody is left waiting)."""
 
     def __init__(self, dist, rank: int, world: int, n_per_rank: int, stride: int):
         import secrets
@@ -78,11 +100,19 @@ class SharedHostRing:
         self.rank, self.world, self.n, self.stride = rank, world, n_per_rank, stride
         self.slot_bytes = world * n_per_rank * stride
         size = self.slot_bytes + world * n_per_rank * RECORD_BYTES
-        name = [f"pn_ring_{secrets.token_hex(6)}" if rank == 0 else None]
+        name = [None, None]
         if rank == 0:
-            self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=size)
+            name[1] = room_for(size)
+            if name[1] is None:
+                try:
+                    name[0] = f"pn_ring_{secrets.token_hex(6)}"
+                    self.shm = shared_memory.SharedMemory(name=name[0], create=True, size=size)
+                except OSError as ex:
+                    name = [None, f"creating the shared ring: {ex!r}"]
         if dist is not None and world > 1:
             dist.broadcast_object_list(name, src=0)
+        if name[0] is None:
+            raise RuntimeError(f"no shared host ring: {name[1]}")
         if rank != 0:
             self.shm = shared_memory.SharedMemory(name=name[0])
             from multiprocessing import resource_tracker

@@ -402,3 +402,17 @@ def test_bench_e2e_host_ring_two_ranks():
     assert e2e["frames_per_rank"] == 1 << 21
     assert line["summary"]["e2e_host_ring_records_ok"] is True
     assert list(line)[-1] == "summary"
+
+
+def test_shared_host_ring_refuses_what_does_not_fit():
+    """A ring larger than /dev/shm's free space (or half the host's available memory) is refused before anything is
+    created (a tmpfs filling up under a mapping would kill the writer with SIGBUS); bench.py then skips the e2e leg."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    from pollnet_amd.host_ring import SharedHostRing, room_for
+
+    assert room_for(1 << 20) is None
+    assert "GiB" in room_for(1 << 50)
+    with pytest.raises(RuntimeError, match="no shared host ring"):
+        SharedHostRing(None, 0, 1, 1 << 40, 2048)
