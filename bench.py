@@ -131,6 +131,11 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
 
     threads = cpu_threads()
     sample = min(n, 1 << 18)  # 256 Ki frames (~0.4 GB of frame bytes)
+    # a private copy of the sample: numpy backs a large array with transparent huge pages (madvise), where the
+    # shared ring's shard is tmpfs with 4-KiB pages; on the pool's EPYC hosts the reference's own code reads that
+    # 1.7-2.1x slower, the port 1.1-1.3x (scripts/cpu_placement_probe.py, profiles/r05/cpu_placement.json) -- the
+    # baseline takes the placement that is fastest for the reference
+    slots = np.array(slots[:sample], copy=True)
     wire = pa.wire_bytes(slots, STRIDE, FRAME_OFF, sample)
     ref = None
     try:
@@ -213,7 +218,7 @@ def cpu_baseline(slots, n, entries, mask, max_conn, budget_s, gpu_records=None):
     out.update({
         "kind": kind,
         "sample": f"Core::checksum + pollNet's key/probe/TIME_WAIT test + onPack's payload head per frame, {code}, "
-                  f"over {sample} frames of the same workload; median of {head['reps']} timed passes (min/max beside "
+                  f"over {sample} frames of the same workload (a private, huge-page-backed copy); median of {head['reps']} timed passes (min/max beside "
                   f"it), the passes of every CPU figure interleaved round-robin; contiguous index shards over {head['cores']} threads, the fastest of a sweep up to this "
                   f"process's {cpu_threads()} available cores (CPU affinity {len(os.sched_getaffinity(0))}, cgroup "
                   f"CPU quota {cgroup_cpu_quota()}, machine {os.cpu_count()})",
