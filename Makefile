@@ -34,6 +34,7 @@ TXSMALLBENCH = bench/bench_tx_small
 # (defined before `all`: make expands a rule's prerequisites where the rule is read)
 SIGBENCH = bench/bench_signal
 STREAMBENCH = bench/bench_streams
+DOORBENCH = bench/bench_doorbell
 RINGTEST = tests/cpp/test_rx_ring
 STREAMTEST = tests/cpp/test_tcp_stream
 GPUSTREAMTEST = tests/cpp/test_gpu_tcp_stream
@@ -61,7 +62,7 @@ CONN_INCS = $(addprefix oracle/_ref/,conn_tcpconn.inc conn_tcpserver.inc conn_ef
 HAVE_REF_TEXT = $(or $(wildcard $(REFDIR)/example/tcpserver.cc),$(and $(wildcard oracle/_ref/tcpserver_handler.inc),$(wildcard oracle/_ref/tcpclient_handler.inc)))
 REF_TESTS = $(if $(HAVE_REF_TEXT),$(SERVERTEST) $(CLISRVTEST) $(REFSERVERTEST) $(REFCONNTEST) $(REFCLIENTTEST))
 
-all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(STREAMBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST) $(TXHOSTTEST)
+all: $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) ref $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(STREAMBENCH) $(DOORBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(REF_TESTS) $(PEERTEST) $(TXHOSTTEST)
 
 # GpuTcpServer (pollnet's EfviTcpServer surface) running the reference example's own handler
 # (oracle/_ref/tcpserver_handler.inc, extracted by oracle/ref.mk) on the GPU vs a sequential twin
@@ -148,6 +149,10 @@ $(TXSMALLBENCH): bench/bench_tx_small.cpp $(HDRS) include/pollnet_amd_tuning.h $
 $(SIGBENCH): bench/bench_signal.cpp $(HDRS) $(LIB) $(GEN_LIB)
 	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_gen -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
 
+# GPU round-trip latency floor: launch per request vs a resident kernel polling a doorbell (tuning library)
+$(DOORBENCH): bench/bench_doorbell.cpp $(HDRS) include/pollnet_amd_tuning.h $(LIB) $(TUNING_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -lpollnet_amd_tuning -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
+
 # the sniffer path end to end: GpuTcpStreams::poll vs every stream's filterPacket + handlePacket on one core
 $(STREAMBENCH): bench/bench_streams.cpp include/pollnet_amd/tcp_stream.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB)
 	$(HOSTHIP) -O3 -std=c++17 -Wall -o $@ $< -Lpollnet_amd -lpollnet_amd -Wl,-rpath,'$$ORIGIN/../pollnet_amd'
@@ -195,6 +200,6 @@ ref:
 	@if [ -d $(REFDIR) ]; then $(MAKE) -C oracle -f ref.mk REFDIR=$(REFDIR); else echo "no $(REFDIR): using prebuilt oracle/_ref"; fi
 
 clean:
-	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(STREAMBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST) $(REFSERVERTEST) $(REFCONNTEST) $(REFCLIENTTEST)
+	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(STREAMBENCH) $(DOORBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST) $(REFSERVERTEST) $(REFCONNTEST) $(REFCLIENTTEST)
 
 .PHONY: all ref clean

@@ -1,0 +1,75 @@
+// Latency floor of a GPU round trip from the host (round 5): a value written to pinned host memory and
+// answered by the GPU into pinned host memory, the host spinning on the answer.
+//   launch:     one kernel launch per request (answers the value and ends) -- what pn_classify_notify pays
+//   resident:   one resident kernel polling the doorbell (pn_test_doorbell_echo), with / without s_sleep
+// Prints one JSON line: median / p90 microseconds per round trip.   argv: iterations (2000)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../include/pollnet_amd.h"
+#include "../include/pollnet_amd_tuning.h"
+
+using Clock = std::chrono::steady_clock;
+
+static void stats(const char* name, std::vector<double>& us, bool last) {
+  std::sort(us.begin(), us.end());
+  std::printf("\"%s\": {\"us_median\": %.2f, \"us_p10\": %.2f, \"us_p90\": %.2f}%s", name, us[us.size() / 2],
+              us[us.size() / 10], us[us.size() * 9 / 10], last ? "" : ", ");
+}
+
+static bool spin(volatile uint32_t* w, uint32_t v) {
+  const auto t0 = Clock::now();
+  while (__atomic_load_n(w, __ATOMIC_ACQUIRE) != v)
+    if (Clock::now() - t0 > std::chrono::seconds(2)) return false;
+  return true;
+}
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+  uint32_t* words = nullptr;
+  if (hipHostMalloc((void**)&words, 256, hipHostMallocDefault) != hipSuccess) return 2;
+  uint32_t* bell = words;
+  uint32_t* echo = words + 32; // another 128-B line
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 2;
+  std::printf("{\"bench\": \"doorbell_round_trip\", \"iterations\": %d, ", iters);
+  // launch per request
+  {
+    std::vector<double> us;
+    for (int i = 1; i <= iters + 50; i++) {
+      __atomic_store_n(bell, (uint32_t)i, __ATOMIC_RELEASE);
+      const auto t0 = Clock::now();
+      if (pn_test_doorbell_echo(bell, echo, 100, 1, 0, s)) return 3;
+      if (!spin(echo, (uint32_t)i)) return 4;
+      if (i > 50) us.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return 5;
+    stats("launch_per_request", us, false);
+  }
+  for (int sl = 0; sl < 2; sl++) {
+    __atomic_store_n(bell, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(echo, 0u, __ATOMIC_RELEASE);
+    if (pn_test_doorbell_echo(bell, echo, 200, 0, sl, s)) return 3; // ends 200 ms after the last request
+    std::vector<double> us;
+    bool ok = true;
+    for (int i = 1; i <= iters + 50 && ok; i++) {
+      const auto t0 = Clock::now();
+      __atomic_store_n(bell, (uint32_t)i, __ATOMIC_RELEASE);
+      ok = spin(echo, (uint32_t)i);
+      if (i > 50) us.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+    }
+    __atomic_store_n(bell, 0xFFFFFFFFu, __ATOMIC_RELEASE); // stop
+    if (hipStreamSynchronize(s) != hipSuccess) return 5;
+    if (!ok) return 6;
+    stats(sl ? "resident_sleep" : "resident_spin", us, sl == 1);
+  }
+  std::printf("}\n");
+  (void)hipStreamDestroy(s);
+  (void)hipHostFree(words);
+  return 0;
+}

@@ -12,8 +12,8 @@
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
 //   argv: n_flows (256)  polls (400)  [cpu|quick]   prints one JSON line; exit 0 = all data delivered
-//         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512, GPU
-//         pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
+//         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512 (also pipelined),
+//         GPU pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
 //         checksum summed) — bench.py's secondary.tcp_server_poll)
 #include <arpa/inet.h>
 
@@ -284,6 +284,10 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
     leg("gpu_rxbatch_512_release_path", runOne<512, GpuBackend>(n_flows, polls, false));
     leg("gpu_rxbatch_16384_pipelined_release_path", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4, false));
+    // the reference's batch in throughput mode (Conf::RxPipeline: each poll's frames dispatched in the next poll,
+    // their classify overlapped with this poll's host work), both paths
+    leg("gpu_rxbatch_512_pipelined", runOne<512, GpuBackend, 0, true>(n_flows, polls));
+    leg("gpu_rxbatch_512_pipelined_release_path", runOne<512, GpuBackend, 0, true>(n_flows, polls, false));
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     // the same sequential server with the discard off: the reference's release build (no checksum summed per frame)
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));

@@ -53,6 +53,12 @@ int pn_match_streams_variant(pn_ctx* ctx, const void* frames, uint32_t slot_stri
  * pinned host memory.  Unrelated work in flight on a foreign stream (tests/test_gpu_notify.py). */
 int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max_ms, void* stream);
 
+/* Latency probe (no ctx; bench/bench_doorbell): one lane copies each new value of *bell_host to *echo_host (both
+ * pinned host memory) until the value 0xFFFFFFFF or max_idle_ms (<= 10000) without a new value; once != 0: answer
+ * the current value and end.  sleep != 0: s_sleep between polls. */
+int pn_test_doorbell_echo(const uint32_t* bell_host, uint32_t* echo_host, uint32_t max_idle_ms, int once, int sleep,
+                          void* stream);
+
 /* ---- A/B variants (built by default, TUNING=1; ids documented at their definitions) ---- */
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                         void* results_dev, void* stream, int variant);

@@ -38,6 +38,33 @@ __global__ __launch_bounds__(64) void spin_wait_kernel(const uint32_t* go, uint3
   __hip_atomic_store(done, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Latency probe (round 5, bench/bench_doorbell): how fast can a resident kernel answer the host?  One lane
+// watches *bell (pinned host memory) and copies every new value to *echo; it ends at the value 0xFFFFFFFF or
+// after max_idle_ticks of the device wall clock without a new value (always exits).  once = 1: answer the
+// value already there and end (the launch-per-request form the product uses today).
+__global__ __launch_bounds__(64) void doorbell_echo_kernel(const uint32_t* bell, uint32_t* echo, uint64_t max_idle_ticks,
+                                                            uint32_t once, uint32_t sleep) {
+  if (threadIdx.x != 0) return;
+  uint32_t last = 0;
+  uint64_t t_last = wall_clock64();
+  for (;;) {
+    // relaxed in the loop (a system-scope load reads memory; an acquire would invalidate the caches every
+    // iteration); the acquire fence once a new value has arrived
+    const uint32_t v = __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v == 0xFFFFFFFFu) break;
+    if (v != last || once) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      last = v;
+      __hip_atomic_store(echo, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (once) break;
+      t_last = wall_clock64();
+    } else if (wall_clock64() - t_last > max_idle_ticks) {
+      break;
+    }
+    if (sleep) __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 // Read-only ceilings for the slot layout (no header work, no arithmetic): each wave
 // streams the first `bytes` of each of its 64 slots with the RX kernel's 1-KiB
 // buffer loads, 8 slots per batch.  STORE = 16 / 8: plus a per-slot record store
@@ -456,6 +483,20 @@ int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max
                      (uint64_t)khz * max_ms);
   e = hipGetLastError();
   return e == hipSuccess ? PN_OK : hip_err(nullptr, e, "spin_wait launch");
+}
+
+int pn_test_doorbell_echo(const uint32_t* bell_host, uint32_t* echo_host, uint32_t max_idle_ms, int once, int sleep,
+                          void* stream) {
+  if (!bell_host || !echo_host || max_idle_ms == 0 || max_idle_ms > 10000)
+    return set_err(nullptr, PN_EINVAL, "pn_test_doorbell_echo: bell/echo must be set, max_idle_ms in [1, 10000]");
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess || khz <= 0) return hip_err(nullptr, e, "wall clock rate");
+  hipLaunchKernelGGL(doorbell_echo_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, bell_host, echo_host,
+                     (uint64_t)khz * max_idle_ms, (uint32_t)(once != 0), (uint32_t)(sleep != 0));
+  e = hipGetLastError();
+  return e == hipSuccess ? PN_OK : hip_err(nullptr, e, "doorbell_echo launch");
 }
 
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream) {
