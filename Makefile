@@ -6,7 +6,8 @@ HIPFLAGS = --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
 CFLAGS_ORACLE = -O3 -march=x86-64-v3 -fPIC -Wall -std=c11
 
 LIB = pollnet_amd/libpollnet_amd.so
-SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip pollnet_amd/csrc/conn_table.cpp
+SRCS = pollnet_amd/csrc/rx_kernel.hip pollnet_amd/csrc/rx_service.hip pollnet_amd/csrc/stream_kernel.hip pollnet_amd/csrc/tx_kernel.hip \
+  pollnet_amd/csrc/conn_table.cpp
 # the seeded workload generator (tests, bench): its own library, outside the product ABI
 GEN_LIB = pollnet_amd/libpollnet_amd_gen.so
 HDRS = include/pollnet_amd.h

@@ -265,6 +265,29 @@ int pn_classify_notify(pn_ctx* ctx, const void* frames, uint32_t slot_stride, ui
 int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t frame_off, uint32_t n,
                       const uint16_t* lens, uint32_t mode, void* stream, uint32_t* done_word, uint32_t token);
 
+/* ---- resident classify service: no launch per batch (round 5) ----
+ * pn_service_open launches a kernel that stays on the GPU (PN_SERVICE_WAVES one-wave workgroups, on a stream of its
+ * own) and classifies every batch the host posts afterwards, with the same code and records as pn_classify on the
+ * layout given at open (strided slots).  A post is a few stores into pinned host memory that the kernel polls, so a
+ * batch starts ~1-2 us after it is posted instead of a launch's ~7 us (bench/bench_doorbell).
+ *   pn_service_post: frames (pinned host or device memory, 16-B aligned), n in [1, PN_SERVICE_MAX_FRAMES], results
+ *     (pinned host or device memory, 16-B aligned).  The ctx's conn table and pn_set_verify setting at the post are
+ *     used.  At most two posts outstanding; non-blocking.
+ *   pn_service_wait: spins until the last post's records are visible to the host (as pn_classify_notify's word).
+ *   pn_service_close: waits for outstanding posts, stops the kernel, frees the service (before pn_close).
+ * After idle_ms (1..10000) without a post the kernel ends by itself (every wait inside it has a wall-clock limit);
+ * the next post relaunches it.  pn_set_conn_table may be called with at most one post outstanding (the table is
+ * double-buffered; the post in flight keeps reading its buffer).  One thread per service, as per ctx.
+ * Replaces the launch of the reference's per-poll work with its own busy-poll style (Core.h:494-498). */
+typedef struct pn_service pn_service;
+#define PN_SERVICE_WAVES 64u
+#define PN_SERVICE_MAX_FRAMES (1u << 20)
+#define PN_SERVICE_STOP 0xFFFFFFFFu /* internal: the stop post */
+int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, pn_service** out);
+int pn_service_post(pn_service* svc, const void* frames, uint32_t n, void* results);
+int pn_service_wait(pn_service* svc);
+int pn_service_close(pn_service* svc);
+
 /* Wait until every launch this ctx issued (on any stream) has finished: synchronizes each
  * stream launched on since the last pn_set_conn_table, and the events that set recorded
  * for the launches before it.  Not a device-wide wait. */

@@ -24,6 +24,7 @@ from .rx import (  # noqa: F401
     ConnTable,
     PollnetError,
     RxContext,
+    RxService,
     conn_hash_key,
     device_count,
     gen_conn_table,

@@ -1,0 +1,347 @@
+// Resident classify service (round 5): one launch, then the host posts batches through pinned host
+// memory and the kernel -- already on the GPU -- classifies each with the production code (classify_group,
+// rx_classify.hpp), without a launch per batch.  A launch costs ≈7 µs of host-to-GPU round trip; a resident wave
+// answering a doorbell ≈2.7 µs (bench/bench_doorbell, profiles/r05/latency/).
+//
+// Protocol.  Two mailbox slots of one 64-B line each (pinned host memory; post k uses slot k & 1).  The host
+// fills a slot's fields, its first word (gen) and last word (seq) = k, seq last with a release store.  Wave 0 of
+// the kernel polls only the slot of the next post (one 64-B read per poll: 16 lanes x 4 B), accepts it when gen
+// and seq both read k, copies it to device memory and publishes k to the other waves through a device word.  Each
+// wave classifies its groups of the batch, makes its records system-visible and counts itself done; the last
+// resets the counter and stores k to the host's done word.  Wave 0 looks for post k + 1 only once post k is done.
+// A post whose n is PN_SERVICE_STOP ends every wave.  Every wait has a device-wall-clock limit: after idle_ms
+// without a post wave 0 publishes "idle", stores the launch's epoch to the host's exit word and ends, and the
+// others end on seeing it (or at their own limit); the host relaunches on its next post.  So the kernel always
+// ends.  Only vector memory operations (global loads / stores / one atomic add).
+#include <chrono>
+
+#include "rx_classify.hpp"
+
+namespace {
+using pn_internal::hip_err;
+using pn_internal::set_err;
+
+struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its device copy
+  uint32_t gen;              // = seq, stored first
+  uint32_t n;                // frames, or PN_SERVICE_STOP
+  uint32_t verify;           // pn_set_verify's setting at the post
+  uint32_t max_conn;
+  const uint8_t* frames;
+  pn_result* out;
+  const pn_conn_entry* tbl;
+  uint64_t mask;
+  uint32_t n_entries;
+  uint32_t pad0, pad1;
+  uint32_t seq; // stored last (release)
+};
+static_assert(sizeof(SvcPost) == 64, "one line per post");
+
+constexpr uint32_t kSvcIdle = 0xFFFFFFFFu; // published on the device word when wave 0 ends for lack of posts
+
+struct alignas(64) SvcDev { // device memory, set by the host before every launch
+  uint32_t seq;             // the post the waves may work on (wave 0 publishes), or kSvcIdle
+  uint32_t pad0[15];
+  uint32_t count; // waves done with the current post
+  uint32_t done;  // the last post every wave finished
+  uint32_t pad1[14];
+  SvcPost post[2];
+};
+
+struct SArgs {
+  const SvcPost* mail; // host: the two mailbox slots
+  uint32_t* done_word; // host: the last completed post
+  uint32_t* exit_word; // host: the launch's epoch once it ended for lack of posts
+  SvcDev* dev;
+  uint64_t idle_ticks; // device wall clock
+  uint32_t epoch;
+  uint32_t last; // the post completed before this launch
+  uint32_t stride, ipa_off, avail;
+};
+
+__device__ __forceinline__ uint32_t svc_fpw(uint32_t n, uint32_t waves) {
+  uint32_t fpw = 8; // a small batch over more waves (latency); 64 once the waves are full
+  while (fpw < kFramesPerWave && (n + fpw - 1) / fpw > waves) fpw <<= 1;
+  return fpw;
+}
+
+template <int MIS, int COOP>
+__global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
+  const int lane = threadIdx.x;
+  const uint32_t w = blockIdx.x, W = gridDim.x;
+  uint32_t last = s.last;
+  uint64_t t0 = wall_clock64();
+  for (;;) {
+    const uint32_t want = last + 1;
+    if (w == 0) {
+      // the next post's slot, one 64-B read: lane i holds word i
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(s.mail + (want & 1));
+      const uint32_t v = lane < 16 ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+      const uint32_t gen = __builtin_amdgcn_readlane(v, 0), seq = __builtin_amdgcn_readlane(v, 15);
+      if (gen == want && seq == want) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[want & 1])[lane] = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) __hip_atomic_store(&s.dev->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
+          if (lane == 0) {
+            __hip_atomic_store(&s.dev->seq, kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+    } else {
+      const uint32_t d = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      if (d == kSvcIdle) return;
+      if (d != want) {
+        // wave 0 publishes at most one post past the last completed one, so d is want or want - 1; the limit is
+        // wave 0's plus a margin (a safety net: wave 0 always publishes kSvcIdle first)
+        if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) return;
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    const SvcPost p = s.dev->post[want & 1];
+    if (p.n == PN_SERVICE_STOP) return;
+    KArgs a;
+    a.frames = p.frames;
+    a.out = p.out;
+    a.tbl = p.tbl;
+    a.mask = p.mask;
+    a.n_entries = p.n_entries;
+    a.max_conn = p.max_conn;
+    a.n = p.n;
+    a.stride = s.stride;
+    a.ipa_off = s.ipa_off;
+    a.avail = s.avail;
+    a.offs = nullptr;
+    a.fpw = svc_fpw(p.n, W);
+    const bool verify = __builtin_amdgcn_readfirstlane(p.verify) != 0;
+    for (uint32_t g = w; g * a.fpw < a.n; g += W) {
+      if (verify) classify_group<MIS, COOP, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
+      else classify_group<MIS, COOP, kProdAbl | kHeaderOnly, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
+    }
+    // this wave's records visible to the host, then count it; the last wave completes the post
+    __threadfence_system();
+    if (lane == 0) {
+      const uint32_t prev = atomicAdd(&s.dev->count, 1u);
+      if (prev == W - 1) {
+        s.dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
+        __hip_atomic_store(&s.dev->done, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(s.done_word, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (w == 0) { // the next post only once every wave is done with this one
+      while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
+             want) {
+        if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) { // a wave that never finishes: give up
+          if (lane == 0) __hip_atomic_store(&s.dev->seq, kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    last = want;
+    t0 = wall_clock64();
+  }
+}
+
+template <int MIS>
+void launch_svc(bool coop, uint32_t waves, const SArgs& a, hipStream_t s) {
+  if (coop) hipLaunchKernelGGL((rx_service_kernel<MIS, 1>), dim3(waves), dim3(kWave), 0, s, a);
+  else hipLaunchKernelGGL((rx_service_kernel<MIS, 0>), dim3(waves), dim3(kWave), 0, s, a);
+}
+} // namespace
+
+struct pn_service {
+  pn_ctx* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  uint32_t stride = 0, frame_off = 0, waves = 0;
+  uint64_t idle_ticks = 0;
+  SvcPost* mail = nullptr;    // pinned host: 2 slots
+  uint32_t* words = nullptr;  // pinned host: [0] done, [16] exit (separate lines)
+  SvcDev* dev = nullptr;      // device
+  uint32_t seq = 0;           // last post issued
+  uint32_t epoch = 0;         // launches so far
+  bool running = false;       // a launch that has not been seen to end
+  bool coop = false;
+};
+
+namespace {
+// Launch (or relaunch) the kernel; it starts waiting for post base + 1, base = the last completed post, so posts
+// issued but not yet seen by an ended launch are taken by this one (they are still in their slots).
+int svc_launch(pn_service* v, uint32_t base) {
+  pn_ctx* ctx = v->ctx;
+  SvcDev init{};
+  init.seq = base;
+  init.done = base;
+  hipError_t e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(v->stream); // the previous launch has ended, the state is in place
+  if (e != hipSuccess) return hip_err(ctx, e, "pn_service: device state");
+  ++v->epoch;
+  SArgs a;
+  a.mail = v->mail;
+  a.done_word = v->words;
+  a.exit_word = v->words + 16;
+  a.dev = v->dev;
+  a.idle_ticks = v->idle_ticks;
+  a.epoch = v->epoch;
+  a.last = base;
+  a.stride = v->stride;
+  a.ipa_off = (v->frame_off + 14) & ~15u;
+  a.avail = v->stride - v->frame_off;
+  switch ((v->frame_off + 14) & 15) {
+    case 0: launch_svc<0>(v->coop, v->waves, a, v->stream); break;
+    case 2: launch_svc<2>(v->coop, v->waves, a, v->stream); break;
+    case 4: launch_svc<4>(v->coop, v->waves, a, v->stream); break;
+    case 6: launch_svc<6>(v->coop, v->waves, a, v->stream); break;
+    case 8: launch_svc<8>(v->coop, v->waves, a, v->stream); break;
+    case 10: launch_svc<10>(v->coop, v->waves, a, v->stream); break;
+    case 12: launch_svc<12>(v->coop, v->waves, a, v->stream); break;
+    default: launch_svc<14>(v->coop, v->waves, a, v->stream); break;
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(ctx, e, "pn_service: launch");
+  v->running = true;
+  return PN_OK;
+}
+
+void svc_free(pn_service* v) {
+  if (v->mail) (void)hipHostFree(v->mail);
+  if (v->words) (void)hipHostFree(v->words);
+  if (v->dev) (void)hipFree(v->dev);
+  if (v->stream) (void)hipStreamDestroy(v->stream);
+  delete v;
+}
+} // namespace
+
+extern "C" {
+
+int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, pn_service** out) {
+  if (!ctx || !out) return set_err(ctx, PN_EINVAL, "pn_service_open: ctx / out is NULL");
+  *out = nullptr;
+  if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || slot_stride < frame_off + 96)
+    return set_err(ctx, PN_EINVAL, "pn_service_open: slot_stride/frame_off violate the layout contract");
+  if (idle_ms == 0 || idle_ms > 10000) return set_err(ctx, PN_EINVAL, "pn_service_open: idle_ms must be in [1, 10000]");
+  hipError_t e = hipSetDevice(ctx->device);
+  if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
+  int khz = 0;
+  e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device);
+  if (e != hipSuccess || khz <= 0) return hip_err(ctx, e, "pn_service_open: wall clock rate");
+  pn_service* v = new pn_service();
+  v->ctx = ctx;
+  v->stride = slot_stride;
+  v->frame_off = frame_off;
+  v->waves = PN_SERVICE_WAVES;
+  v->idle_ticks = (uint64_t)khz * idle_ms;
+  // the cooperative window needs a 16-B chunk before it inside the slot (frame_off >= 2); the frames' 16-B
+  // alignment is checked per post
+  v->coop = (slot_stride % 16) == 0 && ((frame_off + 14) & ~15u) >= 16;
+  if ((e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipHostMalloc((void**)&v->mail, 2 * sizeof(SvcPost), hipHostMallocDefault)) != hipSuccess ||
+      (e = hipHostMalloc((void**)&v->words, 128, hipHostMallocDefault)) != hipSuccess ||
+      (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess) {
+    const int rc = hip_err(ctx, e, "pn_service_open: allocation");
+    svc_free(v);
+    return rc;
+  }
+  std::memset(v->mail, 0, 2 * sizeof(SvcPost));
+  std::memset(v->words, 0, 128);
+  const int rc = svc_launch(v, 0);
+  if (rc) {
+    svc_free(v);
+    return rc;
+  }
+  *out = v;
+  return PN_OK;
+}
+
+int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results) {
+  if (!v) return set_err(nullptr, PN_EINVAL, "pn_service_post: service is NULL");
+  pn_ctx* ctx = v->ctx;
+  if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, "pn_service_post: no conn table (call pn_set_conn_table)");
+  if (n == 0 || n > PN_SERVICE_MAX_FRAMES || !frames || !results)
+    return set_err(ctx, PN_EINVAL, "pn_service_post: n must be in [1, PN_SERVICE_MAX_FRAMES], buffers set");
+  if (((uintptr_t)frames & 15) || ((uintptr_t)results & 15))
+    return set_err(ctx, PN_EINVAL, "pn_service_post: frames/results must be 16-byte aligned");
+  // at most two posts outstanding: post k reuses the slot of post k - 2, which must be done
+  const uint32_t done = __atomic_load_n(v->words, __ATOMIC_ACQUIRE);
+  if ((int32_t)(v->seq - done) >= 2) return set_err(ctx, PN_EINVAL, "pn_service_post: two posts already outstanding");
+  if (v->running && __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) == v->epoch) v->running = false; // ended: idle
+  if (!v->running) {
+    const int rc = svc_launch(v, done);
+    if (rc) return rc;
+  }
+  const uint32_t k = v->seq + 1;
+  SvcPost* p = v->mail + (k & 1);
+  __atomic_store_n(&p->seq, 0u, __ATOMIC_RELAXED); // a half-written slot never reads as post k
+  __atomic_store_n(&p->gen, k, __ATOMIC_RELAXED);
+  p->n = n;
+  p->verify = ctx->verify_tcp ? 1u : 0u;
+  p->max_conn = ctx->max_conn;
+  p->frames = (const uint8_t*)frames;
+  p->out = (pn_result*)results;
+  p->tbl = ctx->tbl_dev;
+  p->mask = ctx->mask;
+  p->n_entries = ctx->n_entries;
+  __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
+  v->seq = k;
+  return PN_OK;
+}
+
+int pn_service_wait(pn_service* v) {
+  if (!v) return set_err(nullptr, PN_EINVAL, "pn_service_wait: service is NULL");
+  const uint32_t k = v->seq;
+  const auto t_start = std::chrono::steady_clock::now();
+  for (uint64_t i = 1;; ++i) {
+    if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - k) >= 0) return PN_OK;
+    if ((i & 4095) == 0) {
+      if (std::chrono::steady_clock::now() - t_start > std::chrono::seconds(10))
+        return set_err(v->ctx, PN_EHIP, "pn_service_wait: no completion within 10 s");
+      // the launch ended by itself (no post for idle_ms) before it saw this one: relaunch, it takes the pending
+      // posts (the device state starts at the last completed one)
+      if (__atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) == v->epoch) {
+        const uint32_t done = __atomic_load_n(v->words, __ATOMIC_ACQUIRE);
+        if ((int32_t)(done - k) >= 0) return PN_OK;
+        v->running = false;
+        const int rc = svc_launch(v, done);
+        if (rc) return rc;
+        continue;
+      }
+      const hipError_t q = hipStreamQuery(v->stream);
+      if (q != hipErrorNotReady && q != hipSuccess) return hip_err(v->ctx, q, "pn_service_wait: the service kernel failed");
+      if (q == hipSuccess && (int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - k) < 0 &&
+          __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) != v->epoch)
+        return set_err(v->ctx, PN_EHIP, "pn_service_wait: the service kernel ended without completing the post");
+    }
+  }
+}
+
+int pn_service_close(pn_service* v) {
+  if (!v) return PN_OK;
+  pn_ctx* ctx = v->ctx;
+  int rc = PN_OK;
+  if (v->running && __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) != v->epoch) {
+    // wait for the outstanding posts, then post the stop
+    if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - v->seq) < 0) rc = pn_service_wait(v);
+    const uint32_t k = v->seq + 1;
+    SvcPost* p = v->mail + (k & 1);
+    __atomic_store_n(&p->seq, 0u, __ATOMIC_RELAXED);
+    __atomic_store_n(&p->gen, k, __ATOMIC_RELAXED);
+    p->n = PN_SERVICE_STOP;
+    __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
+    v->seq = k;
+  }
+  const hipError_t e = hipStreamSynchronize(v->stream); // the kernel ends at the stop or its idle limit
+  if (e != hipSuccess && rc == PN_OK) rc = hip_err(ctx, e, "pn_service_close");
+  svc_free(v);
+  return rc;
+}
+
+} // extern "C"

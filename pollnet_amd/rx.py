@@ -121,6 +121,12 @@ _pn_tx_fill_notify = _sig("pn_tx_fill_notify", _i32, _vp, _vp, _u32, _u32, _u32,
 _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_set_verify = _sig("pn_set_verify", _i32, _vp, _i32)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
+_pn_service_open = _sig("pn_service_open", _i32, _vp, _u32, _u32, _u32, _c.POINTER(_vp))
+_pn_service_post = _sig("pn_service_post", _i32, _vp, _vp, _u32, _vp)
+_pn_service_wait = _sig("pn_service_wait", _i32, _vp)
+_pn_service_close = _sig("pn_service_close", _i32, _vp)
+PN_SERVICE_WAVES = 64
+PN_SERVICE_MAX_FRAMES = 1 << 20
 
 # The seeded workload generator lives in its own library (include/pollnet_amd_gen.h), outside
 # the product ABI; loaded on first use.
@@ -387,3 +393,34 @@ def gen_conn_table(params: GenParams, max_tw_cnt: int | None = None) -> ConnTabl
 def wire_bytes(slots: np.ndarray, slot_stride: int, frame_off: int, n: int) -> int:
     """Σ(14 + tot_len): the metric's numerator (wire frame bytes without FCS)."""
     return int(_gen_fn("pn_wire_bytes", _u64, _vp, _u32, _u32, _u32)(slots.ctypes.data, slot_stride, frame_off, n))
+
+
+class RxService:
+    """The resident classify service (pn_service_*): one launch, then batches posted through pinned host memory
+    and classified by the kernel already on the GPU.  Frames / results: pinned host or device memory."""
+
+    def __init__(self, ctx: RxContext, slot_stride: int, frame_off: int, idle_ms: int = 200):
+        h = _vp()
+        _check(_pn_service_open(ctx._h, slot_stride, frame_off, idle_ms, _c.byref(h)), ctx._h, "pn_service_open")
+        self._h, self._ctx = h, ctx
+
+    def post(self, frames, n: int, results):
+        _check(_pn_service_post(self._h, _ptr(frames), n, _ptr(results)), self._ctx._h, "pn_service_post")
+
+    def wait(self):
+        _check(_pn_service_wait(self._h), self._ctx._h, "pn_service_wait")
+
+    def classify(self, frames, n: int, results):
+        self.post(frames, n, results)
+        self.wait()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            h, self._h = self._h, None
+            _check(_pn_service_close(h), self._ctx._h, "pn_service_close")
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # interpreter teardown
+            pass

@@ -1,0 +1,172 @@
+"""GPU: the resident classify service (pn_service_*, pollnet_amd/csrc/rx_service.hip): one launch, batches posted
+through pinned host memory.  Every post's records must equal the oracle's (and, on the release path, the records
+pn_set_verify(ctx, 0) writes): small and large posts (1 .. 70,000 frames: every wave count, the group loop), frames
+and records in pinned host memory (zero copy) or device memory, two posts outstanding, a table change between
+posts, the kernel ending by itself after idle_ms and the next post relaunching it, every alignment class of the
+strided layout, and close.  Every wait inside the kernel has a wall-clock limit (it always ends)."""
+import time
+
+import numpy as np
+import pytest
+
+import pollnet_amd as pa
+from oracle import pyoracle as orc
+
+from frames import FRAME_OFF, STRIDE
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+
+    assert t.cuda.is_available(), "GPU tests need an MI355X"
+    return t
+
+
+def _frames(cfg, n, first=0, off=FRAME_OFF, stride=STRIDE):
+    p = pa.rx.GenParams.for_config(cfg)
+    s = np.ascontiguousarray(pa.gen_frames(p, n, stride, off, first_index=first, threads=8))
+    return p, s
+
+
+def _expected(s, n, table, off=FRAME_OFF, stride=STRIDE, verify=True):
+    e, m = table.snapshot()
+    return orc.classify_batch(s, stride, off, n, e, m, table.max_conn_cnt, threads=8, unverified=not verify)
+
+
+def _pinned(torch, arr):
+    return torch.from_numpy(np.ascontiguousarray(arr).reshape(-1)).pin_memory()
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_service_posts_equal_oracle_zero_copy(torch, cfg):
+    p, s = _frames(cfg, 70000)
+    table = pa.gen_conn_table(p)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            host = _pinned(torch, s)
+            res = torch.zeros(70000 * 16, dtype=torch.uint8).pin_memory()
+            exp_all = _expected(s, 70000, table)
+            unv_all = _expected(s, 70000, table, verify=False)
+            for n in (1, 7, 64, 65, 511, 512, 513, 4096, 4097, 70000):
+                for verify in (True, False):
+                    ctx.set_verify(verify)
+                    res.zero_()
+                    svc.classify(host, n, res)
+                    got = res.numpy()[: n * 16].view(pa.RESULT_DTYPE)
+                    exp = (exp_all if verify else unv_all)[:n]
+                    assert np.array_equal(got, exp), (n, verify, np.nonzero(got != exp)[0][:5])
+                    assert not res.numpy()[n * 16:].any(), "records written past n"
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+def test_service_device_memory_and_two_outstanding(torch):
+    p, s = _frames(2, 8192)
+    table = pa.gen_conn_table(p)
+    exp = _expected(s, 8192, table)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            dev = torch.from_numpy(s.reshape(-1)).cuda()
+            r = [torch.zeros(4096 * 16, dtype=torch.uint8, device="cuda") for _ in range(2)]
+            # two posts in flight: the halves of the batch, then wait for the second (posts complete in order)
+            svc.post(dev, 4096, r[0])
+            svc.post(dev[4096 * STRIDE:], 4096, r[1])
+            with pytest.raises(pa.PollnetError, match="two posts"):
+                svc.post(dev, 1, r[0])
+            svc.wait()
+            got = np.concatenate([x.cpu().numpy() for x in r]).view(pa.RESULT_DTYPE)
+            assert np.array_equal(got, exp)
+            # 200 back-to-back posts, alternating halves
+            for k in range(200):
+                svc.post(dev[(k & 1) * 4096 * STRIDE:], 4096, r[k & 1])
+                if k & 1:
+                    svc.wait()
+            svc.wait()
+            got = np.concatenate([x.cpu().numpy() for x in r]).view(pa.RESULT_DTYPE)
+            assert np.array_equal(got, exp)
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+def test_service_table_change_and_idle_relaunch(torch):
+    p, s = _frames(3, 2048)
+    table = pa.gen_conn_table(p)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=5)
+        try:
+            host = _pinned(torch, s)
+            res = torch.zeros(2048 * 16, dtype=torch.uint8).pin_memory()
+            svc.classify(host, 2048, res)
+            assert np.array_equal(res.numpy().view(pa.RESULT_DTYPE), _expected(s, 2048, table))
+            # a table change between posts: every frame of the flow of frame 0 now misses
+            key = int(pa.conn_hash_key(int(s[0, FRAME_OFF + 26:FRAME_OFF + 30].view("<u4")[0]),
+                                       int(s[0, FRAME_OFF + 34:FRAME_OFF + 36].view("<u2")[0])))
+            table.delete(key)
+            ctx.set_conn_table(table)
+            svc.classify(host, 2048, res)
+            exp = _expected(s, 2048, table)
+            assert np.array_equal(res.numpy().view(pa.RESULT_DTYPE), exp)
+            assert (exp["conn_id"] == pa.PN_MISS).sum() > 0
+            # idle: the kernel ends by itself after 5 ms; the next posts relaunch it
+            for _ in range(3):
+                time.sleep(0.03)
+                res.zero_()
+                svc.classify(host, 2048, res)
+                assert np.array_equal(res.numpy().view(pa.RESULT_DTYPE), exp)
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("off", [0, 2, 6, 10, 14, 18])
+def test_service_alignment_classes(torch, off):
+    stride = 2048 if off != 18 else 1664
+    p, s = _frames(5, 3000, off=off, stride=stride)
+    table = pa.gen_conn_table(p)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, stride, off)
+        try:
+            host = _pinned(torch, s)
+            res = torch.zeros(3000 * 16, dtype=torch.uint8).pin_memory()
+            svc.classify(host, 3000, res)
+            assert np.array_equal(res.numpy().view(pa.RESULT_DTYPE), _expected(s, 3000, table, off=off, stride=stride))
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+def test_service_argument_checks(torch):
+    ctx = pa.RxContext(0)
+    try:
+        with pytest.raises(pa.PollnetError, match="idle_ms"):
+            pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=0)
+        with pytest.raises(pa.PollnetError, match="layout"):
+            pa.RxService(ctx, 100, FRAME_OFF)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            buf = torch.zeros(STRIDE, dtype=torch.uint8).pin_memory()
+            with pytest.raises(pa.PollnetError, match="conn table"):
+                svc.post(buf, 1, buf)
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
