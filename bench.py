@@ -880,6 +880,9 @@ def summary(out):
             "server_512_pipelined_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_pipelined", "mframes_per_s"),
             "server_512_pipelined_release_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_pipelined_release_path",
                                                    "mframes_per_s"),
+            "server_512_resident_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_resident", "mframes_per_s"),
+            "server_512_resident_release_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_resident_release_path",
+                                                  "mframes_per_s"),
             "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s")})
     if cpu:
         s.update({"cpu_ref_gbit_per_s": cpu.get("value"), "cpu_ref_min_max": [cpu.get("min"), cpu.get("max")],

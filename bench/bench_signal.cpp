@@ -2,6 +2,7 @@
 //   sync    pn_classify + hipStreamSynchronize (what GpuRx / the drop-in server do)
 //   signal  pn_classify_notify: the kernel's last workgroup stores a token to a host-visible
 //           word once every record is stored and visible; the host spins on it
+//   service the resident classify service (pn_service_post + pn_service_wait): no launch per batch
 // C2 frames (1514 B) and the generator's table; batches of 64..1024 frames, device-resident
 // (records to device memory) and zero-copy (pinned slots, records to pinned memory).  Host wall
 // clock per batch, median of `reps`, the two forms interleaved; records compared.  One JSON line.
@@ -55,6 +56,8 @@ int main(int argc, char** argv) {
   if (hipMemcpy(d_frames, frames.data(), frames.size(), hipMemcpyHostToDevice) != hipSuccess) return 5;
   *flag = 0;
   uint32_t token = 0;
+  pn_service* svc = nullptr;
+  if (pn_service_open(ctx, stride, off, 2000, &svc)) return std::fprintf(stderr, "%s\n", pn_last_error(ctx)), 4;
   bool ok = true;
   std::string out = "{\"bench\": \"completion_word_vs_stream_sync\", \"frames\": \"C2 1514-B\"";
   // both checksums verified, then the release path (pn_set_verify(ctx, 0): header lines only)
@@ -71,6 +74,7 @@ int main(int argc, char** argv) {
       if (pn_classify_notify(ctx, fr, stride, off, n, rec, s, flag, tok)) return false;
       return pollnet_amd::wait_word(flag, tok, s) == nullptr;
     };
+    auto service_once = [&](uint32_t n) { return pn_service_post(svc, fr, n, rec, nullptr) == 0 && pn_service_wait(svc, 0) == 0; };
     std::string legs;
     for (uint32_t n : {64u, 512u, 1024u}) {
       // records equal: the signalled batch's records (zero-copy: read right after the word) vs sync's
@@ -91,8 +95,21 @@ int main(int argc, char** argv) {
       }
       ok = ok && same;
       ok = ok && hipStreamSynchronize(s) == hipSuccess;
-      std::vector<double> ts, tg;
-      for (int w = 0; w < 20; w++) ok = ok && sync_once(n) && signal_once(n);
+      // the service's records for the same batch
+      std::memset(h_rec, 0, 16 * n);
+      if (!zc) ok = ok && hipMemset(d_rec, 0, 16 * n) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+      ok = ok && service_once(n);
+      bool same_svc;
+      if (zc) {
+        same_svc = std::memcmp(h_rec, h_rec2, 16 * n) == 0;
+      } else {
+        std::vector<pn_result> tmp(n);
+        ok = ok && hipMemcpy(tmp.data(), d_rec, 16 * n, hipMemcpyDeviceToHost) == hipSuccess;
+        same_svc = std::memcmp(tmp.data(), h_rec2, 16 * n) == 0;
+      }
+      ok = ok && same_svc;
+      std::vector<double> ts, tg, tv;
+      for (int w = 0; w < 20; w++) ok = ok && sync_once(n) && signal_once(n) && service_once(n);
       ok = ok && hipStreamSynchronize(s) == hipSuccess;
       for (uint32_t r = 0; r < reps && ok; r++) {
         auto t0 = Clock::now();
@@ -101,13 +118,18 @@ int main(int argc, char** argv) {
         ok = ok && signal_once(n);
         auto t2 = Clock::now();
         ok = ok && hipStreamSynchronize(s) == hipSuccess; // the signalled launch has drained
+        auto t3 = Clock::now();
+        ok = ok && service_once(n);
+        auto t4 = Clock::now();
         ts.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         tg.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
+        tv.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
       }
       if (!ok) break;
-      char buf[256];
-      std::snprintf(buf, sizeof buf, "%s\"%u\": {\"sync_us\": %.2f, \"signal_us\": %.2f, \"records_equal\": %s}",
-                    legs.empty() ? "" : ", ", n, median(ts), median(tg), same ? "true" : "false");
+      char buf[320];
+      std::snprintf(buf, sizeof buf,
+                    "%s\"%u\": {\"sync_us\": %.2f, \"signal_us\": %.2f, \"service_us\": %.2f, \"records_equal\": %s}",
+                    legs.empty() ? "" : ", ", n, median(ts), median(tg), median(tv), same && same_svc ? "true" : "false");
       legs += buf;
     }
     out += std::string(", \"") + (zc ? "zero_copy" : "resident") + (verify ? "" : "_release_path") + "\": {" + legs + "}";
@@ -115,6 +137,7 @@ int main(int argc, char** argv) {
   out += std::string(", \"ok\": ") + (ok ? "true" : "false") + "}";
   std::printf("%s\n", out.c_str());
   (void)hipStreamSynchronize(s);
+  if (pn_service_close(svc)) ok = false;
   pn_close(ctx);
   return ok ? 0 : 1;
 }

@@ -159,7 +159,7 @@ struct Handler {
   }
 };
 
-template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false>
+template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false>
 struct Conf {
   static const uint32_t RecvBufSize = 65536;
   static const uint32_t MaxConns = 1024;
@@ -170,6 +170,7 @@ struct Conf {
   static const uint32_t TxBatch = kBatch;
   static const uint32_t RxChunk = kChunk;
   static const bool RxPipeline = kPipe;
+  static const bool RxResident = kResident;
   struct UserData {};
 };
 
@@ -181,10 +182,10 @@ struct Run {
 
 // verify = false: the checksum discard off, as the reference's release build runs (no checksum verified);
 // the GPU backend then classifies from each frame's header lines only (pn_set_verify)
-template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false>
+template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false>
 static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   Run out;
-  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe>, BenchLink, Backend>;
+  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident>, BenchLink, Backend>;
   auto srv = std::make_unique<Server>();
   srv->link().setup(n_flows);
   if (!srv->initWithLink("10.0.0.1", 1234)) {
@@ -288,6 +289,9 @@ int main(int argc, char** argv) {
     // their classify overlapped with this poll's host work), both paths
     leg("gpu_rxbatch_512_pipelined", runOne<512, GpuBackend, 0, true>(n_flows, polls));
     leg("gpu_rxbatch_512_pipelined_release_path", runOne<512, GpuBackend, 0, true>(n_flows, polls, false));
+    // the classify in the resident service (Conf::RxResident: a post per poll, no launch), both paths
+    leg("gpu_rxbatch_512_resident", runOne<512, GpuBackend, 0, false, true>(n_flows, polls));
+    leg("gpu_rxbatch_512_resident_release_path", runOne<512, GpuBackend, 0, false, true>(n_flows, polls, false));
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     // the same sequential server with the discard off: the reference's release build (no checksum summed per frame)
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));

@@ -272,8 +272,9 @@ int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
  * batch starts ~1-2 us after it is posted instead of a launch's ~7 us (bench/bench_doorbell).
  *   pn_service_post: frames (pinned host or device memory, 16-B aligned), n in [1, PN_SERVICE_MAX_FRAMES], results
  *     (pinned host or device memory, 16-B aligned).  The ctx's conn table and pn_set_verify setting at the post are
- *     used.  At most two posts outstanding; non-blocking.
- *   pn_service_wait: spins until the last post's records are visible to the host (as pn_classify_notify's word).
+ *     used.  At most two posts outstanding; non-blocking; *post_id (may be NULL) names the post.
+ *   pn_service_wait: spins until post post_id's records are visible to the host (as pn_classify_notify's word);
+ *     posts complete in order; post_id 0 = the last post.
  *   pn_service_close: waits for outstanding posts, stops the kernel, frees the service (before pn_close).
  * After idle_ms (1..10000) without a post the kernel ends by itself (every wait inside it has a wall-clock limit);
  * the next post relaunches it.  pn_set_conn_table may be called with at most one post outstanding (the table is
@@ -284,8 +285,8 @@ typedef struct pn_service pn_service;
 #define PN_SERVICE_MAX_FRAMES (1u << 20)
 #define PN_SERVICE_STOP 0xFFFFFFFFu /* internal: the stop post */
 int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, pn_service** out);
-int pn_service_post(pn_service* svc, const void* frames, uint32_t n, void* results);
-int pn_service_wait(pn_service* svc);
+int pn_service_post(pn_service* svc, const void* frames, uint32_t n, void* results, uint32_t* post_id);
+int pn_service_wait(pn_service* svc, uint32_t post_id);
 int pn_service_close(pn_service* svc);
 
 /* Wait until every launch this ctx issued (on any stream) has finished: synchronizes each

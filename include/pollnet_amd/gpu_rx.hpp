@@ -106,7 +106,10 @@ class GpuRx {
   // device: GPU ordinal; slot_stride/frame_off: the ring layout (RecvBufSize = 2048,
   // frame_off = sizeof(RecvBuf) + receive_prefix_len in the reference); max_batch:
   // the chunk pollBatch() classifies per launch (two chunks are in flight at once).
-  const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, Mode mode = Mode::Copy) {
+  // resident (ZeroCopy only): the chunks go to the resident classify service (pn_service_*: one launch, then a post
+  // per chunk through pinned memory) instead of a launch each; resident_idle_ms: how long it stays without a post.
+  const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, Mode mode = Mode::Copy,
+                   bool resident = false, uint32_t resident_idle_ms = 100) {
     destruct();
     if (max_batch == 0) return "max_batch must be > 0";
     if (pn_open(device, &ctx_)) return pn_last_error(nullptr);
@@ -120,6 +123,8 @@ class GpuRx {
       if (hipHostMalloc((void**)&h_word_, 128, hipHostMallocDefault) != hipSuccess) return "hipHostMalloc(notify words) failed";
       std::memset(h_word_, 0, 128);
     }
+    if (resident && mode == Mode::ZeroCopy && pn_service_open(ctx_, slot_stride, frame_off, resident_idle_ms, &svc_))
+      return pn_last_error(ctx_);
     for (int b = 0; b < 2; b++) {
       if (mode == Mode::Copy) {
         if (hipMalloc(&d_frames_[b], (size_t)slot_stride * max_batch) != hipSuccess) return "hipMalloc(frames) failed";
@@ -195,7 +200,7 @@ class GpuRx {
     if (mode_ == Mode::ZeroCopy)
       if (const char* e = check_pinned(host_slots)) return e;
     const char* e = launch_at(host_slots, n, b);
-    if (e) (void)hipStreamSynchronize(stream_);
+    if (e) drain();
     return e;
   }
   template <class RecvHandler, class TwHandler>
@@ -203,7 +208,7 @@ class GpuRx {
                        RecvHandler&& recv_handler, TwHandler&& tw_handler) {
     if (n > cap_ || b > 1) return "complete: n > max_batch or buffer > 1";
     if (const char* e = wait_done(b)) {
-      (void)hipStreamSynchronize(stream_);
+      drain();
       return e;
     }
     auto eth_of = [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; };
@@ -212,6 +217,7 @@ class GpuRx {
   }
 
   pn_ctx* ctx() { return ctx_; }
+  bool resident() const { return svc_ != nullptr; }
   hipStream_t stream() { return stream_; }
   Mode mode() const { return mode_; }
 
@@ -231,7 +237,7 @@ class GpuRx {
   const char* run(uint32_t n, const ConnTable& table, Launch&& launch_k, EthOf&& eth_of, RecvHandler& recv_handler,
                   TwHandler& tw_handler) {
     const char* e = run_chunks(n, table, launch_k, eth_of, recv_handler, tw_handler);
-    if (e) (void)hipStreamSynchronize(stream_);
+    if (e) drain();
     return e;
   }
   template <class Launch, class EthOf, class RecvHandler, class TwHandler>
@@ -276,14 +282,28 @@ class GpuRx {
     const uint32_t base = k * cap_;
     return launch_at(host_slots + (size_t)base * stride_, std::min(cap_, n - base), k & 1);
   }
-  // Wait for buffer b's launch: its notify word, or its event.
+  // After an error: nothing of this GpuRx left in flight (service posts waited for, the stream drained).
+  void drain() {
+    for (uint32_t b = 0; b < 2; b++)
+      if (post_[b]) (void)wait_done(b);
+    (void)hipStreamSynchronize(stream_);
+  }
+  // Wait for buffer b's launch: its service post, its notify word, or its event.
   const char* wait_done(uint32_t b) {
+    if (post_[b]) {
+      const uint32_t id = post_[b];
+      post_[b] = 0;
+      return pn_service_wait(svc_, id) ? pn_last_error(ctx_) : nullptr;
+    }
     if (use_word_[b]) return wait_word(&h_word_[16 * b], tok_[b], stream_);
     return hipEventSynchronize(done_[b]) == hipSuccess ? nullptr : "hipEventSynchronize failed";
   }
   // Issue the m slots at src into buffer b.
   const char* launch_at(const uint8_t* src, uint32_t m, uint32_t b) {
     use_word_[b] = false;
+    post_[b] = 0;
+    if (svc_) // resident service: a post, no launch
+      return pn_service_post(svc_, src, m, h_res_[b], &post_[b]) ? pn_last_error(ctx_) : nullptr;
     if (mode_ == Mode::ZeroCopy && m <= PN_NOTIFY_MAX_FRAMES) { // small batch: completion by a pinned word
       tok_[b] = ++next_tok_;
       if (pn_classify_notify(ctx_, src, stride_, off_, m, h_res_[b], stream_, &h_word_[16 * b], tok_[b]))
@@ -305,6 +325,9 @@ class GpuRx {
   }
 
   void destruct() {
+    if (svc_) (void)pn_service_close(svc_);
+    svc_ = nullptr;
+    post_[0] = post_[1] = 0;
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (int b = 0; b < 2; b++) {
       if (done_[b]) (void)hipEventDestroy(done_[b]);
@@ -337,6 +360,8 @@ class GpuRx {
   uint32_t* h_word_ = nullptr; // ZeroCopy: pinned notify words of buffers 0 and 1 (64 B apart)
   uint32_t tok_[2] = {0, 0}, next_tok_ = 0;
   bool use_word_[2] = {false, false};
+  pn_service* svc_ = nullptr;       // resident classify service (ZeroCopy, init's `resident`)
+  uint32_t post_[2] = {0, 0};       // buffer b's outstanding service post (0: none)
   uint32_t stride_ = 0, off_ = 0, cap_ = 0, max_conn_ = 0;
 };
 

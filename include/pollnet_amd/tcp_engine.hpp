@@ -79,6 +79,8 @@ PN_CONF_OPT(RxChunk, uint32_t, 0)           // frames per classify launch within
                                             // k+1 is on the GPU while chunk k is dispatched
 PN_CONF_OPT(RxPipeline, bool, false)        // throughput mode: a poll's frames are classified while the
                                             // previous poll's are dispatched (one poll of added latency)
+PN_CONF_OPT(RxResident, bool, false)        // the classify runs in the resident service (pn_service_*): a post
+                                            // per poll through pinned memory instead of a launch
 PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
 PN_CONF_OPT(Device, int, 0)
 PN_CONF_OPT(ReferenceLiteralTable, bool, false) // PN_TABLE_REFERENCE_LITERAL: the reference's rehash, defect kept
@@ -347,13 +349,13 @@ class GpuBackend {
   // two RX rings of rx_cap slots for launch/collect (one in flight while the other fills).
   // tx_halves = 2: two TX batches (one filled on the GPU while the other is built).
   const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1,
-                   uint32_t tx_halves = 1) {
+                   uint32_t tx_halves = 1, bool resident = false) {
     drain();
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
     rx_ring_ = tx_ring_ = nullptr;
     const uint32_t chunk = rx_chunk && rx_chunk < rx_cap ? rx_chunk : rx_cap;
-    if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy)) return e;
+    if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy, resident)) return e;
     if (pn_set_verify(rx_.ctx(), verify_ ? 1 : 0)) return pn_last_error(rx_.ctx());
     // the TX fill has a stream of its own: pipelined, it runs beside the next batch's classify
     if (!tx_stream_ && hipStreamCreateWithFlags(&tx_stream_, hipStreamNonBlocking) != hipSuccess)
@@ -716,7 +718,7 @@ class TcpEngine {
     std::memcpy(local_mac_, link_.localMac(), 6);
     if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
     if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1,
-                                 kRxPipeline ? 2 : 1))
+                                 kRxPipeline ? 2 : 1, srv_detail::opt_RxResident<Conf>::value))
       return e;
     free_conns_.clear();
     for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i

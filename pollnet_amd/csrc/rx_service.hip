@@ -125,11 +125,14 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       if (verify) classify_group<MIS, COOP, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
       else classify_group<MIS, COOP, kProdAbl | kHeaderOnly, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
     }
-    // this wave's records visible to the host, then count it; the last wave completes the post
-    __threadfence_system();
-    if (lane == 0) {
+    // this wave's records visible to the host, then count it; the last wave completes the post.  Only the waves
+    // that had groups of this post take part (a 64-frame post runs on 8 waves of 8 frames: the other 56 skip the
+    // system fence and the count)
+    const uint32_t groups = (a.n + a.fpw - 1) / a.fpw, active = groups < W ? groups : W;
+    if (w < active) __threadfence_system();
+    if (lane == 0 && w < active) {
       const uint32_t prev = atomicAdd(&s.dev->count, 1u);
-      if (prev == W - 1) {
+      if (prev == active - 1) {
         s.dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
         __hip_atomic_store(&s.dev->done, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         __threadfence_system();
@@ -262,7 +265,7 @@ int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint3
   return PN_OK;
 }
 
-int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results) {
+int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results, uint32_t* post_id) {
   if (!v) return set_err(nullptr, PN_EINVAL, "pn_service_post: service is NULL");
   pn_ctx* ctx = v->ctx;
   if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, "pn_service_post: no conn table (call pn_set_conn_table)");
@@ -292,12 +295,15 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   p->n_entries = ctx->n_entries;
   __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
   v->seq = k;
+  if (post_id) *post_id = k;
   return PN_OK;
 }
 
-int pn_service_wait(pn_service* v) {
+int pn_service_wait(pn_service* v, uint32_t post_id) {
   if (!v) return set_err(nullptr, PN_EINVAL, "pn_service_wait: service is NULL");
-  const uint32_t k = v->seq;
+  if (post_id == 0 || (int32_t)(post_id - v->seq) > 0 || (int32_t)(v->seq - post_id) >= 2)
+    post_id = v->seq; // 0 (or an id not among the last two posts): the last post
+  const uint32_t k = post_id;
   const auto t_start = std::chrono::steady_clock::now();
   for (uint64_t i = 1;; ++i) {
     if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - k) >= 0) return PN_OK;
@@ -329,7 +335,7 @@ int pn_service_close(pn_service* v) {
   int rc = PN_OK;
   if (v->running && __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) != v->epoch) {
     // wait for the outstanding posts, then post the stop
-    if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - v->seq) < 0) rc = pn_service_wait(v);
+    if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - v->seq) < 0) rc = pn_service_wait(v, 0);
     const uint32_t k = v->seq + 1;
     SvcPost* p = v->mail + (k & 1);
     __atomic_store_n(&p->seq, 0u, __ATOMIC_RELAXED);

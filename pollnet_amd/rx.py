@@ -122,8 +122,8 @@ _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_set_verify = _sig("pn_set_verify", _i32, _vp, _i32)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 _pn_service_open = _sig("pn_service_open", _i32, _vp, _u32, _u32, _u32, _c.POINTER(_vp))
-_pn_service_post = _sig("pn_service_post", _i32, _vp, _vp, _u32, _vp)
-_pn_service_wait = _sig("pn_service_wait", _i32, _vp)
+_pn_service_post = _sig("pn_service_post", _i32, _vp, _vp, _u32, _vp, _vp)
+_pn_service_wait = _sig("pn_service_wait", _i32, _vp, _u32)
 _pn_service_close = _sig("pn_service_close", _i32, _vp)
 PN_SERVICE_WAVES = 64
 PN_SERVICE_MAX_FRAMES = 1 << 20
@@ -404,11 +404,15 @@ class RxService:
         _check(_pn_service_open(ctx._h, slot_stride, frame_off, idle_ms, _c.byref(h)), ctx._h, "pn_service_open")
         self._h, self._ctx = h, ctx
 
-    def post(self, frames, n: int, results):
-        _check(_pn_service_post(self._h, _ptr(frames), n, _ptr(results)), self._ctx._h, "pn_service_post")
+    def post(self, frames, n: int, results) -> int:
+        """Non-blocking; returns the post's id (posts complete in order)."""
+        pid = _u32(0)
+        _check(_pn_service_post(self._h, _ptr(frames), n, _ptr(results), _c.byref(pid)), self._ctx._h, "pn_service_post")
+        return pid.value
 
-    def wait(self):
-        _check(_pn_service_wait(self._h), self._ctx._h, "pn_service_wait")
+    def wait(self, post_id: int = 0):
+        """Until post post_id's records are visible (0: the last post)."""
+        _check(_pn_service_wait(self._h, post_id), self._ctx._h, "pn_service_wait")
 
     def classify(self, frames, n: int, results):
         self.post(frames, n, results)

@@ -53,7 +53,8 @@ struct OracleBackend {
   std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
   uint32_t cap = 0;
   uint32_t tcap = 0;
-  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0, uint32_t rx_halves = 1, uint32_t tx_halves = 1) {
+  const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0, uint32_t rx_halves = 1, uint32_t tx_halves = 1,
+                   bool = false) {
     cap = rx_cap;
     tcap = tx_cap;
     rx.assign((size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1), 0);

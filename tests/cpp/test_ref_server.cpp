@@ -43,6 +43,10 @@ struct RefConf {
 struct ProdConf : RefConf {
   static const uint32_t RxBatch = 64;
 };
+// the same with the classify in the resident service (a post per poll, no launch)
+struct ProdConfResident : ProdConf {
+  static const bool RxResident = true;
+};
 
 static const uint32_t kMaxPolls = 30000;
 
@@ -90,9 +94,9 @@ static Transcript runRef(const std::vector<Client>& pop) {
   return t;
 }
 
-template <class Backend>
+template <class Backend, class Conf = ProdConf>
 static Transcript runProd(const std::vector<Client>& pop, bool drop_bad = true) {
-  using Srv = GpuTcpServer<ProdConf, PeerLink, Backend>;
+  using Srv = GpuTcpServer<Conf, PeerLink, Backend>;
   auto srv = std::make_unique<Srv>();
   Transcript t;
   if (!srv->initWithLink("10.0.0.1", 1234, kT0)) {
@@ -375,6 +379,10 @@ int main(int argc, char** argv) {
         fail += compare("GpuTcpServer (GPU backend) vs reference", ref, runProd<GpuBackend>(pop));
         fail += compare("GpuTcpServer (GPU backend, release path: no checksum verification) vs reference", ref,
                         runProd<GpuBackend>(pop, false));
+        fail += compare("GpuTcpServer (GPU backend, resident service) vs reference", ref,
+                        runProd<GpuBackend, ProdConfResident>(pop));
+        fail += compare("GpuTcpServer (GPU backend, resident service, release path) vs reference", ref,
+                        runProd<GpuBackend, ProdConfResident>(pop, false));
       }
     }
   }

@@ -80,9 +80,12 @@ def test_service_device_memory_and_two_outstanding(torch):
             dev = torch.from_numpy(s.reshape(-1)).cuda()
             r = [torch.zeros(4096 * 16, dtype=torch.uint8, device="cuda") for _ in range(2)]
             # two posts in flight: the halves of the batch, then wait for the second (posts complete in order)
-            svc.post(dev, 4096, r[0])
-            svc.post(dev[4096 * STRIDE:], 4096, r[1])
-            svc.wait()
+            a = svc.post(dev, 4096, r[0])
+            b = svc.post(dev[4096 * STRIDE:], 4096, r[1])
+            assert b == a + 1
+            svc.wait(a)
+            assert np.array_equal(r[0].cpu().numpy().view(pa.RESULT_DTYPE), exp[:4096])
+            svc.wait(b)
             got = np.concatenate([x.cpu().numpy() for x in r]).view(pa.RESULT_DTYPE)
             assert np.array_equal(got, exp)
             # 200 back-to-back posts, alternating halves

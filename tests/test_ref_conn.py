@@ -57,6 +57,9 @@ def test_gpu_server_equals_reference_server():
     assert p.stdout.count("GpuTcpServer (GPU backend) vs reference") == 6, p.stdout
     # and with the checksum discard off: the header-only kernel (pn_set_verify(ctx, 0)), the reference's release path
     assert p.stdout.count("GpuTcpServer (GPU backend, release path: no checksum verification) vs reference") == 6, p.stdout
+    # and with the classify in the resident service (Conf::RxResident, pn_service_*), both paths
+    assert p.stdout.count("GpuTcpServer (GPU backend, resident service) vs reference") == 6, p.stdout
+    assert p.stdout.count("GpuTcpServer (GPU backend, resident service, release path) vs reference") == 6, p.stdout
     assert "bad checksums (GPU backend):" in p.stdout and p.stdout.count("-> as documented") == 5, p.stdout
     assert "DIFFERENT" not in p.stdout and p.stdout.rstrip().endswith("PASS"), p.stdout
 
