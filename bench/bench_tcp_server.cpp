@@ -292,6 +292,8 @@ int main(int argc, char** argv) {
     // the classify in the resident service (Conf::RxResident: a post per poll, no launch), both paths
     leg("gpu_rxbatch_512_resident", runOne<512, GpuBackend, 0, false, true>(n_flows, polls));
     leg("gpu_rxbatch_512_resident_release_path", runOne<512, GpuBackend, 0, false, true>(n_flows, polls, false));
+    leg("gpu_rxbatch_512_pipelined_resident", runOne<512, GpuBackend, 0, true, true>(n_flows, polls));
+    leg("gpu_rxbatch_512_pipelined_resident_release_path", runOne<512, GpuBackend, 0, true, true>(n_flows, polls, false));
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     // the same sequential server with the discard off: the reference's release build (no checksum summed per frame)
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));

@@ -6,13 +6,16 @@
 // Protocol.  Two mailbox slots of one 64-B line each (pinned host memory; post k uses slot k & 1).  The host
 // fills a slot's fields, its first word (gen) and last word (seq) = k, seq last with a release store.  Wave 0 of
 // the kernel polls only the slot of the next post (one 64-B read per poll: 16 lanes x 4 B), accepts it when gen
-// and seq both read k, copies it to device memory and publishes k to the other waves through a device word.  Each
-// wave classifies its groups of the batch, makes its records system-visible and counts itself done; the last
-// resets the counter and stores k to the host's done word.  Wave 0 looks for post k + 1 only once post k is done.
-// A post whose n is PN_SERVICE_STOP ends every wave.  Every wait has a device-wall-clock limit: after idle_ms
-// without a post wave 0 publishes "idle", stores the launch's epoch to the host's exit word and ends, and the
-// others end on seeing it (or at their own limit); the host relaunches on its next post.  So the kernel always
-// ends.  Only vector memory operations (global loads / stores / one atomic add).
+// and seq both read k, and publishes (waves << 32) | k in a device word: a post runs on one wave per group of
+// frames (at most all of them; svc_fpw sizes the groups).  A one-wave post wave 0 classifies alone; for a larger
+// one it first copies the slot to device memory, where the post's other waves read it.  Each wave of the post makes
+// its records system-visible and stores k to its own host done word -- the host waits on the words of the post's
+// waves, no cross-wave step on the way -- and then counts itself done on the device; the last resets the counter
+// and marks the post done for wave 0, which looks for post k + 1 only then.  A stop post (n = PN_SERVICE_STOP)
+// ends every wave.  Every wait has a device-wall-clock limit: after idle_ms without a post wave 0 publishes
+// "idle", stores the launch's epoch to the host's exit word and ends, and the others end on seeing it (or at their
+// own limit); the host relaunches on its next post.  So the kernel always ends.  Only vector memory operations
+// (global loads / stores / one atomic add).
 #include <chrono>
 
 #include "rx_classify.hpp"
@@ -31,26 +34,31 @@ struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its devi
   const pn_conn_entry* tbl;
   uint64_t mask;
   uint32_t n_entries;
-  uint32_t pad0, pad1;
+  uint32_t fpw; // frames per group (svc_fpw)
+  uint32_t pad;
   uint32_t seq; // stored last (release)
 };
 static_assert(sizeof(SvcPost) == 64, "one line per post");
 
-constexpr uint32_t kSvcIdle = 0xFFFFFFFFu; // published on the device word when wave 0 ends for lack of posts
+constexpr uint32_t kExitWord = 96;   // host words: the waves' done words, then the exit word on a line of its own
+constexpr uint32_t kWordsBytes = 512;
+static_assert(PN_SERVICE_WAVES <= 64, "the done words fill [0, 64)");
+constexpr uint32_t kSvcIdle = 0xFFFFFFFFu; // published as the post when wave 0 ends for lack of posts
+constexpr uint32_t kSvcStop = 0xFFFFFFFFu; // published as the wave count of a stop post
 
 struct alignas(64) SvcDev { // device memory, set by the host before every launch
-  uint32_t seq;             // the post the waves may work on (wave 0 publishes), or kSvcIdle
-  uint32_t pad0[15];
+  uint64_t cur;             // wave 0 publishes (waves << 32) | post: the post and how many waves it runs on
+  uint32_t pad0[14];
   uint32_t count; // waves done with the current post
-  uint32_t done;  // the last post every wave finished
+  uint32_t done;  // the last multi-wave post every one of its waves finished
   uint32_t pad1[14];
   SvcPost post[2];
 };
 
 struct SArgs {
-  const SvcPost* mail; // host: the two mailbox slots
-  uint32_t* done_word; // host: the last completed post
-  uint32_t* exit_word; // host: the launch's epoch once it ended for lack of posts
+  const SvcPost* mail;  // host: the two mailbox slots
+  uint32_t* done_words; // host: per wave, the last post it finished its groups of
+  uint32_t* exit_word;  // host: the launch's epoch once it ended for lack of posts
   SvcDev* dev;
   uint64_t idle_ticks; // device wall clock
   uint32_t epoch;
@@ -58,12 +66,71 @@ struct SArgs {
   uint32_t stride, ipa_off, avail;
 };
 
-__device__ __forceinline__ uint32_t svc_fpw(uint32_t n, uint32_t waves) {
-  uint32_t fpw = 8; // a small batch over more waves (latency); 64 once the waves are full
+// Frames per group (host, at the post).  The release path reads one header line per frame: 64 frames a wave, so a
+// post of up to 64 frames is wave 0's alone (no cross-wave step at all).  Verifying reads every byte: a small
+// post is spread over more waves (8 frames a group and up, as few waves' worth of streaming as the post allows).
+inline uint32_t svc_fpw(uint32_t n, uint32_t waves, bool verify) {
+  uint32_t fpw = verify ? 8u : kFramesPerWave;
   while (fpw < kFramesPerWave && (n + fpw - 1) / fpw > waves) fpw <<= 1;
   return fpw;
 }
 
+// the waves a post runs on: one per group, at most all (the host computes the same)
+__host__ __device__ __forceinline__ uint32_t svc_active(uint32_t n, uint32_t fpw, uint32_t waves) {
+  const uint32_t groups = (n + fpw - 1) / fpw;
+  return groups < waves ? groups : waves;
+}
+
+// a post's kernel arguments from its 64-B line held one word per lane (lanes 0-15, SvcPost's layout)
+__device__ __forceinline__ KArgs svc_args(uint32_t v, const SArgs& s) {
+  // readlane returns int: each word through uint32_t, or a low word with bit 31 set would sign-extend
+  auto u64 = [&](int lo) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, lo + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane(v, lo);
+  };
+  KArgs a;
+  a.n = __builtin_amdgcn_readlane(v, 1);
+  a.max_conn = __builtin_amdgcn_readlane(v, 3);
+  a.frames = reinterpret_cast<const uint8_t*>(u64(4));
+  a.out = reinterpret_cast<pn_result*>(u64(6));
+  a.tbl = reinterpret_cast<const pn_conn_entry*>(u64(8));
+  a.mask = u64(10);
+  a.n_entries = __builtin_amdgcn_readlane(v, 12);
+  a.stride = s.stride;
+  a.ipa_off = s.ipa_off;
+  a.avail = s.avail;
+  a.offs = nullptr;
+  a.fpw = __builtin_amdgcn_readlane(v, 13);
+  return a;
+}
+
+// wave w's groups of the post (round robin over the post's waves), then its records made visible to the host and
+// post k stored to its done word
+template <int MIS, int COOP>
+__device__ __forceinline__ void svc_run(const KArgs& a, bool verify, uint32_t w, uint32_t act, uint32_t k,
+                                        uint32_t* done_word, int lane) {
+  for (uint32_t g = w; g * a.fpw < a.n; g += act) {
+    if (verify) classify_group<MIS, COOP, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
+    else classify_group<MIS, COOP, kProdAbl | kHeaderOnly, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
+  }
+  __threadfence_system();
+  if (lane == 0) __hip_atomic_store(done_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// a multi-wave post: count this wave done; the last one resets the count and marks the post done for wave 0
+__device__ __forceinline__ void svc_count(SvcDev* dev, uint32_t act, uint32_t k, int lane) {
+  if (lane == 0) {
+    const uint32_t prev = atomicAdd(&dev->count, 1u);
+    if (prev == act - 1) {
+      dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
+      __hip_atomic_store(&dev->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Wave 0 takes posts from the mailbox in order and publishes each with its wave count; a one-wave post it
+// classifies alone.  A post's waves other than 0 read it from the device copy, which wave 0 overwrites (two posts
+// later) only after every one of them counted itself done, so they always see it whole; the waves a post does not
+// run on only note it went by (from the published word alone: they may skip posts).
 template <int MIS, int COOP>
 __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   const int lane = threadIdx.x;
@@ -71,21 +138,15 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   uint32_t last = s.last;
   uint64_t t0 = wall_clock64();
   for (;;) {
-    const uint32_t want = last + 1;
     if (w == 0) {
+      const uint32_t want = last + 1;
       // the next post's slot, one 64-B read: lane i holds word i
       const uint32_t* slot = reinterpret_cast<const uint32_t*>(s.mail + (want & 1));
       const uint32_t v = lane < 16 ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-      const uint32_t gen = __builtin_amdgcn_readlane(v, 0), seq = __builtin_amdgcn_readlane(v, 15);
-      if (gen == want && seq == want) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[want & 1])[lane] = v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_store(&s.dev->seq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
+      if (__builtin_amdgcn_readlane(v, 0) != want || __builtin_amdgcn_readlane(v, 15) != want) {
         if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
           if (lane == 0) {
-            __hip_atomic_store(&s.dev->seq, kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           }
           return;
@@ -93,64 +154,56 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
+      const uint32_t n = __builtin_amdgcn_readlane(v, 1);
+      if (n == PN_SERVICE_STOP) {
+        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)kSvcStop << 32) | want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      const KArgs a = svc_args(v, s);
+      const uint32_t act = svc_active(n, a.fpw, W);
+      const bool verify = __builtin_amdgcn_readlane(v, 2) != 0;
+      if (act == 1) { // one wave's work: classify, then let the others see it go by
+        svc_run<MIS, COOP>(a, verify, 0, 1, want, s.done_words, lane);
+        if (lane == 0) __hip_atomic_store(&s.dev->cur, (1ull << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[want & 1])[lane] = v;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)act << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        svc_run<MIS, COOP>(a, verify, 0, act, want, s.done_words, lane);
+        svc_count(s.dev, act, want, lane);
+        // the next post only once every wave of this one is done (its device copy may then be reused)
+        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
+               want) {
+          if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) { // a wave that never finishes: give up
+            if (lane == 0) __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      last = want;
     } else {
-      const uint32_t d = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      if (d == kSvcIdle) return;
-      if (d != want) {
-        // wave 0 publishes at most one post past the last completed one, so d is want or want - 1; the limit is
-        // wave 0's plus a margin (a safety net: wave 0 always publishes kSvcIdle first)
+      const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t d = __builtin_amdgcn_readfirstlane((uint32_t)c), act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
+      if (d == kSvcIdle || act == kSvcStop) return;
+      if (d == last) {
+        // the limit is wave 0's plus a margin (a safety net: wave 0 always publishes kSvcIdle first)
         if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) return;
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    const SvcPost p = s.dev->post[want & 1];
-    if (p.n == PN_SERVICE_STOP) return;
-    KArgs a;
-    a.frames = p.frames;
-    a.out = p.out;
-    a.tbl = p.tbl;
-    a.mask = p.mask;
-    a.n_entries = p.n_entries;
-    a.max_conn = p.max_conn;
-    a.n = p.n;
-    a.stride = s.stride;
-    a.ipa_off = s.ipa_off;
-    a.avail = s.avail;
-    a.offs = nullptr;
-    a.fpw = svc_fpw(p.n, W);
-    const bool verify = __builtin_amdgcn_readfirstlane(p.verify) != 0;
-    for (uint32_t g = w; g * a.fpw < a.n; g += W) {
-      if (verify) classify_group<MIS, COOP, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
-      else classify_group<MIS, COOP, kProdAbl | kHeaderOnly, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
-    }
-    // this wave's records visible to the host, then count it; the last wave completes the post.  Only the waves
-    // that had groups of this post take part (a 64-frame post runs on 8 waves of 8 frames: the other 56 skip the
-    // system fence and the count)
-    const uint32_t groups = (a.n + a.fpw - 1) / a.fpw, active = groups < W ? groups : W;
-    if (w < active) __threadfence_system();
-    if (lane == 0 && w < active) {
-      const uint32_t prev = atomicAdd(&s.dev->count, 1u);
-      if (prev == active - 1) {
-        s.dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
-        __hip_atomic_store(&s.dev->done, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __threadfence_system();
-        __hip_atomic_store(s.done_word, want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (w < act) { // this wave runs on post d: wave 0 waits for it before the next post, so d is current
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[d & 1]);
+        const uint32_t v = lane < 16 ? cp[lane] : 0u;
+        const KArgs a = svc_args(v, s);
+        svc_run<MIS, COOP>(a, __builtin_amdgcn_readlane(v, 2) != 0, w, act, d, s.done_words + w, lane);
+        svc_count(s.dev, act, d, lane);
       }
+      last = d;
     }
-    if (w == 0) { // the next post only once every wave is done with this one
-      while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
-             want) {
-        if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) { // a wave that never finishes: give up
-          if (lane == 0) __hip_atomic_store(&s.dev->seq, kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          return;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    }
-    last = want;
     t0 = wall_clock64();
   }
 }
@@ -168,7 +221,8 @@ struct pn_service {
   uint32_t stride = 0, frame_off = 0, waves = 0;
   uint64_t idle_ticks = 0;
   SvcPost* mail = nullptr;    // pinned host: 2 slots
-  uint32_t* words = nullptr;  // pinned host: [0] done, [16] exit (separate lines)
+  uint32_t* words = nullptr;  // pinned host: [0, 64) the waves' done words, [kExitWord] exit (its own line)
+  uint32_t post_act[2] = {0, 0}; // waves of the last two posts (slot k & 1): whose words post k completes
   SvcDev* dev = nullptr;      // device
   uint32_t seq = 0;           // last post issued
   uint32_t epoch = 0;         // launches so far
@@ -182,7 +236,7 @@ namespace {
 int svc_launch(pn_service* v, uint32_t base) {
   pn_ctx* ctx = v->ctx;
   SvcDev init{};
-  init.seq = base;
+  init.cur = base;
   init.done = base;
   hipError_t e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(v->stream); // the previous launch has ended, the state is in place
@@ -190,8 +244,8 @@ int svc_launch(pn_service* v, uint32_t base) {
   ++v->epoch;
   SArgs a;
   a.mail = v->mail;
-  a.done_word = v->words;
-  a.exit_word = v->words + 16;
+  a.done_words = v->words;
+  a.exit_word = v->words + kExitWord;
   a.dev = v->dev;
   a.idle_ticks = v->idle_ticks;
   a.epoch = v->epoch;
@@ -214,6 +268,22 @@ int svc_launch(pn_service* v, uint32_t base) {
   v->running = true;
   return PN_OK;
 }
+
+// post k (one of the last two) is complete once every wave it ran on stored k (or later) to its done word
+bool svc_post_done(const pn_service* v, uint32_t k) {
+  const uint32_t act = v->post_act[k & 1];
+  for (uint32_t w = 0; w < act; ++w)
+    if ((int32_t)(__atomic_load_n(v->words + w, __ATOMIC_ACQUIRE) - k) < 0) return false;
+  return true;
+}
+
+// the last completed post (posts complete in order)
+uint32_t svc_done(const pn_service* v) {
+  if (svc_post_done(v, v->seq)) return v->seq;
+  return svc_post_done(v, v->seq - 1) ? v->seq - 1 : v->seq - 2;
+}
+
+bool svc_exited(const pn_service* v) { return __atomic_load_n(v->words + kExitWord, __ATOMIC_ACQUIRE) == v->epoch; }
 
 void svc_free(pn_service* v) {
   if (v->mail) (void)hipHostFree(v->mail);
@@ -248,14 +318,14 @@ int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint3
   v->coop = (slot_stride % 16) == 0 && ((frame_off + 14) & ~15u) >= 16;
   if ((e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void**)&v->mail, 2 * sizeof(SvcPost), hipHostMallocDefault)) != hipSuccess ||
-      (e = hipHostMalloc((void**)&v->words, 128, hipHostMallocDefault)) != hipSuccess ||
+      (e = hipHostMalloc((void**)&v->words, kWordsBytes, hipHostMallocDefault)) != hipSuccess ||
       (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess) {
     const int rc = hip_err(ctx, e, "pn_service_open: allocation");
     svc_free(v);
     return rc;
   }
   std::memset(v->mail, 0, 2 * sizeof(SvcPost));
-  std::memset(v->words, 0, 128);
+  std::memset(v->words, 0, kWordsBytes);
   const int rc = svc_launch(v, 0);
   if (rc) {
     svc_free(v);
@@ -274,9 +344,9 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   if (((uintptr_t)frames & 15) || ((uintptr_t)results & 15))
     return set_err(ctx, PN_EINVAL, "pn_service_post: frames/results must be 16-byte aligned");
   // at most two posts outstanding: post k reuses the slot of post k - 2, which must be done
-  const uint32_t done = __atomic_load_n(v->words, __ATOMIC_ACQUIRE);
+  const uint32_t done = svc_done(v);
   if ((int32_t)(v->seq - done) >= 2) return set_err(ctx, PN_EINVAL, "pn_service_post: two posts already outstanding");
-  if (v->running && __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) == v->epoch) v->running = false; // ended: idle
+  if (v->running && svc_exited(v)) v->running = false; // ended: idle
   if (!v->running) {
     const int rc = svc_launch(v, done);
     if (rc) return rc;
@@ -293,6 +363,8 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   p->tbl = ctx->tbl_dev;
   p->mask = ctx->mask;
   p->n_entries = ctx->n_entries;
+  p->fpw = svc_fpw(n, v->waves, p->verify != 0);
+  v->post_act[k & 1] = svc_active(n, p->fpw, v->waves);
   __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
   v->seq = k;
   if (post_id) *post_id = k;
@@ -306,14 +378,14 @@ int pn_service_wait(pn_service* v, uint32_t post_id) {
   const uint32_t k = post_id;
   const auto t_start = std::chrono::steady_clock::now();
   for (uint64_t i = 1;; ++i) {
-    if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - k) >= 0) return PN_OK;
+    if (svc_post_done(v, k)) return PN_OK;
     if ((i & 4095) == 0) {
       if (std::chrono::steady_clock::now() - t_start > std::chrono::seconds(10))
         return set_err(v->ctx, PN_EHIP, "pn_service_wait: no completion within 10 s");
       // the launch ended by itself (no post for idle_ms) before it saw this one: relaunch, it takes the pending
       // posts (the device state starts at the last completed one)
-      if (__atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) == v->epoch) {
-        const uint32_t done = __atomic_load_n(v->words, __ATOMIC_ACQUIRE);
+      if (svc_exited(v)) {
+        const uint32_t done = svc_done(v);
         if ((int32_t)(done - k) >= 0) return PN_OK;
         v->running = false;
         const int rc = svc_launch(v, done);
@@ -322,8 +394,7 @@ int pn_service_wait(pn_service* v, uint32_t post_id) {
       }
       const hipError_t q = hipStreamQuery(v->stream);
       if (q != hipErrorNotReady && q != hipSuccess) return hip_err(v->ctx, q, "pn_service_wait: the service kernel failed");
-      if (q == hipSuccess && (int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - k) < 0 &&
-          __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) != v->epoch)
+      if (q == hipSuccess && !svc_post_done(v, k) && !svc_exited(v))
         return set_err(v->ctx, PN_EHIP, "pn_service_wait: the service kernel ended without completing the post");
     }
   }
@@ -333,14 +404,15 @@ int pn_service_close(pn_service* v) {
   if (!v) return PN_OK;
   pn_ctx* ctx = v->ctx;
   int rc = PN_OK;
-  if (v->running && __atomic_load_n(v->words + 16, __ATOMIC_ACQUIRE) != v->epoch) {
+  if (v->running && !svc_exited(v)) {
     // wait for the outstanding posts, then post the stop
-    if ((int32_t)(__atomic_load_n(v->words, __ATOMIC_ACQUIRE) - v->seq) < 0) rc = pn_service_wait(v, 0);
+    if (!svc_post_done(v, v->seq)) rc = pn_service_wait(v, 0);
     const uint32_t k = v->seq + 1;
     SvcPost* p = v->mail + (k & 1);
     __atomic_store_n(&p->seq, 0u, __ATOMIC_RELAXED);
     __atomic_store_n(&p->gen, k, __ATOMIC_RELAXED);
     p->n = PN_SERVICE_STOP;
+    v->post_act[k & 1] = 0;
     __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
     v->seq = k;
   }

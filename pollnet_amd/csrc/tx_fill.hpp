@@ -333,14 +333,6 @@ __global__ __launch_bounds__(256) void tx_patch_wt_kernel(TArgs a) {
   }
 }
 
-// Tuning: after a phase-2 kernel with ordinary stores, a short launch whose workgroups each end with a
-// system-scope release, which writes the L2's dirty lines back (one workgroup per XCD suffices; 64 cover the
-// round-robin placement), so the patch's dirty sectors leave before the next call's read stream.
-__global__ __launch_bounds__(64) void tx_l2_release_kernel(uint32_t* sink) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  if (threadIdx.x == 0 && sink[blockIdx.x] == 0x7fffffffu) sink[blockIdx.x] = 0; // never true: keeps the launch
-}
-
 inline bool coop_layout(const TArgs& a) {
   return (a.stride % 16) == 0 && a.ipa_off >= 16 && ((uintptr_t)a.frames % 16) == 0;
 }

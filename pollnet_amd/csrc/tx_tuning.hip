@@ -2,6 +2,15 @@
 // `make` (TUNING=1 by default).  Never part of the product library.
 #include "tx_fill.hpp"
 
+// Tuning: after a phase-2 kernel with ordinary stores, a short launch whose workgroups each end with a
+// system-scope release, which writes the L2's dirty lines back (one workgroup per XCD suffices; 64 cover the
+// round-robin placement), so the patch's dirty sectors leave before the next call's read stream.
+__global__ __launch_bounds__(64) void tx_l2_release_kernel(uint32_t* sink) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  if (threadIdx.x == 0 && sink[blockIdx.x] == 0x7fffffffu) sink[blockIdx.x] = 0; // never true: keeps the launch
+}
+
+
 // Same-run ceiling for pn_tx_fill (bench.py): the production launches (the fill kernel with
 // its header window and stream loads, the patch records, the patch kernel's 2-byte stores) with
 // the stream phase's lane reduction ablated -- the same loads and stores, next to no arithmetic.

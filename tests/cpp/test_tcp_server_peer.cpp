@@ -61,6 +61,14 @@ struct PeerConfChunk : PeerConf {
 struct PeerConfPipe : PeerConf {
   static const bool RxPipeline = true;
 };
+// the classify in the resident service (pn_service_*: a post per poll, no launch), every poll and pipelined
+// (two posts outstanding)
+struct PeerConfResident : PeerConf {
+  static const bool RxResident = true;
+};
+struct PeerConfPipeResident : PeerConfPipe {
+  static const bool RxResident = true;
+};
 
 template <class Backend, class Conf = PeerConf>
 struct Run {
@@ -271,6 +279,8 @@ int main(int argc, char** argv) {
     fail += scenario<PeerConfBudget>(gpu, pop, "3-ms RX latency budget");
     fail += scenario<PeerConfChunk>(gpu, pop, "RX chunks of 16");
     fail += scenario<PeerConfPipe>(gpu, pop, "pipelined RX (dispatch one poll later)");
+    fail += scenario<PeerConfResident>(gpu, pop, "resident service, every poll");
+    fail += scenario<PeerConfPipeResident>(gpu, pop, "resident service, pipelined RX");
     if (g_seed == 0) fail += wrapper_admission(gpu, pop);
   }
   std::printf("%s\n", fail ? "FAIL" : "PASS");

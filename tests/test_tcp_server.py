@@ -61,11 +61,12 @@ def test_server_twin_reactive_peers():
 
 @pytest.mark.gpu
 def test_gpu_server_reactive_peers_match_twin():
-    """The same on the GPU backend, 4 populations x 4 RX modes (every poll, latency budget,
-    chunks, pipelined): handler log and every TX frame equal to the twin's in each run."""
+    """The same on the GPU backend, 4 populations x 6 RX modes (every poll, latency budget,
+    chunks, pipelined, and the resident service every poll and pipelined): handler log and every TX frame
+    equal to the twin's in each run."""
     p = _peer("gpu", 4)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 16, p.stdout
+    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 24, p.stdout
 
 
 CLISRV = os.path.join(ROOT, "tests", "cpp", "test_tcp_client_server")
