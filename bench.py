@@ -584,10 +584,11 @@ def secondary_streams(torch, pa, ctx, frames_b, slots, n, stream):
 def server_poll():
     """The drop-in server itself (bench/bench_tcp_server quick, DESIGN §14): GpuTcpServer::poll over
     256 connections receiving in-order 1514-B segments from a pinned host ring (handshake, RX, the
-    server's ACKs), GPU backend at RxBatch 512 and pipelined at 16384, the same two with the checksum
-    discard off (the reference's release path: the kernel reads each frame's header lines only,
-    pn_set_verify), and the same server on the sequential CPU backend (the oracle classifying each frame
-    on one core).  PCIe-bound: with checksums verified every frame crosses it whole."""
+    server's ACKs), GPU backend at RxBatch 512 and pipelined at 16384; at 512 also pipelined, through the
+    resident classify service (Conf::RxResident, pn_service_*: a post per poll, no launch) and both; each
+    with the checksum discard off too (the reference's release path: the kernel reads each frame's header
+    lines only, pn_set_verify), and the same server on the sequential CPU backend (the oracle classifying
+    each frame on one core).  PCIe-bound: with checksums verified every frame crosses it whole."""
     import subprocess
 
     exe = os.path.join(ROOT, "bench", "bench_tcp_server")
@@ -883,6 +884,11 @@ def summary(out):
             "server_512_resident_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_resident", "mframes_per_s"),
             "server_512_resident_release_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_resident_release_path",
                                                   "mframes_per_s"),
+            "server_512_pipelined_resident_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_pipelined_resident",
+                                                    "mframes_per_s"),
+            "server_512_pipelined_resident_release_mfps": g(sec, "tcp_server_poll",
+                                                            "gpu_rxbatch_512_pipelined_resident_release_path",
+                                                            "mframes_per_s"),
             "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s")})
     if cpu:
         s.update({"cpu_ref_gbit_per_s": cpu.get("value"), "cpu_ref_min_max": [cpu.get("min"), cpu.get("max")],
