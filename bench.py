@@ -626,8 +626,9 @@ def sniffer_streams():
 
 def small_batch_latency():
     """Host-visible round trip of one small batch (bench/bench_signal): pn_classify +
-    stream sync against pn_classify_notify + a spin on the pinned completion word, 64 / 512 / 1024
-    C2 frames, device-resident and zero-copy; median host wall clock, records compared."""
+    stream sync against pn_classify_notify + a spin on the pinned completion word against a post to the
+    resident classify service (pn_service_post + pn_service_wait), 64 / 512 / 1024 C2 frames,
+    device-resident and zero-copy, verified and release path; median host wall clock, records compared."""
     import subprocess
 
     exe = os.path.join(ROOT, "bench", "bench_signal")
@@ -889,7 +890,12 @@ def summary(out):
             "server_512_pipelined_resident_release_mfps": g(sec, "tcp_server_poll",
                                                             "gpu_rxbatch_512_pipelined_resident_release_path",
                                                             "mframes_per_s"),
-            "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s")})
+            "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s"),
+            "zero_copy_64_us_notify_vs_service": [g(sec, "small_batch_latency", "zero_copy", "64", "signal_us"),
+                                                  g(sec, "small_batch_latency", "zero_copy", "64", "service_us")],
+            "zero_copy_64_release_us_notify_vs_service": [
+                g(sec, "small_batch_latency", "zero_copy_release_path", "64", "signal_us"),
+                g(sec, "small_batch_latency", "zero_copy_release_path", "64", "service_us")]})
     if cpu:
         s.update({"cpu_ref_gbit_per_s": cpu.get("value"), "cpu_ref_min_max": [cpu.get("min"), cpu.get("max")],
                   "cpu_ref_cores": cpu.get("cores"), "cpu_ref_consistent_with_sweep": cpu.get("consistent_with_sweep"),
