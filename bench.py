@@ -587,8 +587,11 @@ def server_poll():
     server's ACKs), GPU backend at RxBatch 512 and pipelined at 16384; at 512 also pipelined, through the
     resident classify service (Conf::RxResident, pn_service_*: a post per poll, no launch) and both; each
     with the checksum discard off too (the reference's release path: the kernel reads each frame's header
-    lines only, pn_set_verify), and the same server on the sequential CPU backend (the oracle classifying
-    each frame on one core).  PCIe-bound: with checksums verified every frame crosses it whole."""
+    lines only, pn_set_verify), the same server on the sequential CPU backend (the oracle classifying each
+    frame on one core), and the reference's own server (pollnet's EfviTcpServer over efvitcp, compiled from
+    /root/reference at build time, oracle/ref_server.hpp) on one core: 64 events per pollNet, the release
+    build pollnet ships, no RX checksum (the NIC's job).  PCIe-bound: with checksums verified every frame
+    crosses it whole."""
     import subprocess
 
     exe = os.path.join(ROOT, "bench", "bench_tcp_server")
@@ -891,6 +894,7 @@ def summary(out):
                                                             "gpu_rxbatch_512_pipelined_resident_release_path",
                                                             "mframes_per_s"),
             "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s"),
+            "server_reference_release_mfps": g(sec, "tcp_server_poll", "reference_server_release_build", "mframes_per_s"),
             "zero_copy_64_us_notify_vs_service": [g(sec, "small_batch_latency", "zero_copy", "64", "signal_us"),
                                                   g(sec, "small_batch_latency", "zero_copy", "64", "service_us")],
             "zero_copy_64_release_us_notify_vs_service": [

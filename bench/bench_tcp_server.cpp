@@ -11,23 +11,32 @@
 // bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
-//   argv: n_flows (256)  polls (400)  [cpu|quick]   prints one JSON line; exit 0 = all data delivered
+//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|twin_timed]   prints one JSON line; exit 0 = all data delivered
 //         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512 (also pipelined),
 //         GPU pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
 //         checksum summed) — bench.py's secondary.tcp_server_poll)
 #include <arpa/inet.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../include/pollnet_amd/tcp_server.hpp"
 #include "../tests/cpp/segframes.hpp"
 #include "../tests/cpp/server_harness.hpp"
+// The reference's own server (pollnet's EfviTcpServer over efvitcp's TcpServer / TcpConn, compiled from the text
+// oracle/ref.mk extracts from /root/reference; only the ef_vi plumbing is restated, oracle/ref_server.hpp) as the
+// CPU baseline of the release-path legs, where that text was present at build time.
+#if __has_include("../oracle/_ref/conn_efvitcpserver.inc")
+#define PN_BENCH_REF 1
+#include "../oracle/ref_server.hpp"
+#endif
 
 using namespace pollnet_amd;
 using Clock = std::chrono::steady_clock;
@@ -48,6 +57,15 @@ struct BenchLink {
   uint64_t acks = 0, rsts = 0, synacks = 0, other = 0;
   uint8_t other_flags = 0;
   double fill_s = 0;
+  // a poll smaller than the flow count (the reference's 64 events per pollNet): handshakes continue over polls
+  // from hs_next, data frames rotate over the flows (each slot gets its flow's 54-B header from hdr, payload
+  // written once per slot), seg_k counts each flow's segments
+  uint32_t hs_next = 0, cursor = 0;
+  std::vector<uint8_t> hdr;
+  std::vector<uint64_t> seg_k;
+  const uint8_t* paid_base = nullptr; // the slots [0, paid_n) of that ring already hold the payload
+  uint32_t paid_n = 0;
+  uint64_t data_frames = 0;
 
   static uint32_t ip(uint32_t f) { return 0x0a010000u | f; }
   static uint16_t port(uint32_t f) { return (uint16_t)(32768 + (f * 7919) % 28000); }
@@ -75,13 +93,46 @@ struct BenchLink {
     const auto t0 = Clock::now();
     uint32_t n = 0;
     if (phase == Syn || phase == Ack) {
-      for (uint32_t f = 0; f < n_flows && f < cap; f++, n++) {
+      for (; hs_next < n_flows && n < cap; hs_next++, n++) {
+        const uint32_t f = hs_next;
         segtest::Seg s = phase == Syn ? seg(f, segtest::SYN, cli_isn[f], 0)
                                       : seg(f, segtest::ACK, cli_isn[f] + 1, srv_isn[f] + 1);
         if (phase == Syn) s.opts = {2, 4, 0x05, 0xb4}; // MSS 1460
-        segtest::build(slots + (size_t)f * stride + off, s);
+        segtest::build(slots + (size_t)n * stride + off, s);
       }
-      phase = Idle;
+      if (hs_next == n_flows) phase = Idle, hs_next = 0;
+    } else if (phase == Data && cap < n_flows) {
+      if (hdr.empty()) { // each flow's data-frame header with seq 0, and its TCP sum without the checksum field
+        hdr.resize((size_t)n_flows * 54);
+        seg_k.assign(n_flows, 0);
+        std::vector<uint8_t> fr(2048);
+        for (uint32_t f = 0; f < n_flows; f++) {
+          segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, srv_isn[f] + 1);
+          s.payload = payload.data();
+          s.len = kPayload;
+          segtest::build(fr.data(), s);
+          std::memcpy(&hdr[(size_t)f * 54], fr.data(), 54);
+          sum_base[f] = (uint16_t)~(uint16_t)(fr[50] << 8 | fr[51]);
+        }
+      }
+      for (; n < cap; n++) {
+        const uint32_t f = cursor;
+        cursor = cursor + 1 == n_flows ? 0 : cursor + 1;
+        uint8_t* eth = slots + (size_t)n * stride + off;
+        if (slots != paid_base) paid_base = slots, paid_n = 0;
+        if (n >= paid_n) {
+          std::memcpy(eth + 54, payload.data(), kPayload);
+          paid_n = n + 1;
+        }
+        std::memcpy(eth, &hdr[(size_t)f * 54], 54);
+        const uint32_t seq = dataSeq(f, seg_k[f]++);
+        segtest::put32(eth + 38, seq);
+        uint32_t acc = sum_base[f] + (seq >> 16) + (seq & 0xffff);
+        acc = (acc & 0xffff) + (acc >> 16);
+        acc = (acc & 0xffff) + (acc >> 16);
+        segtest::put16(eth + 50, (uint16_t)~acc);
+      }
+      data_frames += n;
     } else if (phase == Data) {
       const uint32_t per_flow = cap / n_flows;
       n = per_flow * n_flows;
@@ -113,6 +164,7 @@ struct BenchLink {
         segtest::put16(tcp + 16, (uint16_t)~acc);
       }
       poll_no++;
+      data_frames += n;
     }
     fill_s += secs(t0, Clock::now());
     return n;
@@ -157,6 +209,38 @@ struct Handler {
   void onTcpDisconnect(C&) {
     disconnected++;
   }
+  template <class C>
+  void onSendTimeout(C&) {}
+  template <class C>
+  void onRecvTimeout(C&) {}
+};
+
+// The sequential backend with its legs timed: pipelined, a poll's frames are classified in launch() and dispatched
+// (the engine's per-record host work: NIC filter, connection, onPack, handler, ACK decisions) in collect(), so the
+// host dispatch cost per frame is measured on its own -- the part of a poll the GPU backend leaves on the host.
+struct TimedOracleBackend : OracleBackend {
+  double launch_s = 0, collect_s = 0, tx_s = 0;
+  uint64_t collected = 0;
+  const char* launch(uint32_t half, uint32_t n, const ConnTable& t) {
+    const auto t0 = Clock::now();
+    const char* e = OracleBackend::launch(half, n, t);
+    launch_s += secs(t0, Clock::now());
+    return e;
+  }
+  template <class F>
+  const char* collect(uint32_t half, uint32_t n, const ConnTable& t, F&& f) {
+    const auto t0 = Clock::now();
+    const char* e = OracleBackend::collect(half, n, t, f);
+    collect_s += secs(t0, Clock::now());
+    collected += n;
+    return e;
+  }
+  const char* fillTxLaunch(uint32_t n, uint32_t half) {
+    const auto t0 = Clock::now();
+    const char* e = OracleBackend::fillTxLaunch(n, half);
+    tx_s += secs(t0, Clock::now());
+    return e;
+  }
 };
 
 template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false>
@@ -176,6 +260,7 @@ struct Conf {
 
 struct Run {
   double mfps = 0, us_poll = 0, acks_per_frame = 0, fill_share = 0, classify_share = 0, tx_share = 0;
+  double ns_classify = -1, ns_dispatch = -1; // TimedOracleBackend: per frame, in launch() / collect()
   bool ok = false;
   std::string err;
 };
@@ -231,18 +316,16 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   for (uint32_t p = 0; p < polls; p++)
     if (be.classify(n, srv->table(), [](uint64_t, const pn_result&, const uint8_t*) {})) break;
   const auto c1 = Clock::now();
-  // the TX leg as the engine runs it for a poll's ACKs: header-only frames summed on the host
-  // (below TxGpuMinDataFrames payload frames), else one pn_tx_fill launch
-  for (uint32_t p = 0; p < polls && acks; p++) {
-    if (Server::kTxGpuMin > 0) {
-      for (uint32_t i = 0; i < acks; i++)
-        srv_detail::fill_tcp_checksums(be.txSlots(0) + (size_t)i * Backend::kStride + Backend::kFrameOff);
-    } else if (be.fillTx(acks)) {
-      break;
-    }
-  }
+  // the TX leg as the engine runs it for a poll's ACKs: header-only frames get their sums as they are built (part
+  // of the dispatch), so only a batch for pn_tx_fill (TxGpuMinDataFrames 0) is timed here
+  for (uint32_t p = 0; p < polls && acks && Server::kTxGpuMin == 0; p++)
+    if (be.fillTx(acks)) break;
   out.classify_share = secs(c0, c1) / t;
   out.tx_share = secs(c1, Clock::now()) / t;
+  if constexpr (std::is_same_v<Backend, TimedOracleBackend>) {
+    out.ns_classify = be.collected ? be.launch_s * 1e9 / be.collected : 0;
+    out.ns_dispatch = be.collected ? be.collect_s * 1e9 / be.collected : 0;
+  }
   out.ok = timed_bytes == frames * kPayload && h.bytes == (uint64_t)link.poll_no * (kBatch / n_flows) * n_flows * kPayload &&
            !link.rsts && !link.other && !h.disconnected && srv->getLastError() == nullptr;
   if (!out.ok)
@@ -253,16 +336,93 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   return out;
 }
 
+#ifdef PN_BENCH_REF
+// pollnet's EfviTcpServer Conf for the same server (its ServerConf fixes the rest, EfviTcp.h:191-212: 512 RX slots,
+// 64 events per pollNet, 1024 1-KiB send buffers per connection -- ~1 GiB at MaxConns 1024)
+struct RefBenchConf {
+  static const uint32_t RecvBufSize = 65536;
+  static const uint32_t MaxConns = 1024;
+  static const uint32_t SendTimeoutSec = 0;
+  static const uint32_t RecvTimeoutSec = 0;
+  struct UserData {};
+};
+
+// The reference's own server on the same workload, one core: each poll takes at most 64 frames (Core.h:496-498),
+// so the same frames as `polls` polls of 512 take 8x the polls.  Built without EFVITCP_DEBUG, as pollnet ships it:
+// no checksum is verified (the release path).
+static Run runRef(uint32_t n_flows, uint32_t polls) {
+  Run out;
+  using Srv = efvitcp::EfviTcpServer<RefBenchConf>;
+  auto link = std::make_unique<BenchLink>();
+  link->setup(n_flows);
+  efvitcp::RefEnv& env = efvitcp::refEnv();
+  env.link = link.get();
+  env.fill = [](void* l, uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
+    return static_cast<BenchLink*>(l)->fill(slots, stride, off, cap);
+  };
+  env.send = [](void* l, const uint8_t* eth, uint32_t len) { static_cast<BenchLink*>(l)->send(eth, len); };
+  timespec ts;
+  ::clock_gettime(CLOCK_REALTIME, &ts); // the reference's clock (Core::getns)
+  env.init_ns = ts.tv_sec * 1000000000LL + ts.tv_nsec;
+  env.local_ip = link->localIp();
+  std::memcpy(env.local_mac, link->localMac(), 6);
+  std::unique_ptr<Srv> srv(new Srv());
+  if (!srv->init("bench", "10.0.0.1", 1234)) {
+    out.err = srv->getLastError();
+    return out;
+  }
+  Handler h;
+  link->phase = BenchLink::Syn;
+  for (int k = 0; k < 64 && link->synacks < n_flows; k++) srv->poll(h);
+  link->phase = BenchLink::Ack;
+  for (int k = 0; k < 64 && h.connected < n_flows; k++) srv->poll(h);
+  if (h.connected != n_flows || link->rsts) {
+    out.err = "reference handshake: " + std::to_string(h.connected) + " connected, " + std::to_string(link->rsts) + " RSTs";
+    return out;
+  }
+  link->phase = BenchLink::Data;
+  const uint32_t ref_polls = polls * 8, warm = 64;
+  for (uint32_t p = 0; p < warm; p++) srv->poll(h);
+  const uint64_t bytes0 = h.bytes, acks0 = link->acks, frames0 = link->data_frames;
+  link->fill_s = 0;
+  const auto t0 = Clock::now();
+  for (uint32_t p = 0; p < ref_polls; p++) srv->poll(h);
+  const double t = secs(t0, Clock::now());
+  const uint64_t frames = link->data_frames - frames0;
+  out.mfps = frames / t / 1e6;
+  out.us_poll = t * 1e6 / ref_polls;
+  out.acks_per_frame = (double)(link->acks - acks0) / frames;
+  out.fill_share = link->fill_s / t;
+  out.ok = frames == (uint64_t)ref_polls * 64 && h.bytes - bytes0 == frames * kPayload &&
+           h.bytes == link->data_frames * kPayload && !link->rsts && !link->other && !h.disconnected;
+  if (!out.ok)
+    out.err = "reference: delivered " + std::to_string(h.bytes - bytes0) + " B of " + std::to_string(frames) + " frames, " +
+              std::to_string(link->rsts) + " RSTs, " + std::to_string(link->other) + " other frames, " +
+              std::to_string(h.disconnected) + " disconnects";
+  return out;
+}
+#endif
+
 static std::string json(const Run& r) {
-  char b[384];
+  char b[448];
   if (!r.err.empty() && !r.ok) {
     std::snprintf(b, sizeof b, "{\"error\": \"%s\"}", r.err.c_str());
     return b;
   }
   std::snprintf(b, sizeof b,
                 "{\"mframes_per_s\": %.3f, \"gbit_per_s\": %.1f, \"us_per_poll\": %.1f, \"acks_per_frame\": %.3f, "
-                "\"link_fill_share\": %.3f, \"classify_share\": %.3f, \"tx_fill_share\": %.3f}",
-                r.mfps, r.mfps * 1514 * 8 / 1e3, r.us_poll, r.acks_per_frame, r.fill_share, r.classify_share, r.tx_share);
+                "\"link_fill_share\": %.3f, \"mframes_per_s_server_only\": %.3f, \"classify_share\": %.3f, "
+                "\"tx_fill_share\": %.3f}",
+                r.mfps, r.mfps * 1514 * 8 / 1e3, r.us_poll, r.acks_per_frame, r.fill_share,
+                r.fill_share < 1 ? r.mfps / (1 - r.fill_share) : 0.0, r.classify_share, r.tx_share);
+  if (r.ns_dispatch >= 0) {
+    std::string o(b);
+    o.pop_back();
+    char x[160];
+    std::snprintf(x, sizeof x, ", \"ns_per_frame_total\": %.2f, \"ns_per_frame_classify\": %.2f, \"ns_per_frame_dispatch\": %.2f}",
+                  r.mfps > 0 ? 1e3 / r.mfps : 0.0, r.ns_classify, r.ns_dispatch);
+    return o + x;
+  }
   return b;
 }
 
@@ -280,7 +440,15 @@ int main(int argc, char** argv) {
     ok = ok && r.ok;
   };
   const bool cpu_only = argc > 3 && std::strcmp(argv[3], "cpu") == 0;
-  if (argc > 3 && std::strcmp(argv[3], "quick") == 0) { // bench.py's secondary leg
+  if (argc > 3 && std::strcmp(argv[3], "twin_timed") == 0) { // the host dispatch alone (profiling)
+    leg("cpu_rxbatch_512_pipelined_release_path_timed", runOne<512, TimedOracleBackend, 0, true>(n_flows, polls, false));
+  } else if (argc > 3 && std::strcmp(argv[3], "release_pair") == 0) { // one pair on its own (profiling the host side)
+    leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
+    leg("cpu_rxbatch_512_pipelined_release_path_timed", runOne<512, TimedOracleBackend, 0, true>(n_flows, polls, false));
+#ifdef PN_BENCH_REF
+    leg("reference_server_release_build", runRef(n_flows, polls));
+#endif
+  } else if (argc > 3 && std::strcmp(argv[3], "quick") == 0) { // bench.py's secondary leg
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
     leg("gpu_rxbatch_512_release_path", runOne<512, GpuBackend>(n_flows, polls, false));
@@ -297,6 +465,9 @@ int main(int argc, char** argv) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     // the same sequential server with the discard off: the reference's release build (no checksum summed per frame)
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
+#ifdef PN_BENCH_REF
+    leg("reference_server_release_build", runRef(n_flows, polls));
+#endif
   } else if (!cpu_only) {
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_4096", runOne<4096, GpuBackend>(n_flows, polls));
@@ -311,11 +482,15 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_4096_pipelined", runOne<4096, GpuBackend, 0, true>(n_flows, polls));
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
   }
-  if (argc <= 3 || std::strcmp(argv[3], "quick") != 0) {
+  if (argc <= 3 || (std::strcmp(argv[3], "quick") != 0 && std::strcmp(argv[3], "release_pair") != 0 &&
+                    std::strcmp(argv[3], "twin_timed") != 0)) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
     leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
     leg("cpu_rxbatch_4096_pipelined", runOne<4096, OracleBackend, 0, true>(n_flows, polls / 4));
+#ifdef PN_BENCH_REF
+    leg("reference_server_release_build", runRef(n_flows, polls));
+#endif
   }
   std::printf("{\"bench\": \"tcp_server_poll\", \"workload\": \"%u flows connected through the server's handshake, "
               "in-order 1514-B frames (1460-B payload), RxBatch frames per poll, handler consumes, server ACKs\", "

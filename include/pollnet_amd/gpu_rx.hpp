@@ -28,6 +28,14 @@
 
 namespace pollnet_amd {
 
+// connHashKey (Core.h:167-172), inline for the per-record host walk: the remote ip (host order) << 15 | the low 15
+// port bits, the port's msb at bit 47.  pn_conn_hash_key is the same function behind the C ABI (conn_table.cpp);
+// tests/cpp/test_tx_host.cpp checks it against the oracle's.
+inline uint64_t conn_hash_key(uint32_t ip_be, uint16_t port_be) {
+  const uint64_t ip = __builtin_bswap32(ip_be), p = __builtin_bswap16(port_be);
+  return (ip << 15) | (p & 0x7fff) | ((p & 0x8000) << 32);
+}
+
 // A record's checksum verdicts: both OK, or the IP one OK where the TCP sum was not computed (the release
 // path, pn_set_verify(ctx, 0): PN_F_TCP_UNCHECKED).
 inline bool checksums_ok(uint16_t flags) {
@@ -66,7 +74,7 @@ class ConnTable {
                ? "pn_table_create failed"
                : nullptr;
   }
-  static uint64_t key(uint32_t ip_be, uint16_t port_be) { return pn_conn_hash_key(ip_be, port_be); } // Core.h:167
+  static uint64_t key(uint32_t ip_be, uint16_t port_be) { return conn_hash_key(ip_be, port_be); } // Core.h:167
   bool find(uint64_t key, uint32_t* entry_idx, uint32_t* conn_id) const {                              // Core.h:558
     int hit = 0;
     pn_table_find(t_, key, entry_idx, &hit, conn_id);
@@ -266,7 +274,7 @@ class GpuRx {
       uint16_t port_be;
       std::memcpy(&ip_be, eth + 14 + 12, 4);  // ip_hdr->src_ip
       std::memcpy(&port_be, eth + 14 + 20, 2); // tcp_hdr->src_port (tcp = ip + 20)
-      const uint64_t key = pn_conn_hash_key(ip_be, port_be);
+      const uint64_t key = conn_hash_key(ip_be, port_be);
       if (r.flags & PN_F_TW) {
         tw_handler(key, r.conn_id - max_conn_, eth, r);
       } else {

@@ -150,6 +150,25 @@ inline uint16_t csum_fold(uint64_t s) { // CSum::fold (Core.h:94-98), carries fo
   while (s >> 16) s = (s & 0xffff) + (s >> 16);
   return (uint16_t)~s;
 }
+// Both checksums of a header-only frame (20-B IP header, 20-B TCP header, no payload) from the field values the
+// engine writes (TcpEngine::header), without reading the frame back: the same native-order word sums
+// fill_tcp_checksums takes over those bytes, so the same folded values (tests/cpp/test_tx_host.cpp), as the
+// reference's SendBuf::setOptDataLen folds them from its cached header sums (Core.h:157-163).  Addresses and ports
+// are given in memory (network) order, the rest as numbers.
+struct HeaderSums {
+  uint16_t ip, tcp;
+};
+inline HeaderSums header_sums(uint32_t src_ip_mem, uint32_t dst_ip_mem, uint16_t src_port_mem, uint16_t dst_port_mem,
+                              uint32_t seq, uint32_t ack, uint8_t flags, uint16_t window) {
+  auto halves = [](uint32_t x) -> uint64_t { return (x & 0xffffu) + (x >> 16); };
+  const uint64_t addr = halves(src_ip_mem) + halves(dst_ip_mem);
+  // 45 00 | tot_len 40 | id 0 | 40 00 (DF) | ttl 64, proto 6 | checksum | addresses, as native 16-bit loads
+  const uint64_t ip = 0x0045u + 0x2800u + 0x0040u + 0x0640u + addr;
+  // pseudo-header (addresses, protocol 6, TCP length 20), ports, seq, ack, doff 5 | flags, window
+  const uint64_t tcp = addr + 0x0600u + 0x1400u + src_port_mem + dst_port_mem + halves(__builtin_bswap32(seq)) +
+                       halves(__builtin_bswap32(ack)) + (0x50u | (uint32_t)flags << 8) + __builtin_bswap16(window);
+  return {csum_fold(ip), csum_fold(tcp)};
+}
 // Both checksums of a built TCP/IPv4 frame (eth = Ethernet header; 20-B IP header, as every
 // frame the engine builds): the values SendBuf::setOptDataLen folds from its cached header sums
 // (Core.h:157-163, at the end of TcpConn::sendBuf, TcpConn.h:310-323) and pn_tx_fill(PN_TX_TCP)
@@ -593,7 +612,6 @@ class TcpEngine {
     uint16_t peer_port_ = 0;   // network order
     uint16_t local_port_ = 0;  // network order
     uint8_t peer_mac_[6] = {};
-    RxConn<IConf> rx_;
     // send side (TcpConn.h:861-898)
     std::unique_ptr<Seg[]> segs_;
     std::unique_ptr<uint8_t[]> data_;
@@ -601,6 +619,9 @@ class TcpEngine {
     uint32_t smss_ = 536, send_wnd_seq_ = 0, rto_ = 1000, srtt_ = 0, rttvar_ = 0, dup_ack_cnt_ = 0, retries_ = 0;
     bool established_ = false, fin_sent_ = true, fin_received_ = true, fast_re_ = false, in_recover_ = false;
     TimerNode timers_[4]; // resend, delayed ACK, user 0 (send timeout), user 1 (recv timeout)
+    // last: the receive half's state leads its 64-KiB buffer, so everything a segment touches on the common path
+    // (the fields above and the receive state) sits in the connection's first few cache lines
+    RxConn<IConf> rx_;
   };
 
   TcpEngine() : conns_(kMaxConn), tws_(kMaxTw) {}
@@ -646,9 +667,11 @@ class TcpEngine {
     } else if (const char* e2 = be_.fillTx(tx_n_, tx_cur_)) {
       err_ = e2;
       tx_n_ = tx_data_n_ = 0;
+      tx_fill_[tx_cur_].clear();
       return e2;
     } else {
       tx_gpu_frames_ += tx_n_;
+      tx_fill_[tx_cur_].clear(); // pn_tx_fill writes every frame's checksums
     }
     sendTx(tx_cur_, tx_n_);
     tx_n_ = tx_data_n_ = 0;
@@ -746,6 +769,10 @@ class TcpEngine {
     }
     for (uint32_t i = 0; i < kMaxTw; i++) tws_[i].timer.owner = kMaxConn + i;
     tx_n_ = tx_data_n_ = rx_pending_ = cur_ = tx_cur_ = tx_fl_n_ = 0;
+    for (auto& v : tx_fill_) {
+      v.clear();
+      v.reserve(kTxBatch);
+    }
     fl_n_[0] = fl_n_[1] = 0;
     ++tver_;
     ready_ = true;
@@ -767,9 +794,10 @@ class TcpEngine {
     }
   }
   bool txOnHost() const { return tx_data_n_ < kTxGpuMin; }
-  void fillTxHost(uint32_t half, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++)
+  void fillTxHost(uint32_t half, uint32_t n) { // the frames header() left unsummed (header-only ones are done)
+    for (const uint32_t i : tx_fill_[half])
       srv_detail::fill_tcp_checksums(be_.txSlots(half) + (size_t)i * Backend::kStride + Backend::kFrameOff);
+    tx_fill_[half].clear();
     tx_host_frames_ += n;
   }
   // Pipelined TX: start filling the frames built so far and switch to the other batch ...
@@ -781,9 +809,11 @@ class TcpEngine {
     } else if (const char* e = be_.fillTxLaunch(tx_n_, tx_cur_)) {
       err_ = e;
       tx_n_ = tx_data_n_ = 0;
+      tx_fill_[tx_cur_].clear();
       return;
     } else {
       tx_gpu_frames_ += tx_n_;
+      tx_fill_[tx_cur_].clear(); // pn_tx_fill writes every frame's checksums
     }
     tx_fl_n_ = tx_n_;
     tx_n_ = tx_data_n_ = 0;
@@ -1248,7 +1278,8 @@ class TcpEngine {
     }
   }
 
-  // ---- frame building: headers only; both checksums are written at flush (flushTx) ----
+  // ---- frame building: a header-only frame gets both checksums as it is built; one with options or payload at
+  // flush (flushTx: on the host, or the whole batch by pn_tx_fill) ----
   enum Kind { kSyn, kSynAck, kData, kFinAck, kAck, kRstAck };
   uint8_t* txFrame() {
     if (tx_n_ == kTxBatch) flushTx();
@@ -1280,7 +1311,14 @@ class TcpEngine {
     tcp[12] = (uint8_t)(doff_words << 4);
     tcp[13] = flags;
     wr16(tcp + 14, window);
-    wr32(tcp + 16, 0); // checksum (filled at flush), urgent pointer
+    wr32(tcp + 16, 0); // checksum, urgent pointer
+    if (doff_words == 5 && tcp_len == 20) { // header only: both checksums now, from the values
+      const HeaderSums cs = header_sums(local_ip_, dst_ip, src_port, dst_port, seq, ack, flags, window);
+      std::memcpy(ip + 10, &cs.ip, 2);
+      std::memcpy(tcp + 16, &cs.tcp, 2);
+    } else { // options or payload follow: summed at flush, on the host or by pn_tx_fill
+      tx_fill_[tx_cur_].push_back(tx_n_ - 1);
+    }
   }
   // A segment of connection c (TcpConn::sendBuf, TcpConn.h:310-323): ack = what was received
   // so far (updateLastAck, TcpConn.h:838-843), window = free receive buffer.
@@ -1359,6 +1397,7 @@ class TcpEngine {
   uint32_t cur_ = 0, fl_n_[2] = {0, 0};
   uint32_t tx_cur_ = 0, tx_fl_n_ = 0; // TX batch being built; frames of the other one in its fill (pipelined)
   uint32_t tx_data_n_ = 0;            // payload-bearing frames in the batch being built
+  std::vector<uint32_t> tx_fill_[2];  // per TX batch: the frames whose checksums are filled at flush
   bool tx_fl_host_ = false;           // the batch in its fill was summed on the host
   uint64_t tx_host_frames_ = 0, tx_gpu_frames_ = 0;
   uint64_t re_resolved_ = 0;

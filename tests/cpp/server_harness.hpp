@@ -71,7 +71,7 @@ struct OracleBackend {
     uint16_t port_be;
     std::memcpy(&ip_be, eth + 26, 4);
     std::memcpy(&port_be, eth + 34, 2);
-    return pn_conn_hash_key(ip_be, port_be);
+    return pollnet_amd::conn_hash_key(ip_be, port_be);
   }
   void one(const uint8_t* eth, const pollnet_amd::ConnTable& t, pn_result* r) const {
     uint32_t ne = 0;
