@@ -116,3 +116,27 @@ def test_engine_host_tx_checksums_equal_oracle_fill():
         subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tx_host"], check=True, capture_output=True)
     p = subprocess.run([TXHOST, "20000"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "PASS" in p.stdout, p.stdout + p.stderr
+
+
+SRVBENCH = os.path.join(ROOT, "bench", "bench_tcp_server")
+
+
+def test_server_bench_release_pair_cpu():
+    """bench_tcp_server's host-side legs (no GPU): the sequential twin on the release path, the same pipelined with
+    its classify / dispatch split timed, and -- where the reference's text was present at build -- the reference's
+    own server (oracle/ref_server.hpp) on the same workload, 64 events per pollNet.  Every leg must deliver every
+    byte (no RST, no disconnect), and the reference leg must ACK every second segment as the engine does."""
+    import json
+
+    if not os.path.exists(SRVBENCH):
+        subprocess.run(["make", "-C", ROOT, "bench/bench_tcp_server"], check=True, capture_output=True)
+    p = subprocess.run([SRVBENCH, "256", "40", "release_pair"], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["delivered_ok"] is True
+    timed = line["cpu_rxbatch_512_pipelined_release_path_timed"]
+    assert timed["ns_per_frame_dispatch"] > 0 and timed["ns_per_frame_classify"] > 0
+    assert line["cpu_rxbatch_512_release_path"]["acks_per_frame"] == pytest.approx(0.5, abs=0.01)
+    if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "conn_efvitcpserver.inc")):
+        ref = line["reference_server_release_build"]
+        assert ref["mframes_per_s"] > 0 and ref["acks_per_frame"] == pytest.approx(0.5, abs=0.01)
