@@ -171,3 +171,56 @@ def test_service_argument_checks(torch):
             svc.close()
     finally:
         ctx.close()
+
+
+def test_service_soak_random_posts_and_relaunches(torch):
+    """1,500 posts of random size (1 .. 4,096 frames) at random offsets into one pinned ring, verified or release
+    path at random, one or two outstanding, with idle gaps longer than idle_ms (2 ms) between some of them so the
+    kernel ends and is relaunched many times, some posts landing while it ends.  Every post's records equal the
+    oracle's, and every launch ended by itself or at close."""
+    rng = np.random.default_rng(0x50A4)
+    N = 16384
+    p, s = _frames(3, N)
+    table = pa.gen_conn_table(p)
+    exp = {True: _expected(s, N, table), False: _expected(s, N, table, verify=False)}
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=2)
+        try:
+            host = _pinned(torch, s)
+            outs = [torch.zeros(4096 * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            pending = []  # (post id, out index, first frame, n, verify)
+
+            def check(item):
+                pid, o, first, n, verify = item
+                svc.wait(pid)
+                got = outs[o].numpy()[: n * 16].view(pa.RESULT_DTYPE)
+                assert np.array_equal(got, exp[verify][first:first + n]), (pid, first, n, verify)
+
+            relaunch_gaps = 0
+            for k in range(1500):
+                if len(pending) == 2 or (pending and rng.random() < 0.5):
+                    check(pending.pop(0))
+                verify = bool(rng.random() < 0.5)
+                if not pending:  # the verify setting is the ctx's at the post: change it only with nothing in flight
+                    ctx.set_verify(verify)
+                else:
+                    verify = pending[-1][4]
+                n = int(rng.integers(1, 4097))
+                first = int(rng.integers(0, N - n + 1))
+                o = k & 1
+                if pending and pending[0][1] == o:
+                    check(pending.pop(0))
+                pid = svc.post(host[first * STRIDE:], n, outs[o])
+                pending.append((pid, o, first, n, verify))
+                if rng.random() < 0.04:  # longer than idle_ms: the kernel ends before or while the next post arrives
+                    time.sleep(float(rng.uniform(0.001, 0.006)))
+                    relaunch_gaps += 1
+            while pending:
+                check(pending.pop(0))
+            assert relaunch_gaps > 20
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
