@@ -11,7 +11,7 @@
 // bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
-//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|twin_timed]   prints one JSON line; exit 0 = all data delivered
+//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|twin_timed|echo]   prints one JSON line; exit 0 = all data delivered
 //         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512 (also pipelined),
 //         GPU pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
 //         checksum summed) — bench.py's secondary.tcp_server_poll)
@@ -55,6 +55,11 @@ struct BenchLink {
   uint8_t* written[2] = {nullptr, nullptr}; // rings (halves, pipelined) whose slots hold full data frames
   uint32_t written_n = 0;
   uint64_t acks = 0, rsts = 0, synacks = 0, other = 0;
+  // echo workload: the peers acknowledge every byte the server sent them (their next frames carry it)
+  bool echo = false;
+  std::vector<uint32_t> flow_of_port; // port -> flow + 1
+  std::vector<uint64_t> srv_data;     // payload bytes the server sent each flow
+  uint64_t echo_bytes = 0, echo_frames = 0;
   uint8_t other_flags = 0;
   double fill_s = 0;
   // a poll smaller than the flow count (the reference's 64 events per pollNet): handshakes continue over polls
@@ -71,6 +76,9 @@ struct BenchLink {
   static uint16_t port(uint32_t f) { return (uint16_t)(32768 + (f * 7919) % 28000); }
   void setup(uint32_t n) {
     n_flows = n;
+    flow_of_port.assign(65536, 0);
+    for (uint32_t f = 0; f < n; f++) flow_of_port[port(f)] = f + 1;
+    srv_data.assign(n, 0);
     cli_isn.resize(n);
     srv_isn.assign(n, 0);
     sum_base.resize(n);
@@ -87,6 +95,17 @@ struct BenchLink {
     return s;
   }
   uint32_t dataSeq(uint32_t f, uint64_t k) const { return cli_isn[f] + 1 + (uint32_t)(k * kPayload); }
+  uint32_t ackOf(uint32_t f) const { return srv_isn[f] + 1 + (uint32_t)srv_data[f]; }
+  // a data frame's seq and ack (and its TCP checksum from the flow's base sum, built with both 0)
+  void patch(uint8_t* eth, uint32_t f, uint32_t seq) const {
+    const uint32_t ack = ackOf(f);
+    segtest::put32(eth + 38, seq);
+    segtest::put32(eth + 42, ack);
+    uint32_t acc = sum_base[f] + (seq >> 16) + (seq & 0xffff) + (ack >> 16) + (ack & 0xffff);
+    acc = (acc & 0xffff) + (acc >> 16);
+    acc = (acc & 0xffff) + (acc >> 16);
+    segtest::put16(eth + 50, (uint16_t)~acc);
+  }
 
   const char* open(const char*) { return nullptr; }
   uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
@@ -107,7 +126,7 @@ struct BenchLink {
         seg_k.assign(n_flows, 0);
         std::vector<uint8_t> fr(2048);
         for (uint32_t f = 0; f < n_flows; f++) {
-          segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, srv_isn[f] + 1);
+          segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, 0);
           s.payload = payload.data();
           s.len = kPayload;
           segtest::build(fr.data(), s);
@@ -125,12 +144,7 @@ struct BenchLink {
           paid_n = n + 1;
         }
         std::memcpy(eth, &hdr[(size_t)f * 54], 54);
-        const uint32_t seq = dataSeq(f, seg_k[f]++);
-        segtest::put32(eth + 38, seq);
-        uint32_t acc = sum_base[f] + (seq >> 16) + (seq & 0xffff);
-        acc = (acc & 0xffff) + (acc >> 16);
-        acc = (acc & 0xffff) + (acc >> 16);
-        segtest::put16(eth + 50, (uint16_t)~acc);
+        patch(eth, f, dataSeq(f, seg_k[f]++));
       }
       data_frames += n;
     } else if (phase == Data) {
@@ -139,12 +153,12 @@ struct BenchLink {
       if ((written[0] != slots && written[1] != slots) || written_n != n) { // first data poll: whole frames
         for (uint32_t i = 0; i < n; i++) {
           const uint32_t f = i % n_flows;
-          segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, srv_isn[f] + 1);
+          segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, 0);
           s.payload = payload.data();
           s.len = kPayload;
           uint8_t* eth = slots + (size_t)i * stride + off;
           segtest::build(eth, s);
-          if (i < n_flows) { // the sum without the checksum field and with seq 0
+          if (i < n_flows) { // the sum without the checksum field, with seq and ack 0
             const uint16_t c = (uint16_t)(eth[50] << 8 | eth[51]);
             sum_base[f] = (uint16_t)~c;
           }
@@ -153,15 +167,9 @@ struct BenchLink {
         (written[0] ? written[1] : written[0]) = slots;
         written_n = n;
       }
-      for (uint32_t i = 0; i < n; i++) { // seq and checksum of segment k of flow f
+      for (uint32_t i = 0; i < n; i++) { // seq, ack and checksum of segment k of flow f
         const uint32_t f = i % n_flows;
-        const uint32_t seq = dataSeq(f, poll_no * per_flow + i / n_flows);
-        uint8_t* tcp = slots + (size_t)i * stride + off + 34;
-        segtest::put32(tcp + 4, seq);
-        uint32_t acc = sum_base[f] + (seq >> 16) + (seq & 0xffff);
-        acc = (acc & 0xffff) + (acc >> 16);
-        acc = (acc & 0xffff) + (acc >> 16);
-        segtest::put16(tcp + 16, (uint16_t)~acc);
+        patch(slots + (size_t)i * stride + off, f, dataSeq(f, poll_no * per_flow + i / n_flows));
       }
       poll_no++;
       data_frames += n;
@@ -179,7 +187,18 @@ struct BenchLink {
         if (port(f) == dport) srv_isn[f] = (uint32_t)eth[38] << 24 | eth[39] << 16 | eth[40] << 8 | eth[41];
       synacks++;
     } else if ((flags & ~segtest::PSH) == segtest::ACK) { // pure ACKs carry PSH, as all of efvitcp's frames (TcpConn.h:427)
-      acks++;
+      const uint32_t tot = (uint32_t)(eth[16] << 8 | eth[17]), payload = tot - 20 - (eth[46] >> 4) * 4;
+      if (payload == 0) {
+        acks++;
+      } else if (echo) { // echoed data: the peer acknowledges it in its next frames
+        const uint32_t f = flow_of_port[(uint16_t)(eth[36] << 8 | eth[37])];
+        if (f) srv_data[f - 1] += payload;
+        echo_bytes += payload;
+        echo_frames++;
+      } else {
+        other++;
+        other_flags = flags;
+      }
     } else {
       other++;
       other_flags = flags;
@@ -191,14 +210,16 @@ struct BenchLink {
 };
 
 struct Handler {
-  uint64_t bytes = 0, calls = 0, sink = 0, connected = 0, disconnected = 0;
+  uint64_t bytes = 0, calls = 0, sink = 0, connected = 0, disconnected = 0, echo_refused = 0;
+  bool echo = false; // the reference example's echo server (example/tcpserver.cc): every delivery written back
   template <class C>
-  uint32_t onTcpData(C&, const uint8_t* d, uint32_t n) {
+  uint32_t onTcpData(C& c, const uint8_t* d, uint32_t n) {
     uint64_t w;
     std::memcpy(&w, d, 8);
     sink ^= w;
     bytes += n;
     calls++;
+    if (echo && !c.writeNonblock(d, n)) echo_refused++;
     return 0;
   }
   template <class C>
@@ -243,15 +264,17 @@ struct TimedOracleBackend : OracleBackend {
   }
 };
 
-template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false>
+template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false, bool kEcho = false>
 struct Conf {
   static const uint32_t RecvBufSize = 65536;
   static const uint32_t MaxConns = 1024;
   static const uint32_t SendTimeoutSec = 0;
   static const uint32_t RecvTimeoutSec = 0;
-  static const uint32_t ConnSendBufCnt = 16; // the server sends no data
+  // echo: every 1,460-B delivery goes back as two segments (SMSS 956 with 1-KiB send buffers), acknowledged a
+  // poll or two later; otherwise the server sends no data
+  static const uint32_t ConnSendBufCnt = kEcho ? 64 : 16;
   static const uint32_t RxBatch = kBatch;
-  static const uint32_t TxBatch = kBatch;
+  static const uint32_t TxBatch = kEcho ? 4 * kBatch : kBatch;
   static const uint32_t RxChunk = kChunk;
   static const bool RxPipeline = kPipe;
   static const bool RxResident = kResident;
@@ -261,16 +284,18 @@ struct Conf {
 struct Run {
   double mfps = 0, us_poll = 0, acks_per_frame = 0, fill_share = 0, classify_share = 0, tx_share = 0;
   double ns_classify = -1, ns_dispatch = -1; // TimedOracleBackend: per frame, in launch() / collect()
+  double echo_gbps = -1;                      // echo workload: payload bits the server sent back per second
   bool ok = false;
   std::string err;
 };
 
 // verify = false: the checksum discard off, as the reference's release build runs (no checksum verified);
 // the GPU backend then classifies from each frame's header lines only (pn_set_verify)
-template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false>
+template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false,
+          bool kEcho = false>
 static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   Run out;
-  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident>, BenchLink, Backend>;
+  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident, kEcho>, BenchLink, Backend>;
   auto srv = std::make_unique<Server>();
   srv->link().setup(n_flows);
   if (!srv->initWithLink("10.0.0.1", 1234)) {
@@ -280,6 +305,7 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   srv->setDropBadChecksum(verify);
   Handler h;
   BenchLink& link = srv->link();
+  h.echo = link.echo = kEcho;
   link.phase = BenchLink::Syn;
   srv->poll(h);
   // (pipelined: frames are dispatched one poll later and the replies sent one poll after that)
@@ -294,15 +320,16 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   link.phase = BenchLink::Data;
   const uint32_t warm = 8;
   for (uint32_t p = 0; p < warm; p++) srv->poll(h);
-  const uint64_t bytes0 = h.bytes, acks0 = link.acks;
+  const uint64_t bytes0 = h.bytes, acks0 = link.acks, echo0 = link.echo_bytes;
   link.fill_s = 0;
   const auto t0 = Clock::now();
   for (uint32_t p = 0; p < polls; p++) srv->poll(h);
   const double t = secs(t0, Clock::now());
   const uint64_t timed_bytes = h.bytes - bytes0;
+  if (kEcho) out.echo_gbps = (link.echo_bytes - echo0) * 8.0 / t / 1e9;
   link.phase = BenchLink::Idle;
-  srv->poll(h); // pipelined: the last batch is still in flight
-  srv->poll(h);
+  // pipelined: the last batch is still in flight (echo: its replies leave a poll after their dispatch)
+  for (int k = 0; k < (kEcho ? 6 : 2); k++) srv->poll(h);
   const uint64_t frames = (uint64_t)polls * (kBatch / n_flows) * n_flows;
   out.mfps = frames / t / 1e6;
   out.us_poll = t * 1e6 / polls;
@@ -327,12 +354,16 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
     out.ns_dispatch = be.collected ? be.collect_s * 1e9 / be.collected : 0;
   }
   out.ok = timed_bytes == frames * kPayload && h.bytes == (uint64_t)link.poll_no * (kBatch / n_flows) * n_flows * kPayload &&
-           !link.rsts && !link.other && !h.disconnected && srv->getLastError() == nullptr;
+           !link.rsts && !link.other && !h.disconnected && srv->getLastError() == nullptr &&
+           (!kEcho || (link.echo_bytes == h.bytes && !h.echo_refused));
   if (!out.ok)
     out.err = srv->getLastError() ? srv->getLastError()
                                   : "delivered " + std::to_string(timed_bytes) + " of " + std::to_string(frames * kPayload) +
                                         " B, " + std::to_string(link.rsts) + " RSTs, " + std::to_string(link.other) +
-                                        " other frames (flags " + std::to_string(link.other_flags) + "), " + std::to_string(h.disconnected) + " disconnects";
+                                        " other frames (flags " + std::to_string(link.other_flags) + "), " + std::to_string(h.disconnected) + " disconnects" +
+                                        (kEcho ? ", echoed " + std::to_string(link.echo_bytes) + " of " + std::to_string(h.bytes) +
+                                                     " B, " + std::to_string(h.echo_refused) + " refused writes"
+                                               : std::string());
   return out;
 }
 
@@ -350,7 +381,7 @@ struct RefBenchConf {
 // The reference's own server on the same workload, one core: each poll takes at most 64 frames (Core.h:496-498),
 // so the same frames as `polls` polls of 512 take 8x the polls.  Built without EFVITCP_DEBUG, as pollnet ships it:
 // no checksum is verified (the release path).
-static Run runRef(uint32_t n_flows, uint32_t polls) {
+static Run runRef(uint32_t n_flows, uint32_t polls, bool echo = false) {
   Run out;
   using Srv = efvitcp::EfviTcpServer<RefBenchConf>;
   auto link = std::make_unique<BenchLink>();
@@ -372,6 +403,7 @@ static Run runRef(uint32_t n_flows, uint32_t polls) {
     return out;
   }
   Handler h;
+  h.echo = link->echo = echo;
   link->phase = BenchLink::Syn;
   for (int k = 0; k < 64 && link->synacks < n_flows; k++) srv->poll(h);
   link->phase = BenchLink::Ack;
@@ -383,18 +415,20 @@ static Run runRef(uint32_t n_flows, uint32_t polls) {
   link->phase = BenchLink::Data;
   const uint32_t ref_polls = polls * 8, warm = 64;
   for (uint32_t p = 0; p < warm; p++) srv->poll(h);
-  const uint64_t bytes0 = h.bytes, acks0 = link->acks, frames0 = link->data_frames;
+  const uint64_t bytes0 = h.bytes, acks0 = link->acks, frames0 = link->data_frames, echo0 = link->echo_bytes;
   link->fill_s = 0;
   const auto t0 = Clock::now();
   for (uint32_t p = 0; p < ref_polls; p++) srv->poll(h);
   const double t = secs(t0, Clock::now());
   const uint64_t frames = link->data_frames - frames0;
+  if (echo) out.echo_gbps = (link->echo_bytes - echo0) * 8.0 / t / 1e9;
   out.mfps = frames / t / 1e6;
   out.us_poll = t * 1e6 / ref_polls;
   out.acks_per_frame = (double)(link->acks - acks0) / frames;
   out.fill_share = link->fill_s / t;
   out.ok = frames == (uint64_t)ref_polls * 64 && h.bytes - bytes0 == frames * kPayload &&
-           h.bytes == link->data_frames * kPayload && !link->rsts && !link->other && !h.disconnected;
+           h.bytes == link->data_frames * kPayload && !link->rsts && !link->other && !h.disconnected &&
+           (!echo || (link->echo_bytes == h.bytes && !h.echo_refused));
   if (!out.ok)
     out.err = "reference: delivered " + std::to_string(h.bytes - bytes0) + " B of " + std::to_string(frames) + " frames, " +
               std::to_string(link->rsts) + " RSTs, " + std::to_string(link->other) + " other frames, " +
@@ -415,6 +449,13 @@ static std::string json(const Run& r) {
                 "\"tx_fill_share\": %.3f}",
                 r.mfps, r.mfps * 1514 * 8 / 1e3, r.us_poll, r.acks_per_frame, r.fill_share,
                 r.fill_share < 1 ? r.mfps / (1 - r.fill_share) : 0.0, r.classify_share, r.tx_share);
+  if (r.echo_gbps >= 0) {
+    std::string o(b);
+    o.pop_back();
+    char x[96];
+    std::snprintf(x, sizeof x, ", \"echo_payload_gbit_per_s\": %.2f}", r.echo_gbps);
+    return o + x;
+  }
   if (r.ns_dispatch >= 0) {
     std::string o(b);
     o.pop_back();
@@ -440,7 +481,17 @@ int main(int argc, char** argv) {
     ok = ok && r.ok;
   };
   const bool cpu_only = argc > 3 && std::strcmp(argv[3], "cpu") == 0;
-  if (argc > 3 && std::strcmp(argv[3], "twin_timed") == 0) { // the host dispatch alone (profiling)
+  if (argc > 3 && std::strcmp(argv[3], "echo") == 0) {
+    // the reference example's server (example/tcpserver.cc): every delivery written back, the peers acknowledging
+    // it; TX batches of data frames take pn_tx_fill (GPU) / the oracle's fill (twin) / copyAndSum (reference)
+    leg("gpu_echo_512_release_path", runOne<512, GpuBackend, 0, false, false, true>(n_flows, polls, false));
+    leg("gpu_echo_512_pipelined_release_path", runOne<512, GpuBackend, 0, true, false, true>(n_flows, polls, false));
+    leg("gpu_echo_512_pipelined_resident_release_path", runOne<512, GpuBackend, 0, true, true, true>(n_flows, polls, false));
+    leg("cpu_echo_512_release_path", runOne<512, OracleBackend, 0, false, false, true>(n_flows, polls, false));
+#ifdef PN_BENCH_REF
+    leg("reference_server_echo_release_build", runRef(n_flows, polls, true));
+#endif
+  } else if (argc > 3 && std::strcmp(argv[3], "twin_timed") == 0) { // the host dispatch alone (profiling)
     leg("cpu_rxbatch_512_pipelined_release_path_timed", runOne<512, TimedOracleBackend, 0, true>(n_flows, polls, false));
   } else if (argc > 3 && std::strcmp(argv[3], "release_pair") == 0) { // one pair on its own (profiling the host side)
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
@@ -483,7 +534,7 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
   }
   if (argc <= 3 || (std::strcmp(argv[3], "quick") != 0 && std::strcmp(argv[3], "release_pair") != 0 &&
-                    std::strcmp(argv[3], "twin_timed") != 0)) {
+                    std::strcmp(argv[3], "twin_timed") != 0 && std::strcmp(argv[3], "echo") != 0)) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
     leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));
