@@ -608,6 +608,11 @@ class TcpEngine {
     TcpEngine* eng_ = nullptr;
     uint32_t id_ = 0;
     uint64_t key_ = 0;
+    // every frame of this connection starts from these 54 bytes (Ethernet, IPv4 and TCP headers with the
+    // connection's addresses and ports, the rest zero), as the reference's SendBufs are pre-filled (Core.h:291-301);
+    // hdr_ip_sum_ / hdr_tcp_sum_: their fixed words summed (TcpEngine::connHeader)
+    alignas(64) uint8_t hdr_[64] = {};
+    uint32_t hdr_ip_sum_ = 0, hdr_tcp_sum_ = 0;
     uint32_t peer_ip_ = 0;     // network order
     uint16_t peer_port_ = 0;   // network order
     uint16_t local_port_ = 0;  // network order
@@ -953,6 +958,29 @@ class TcpEngine {
     // genISN (TcpConn.h:856-858): connHashKey(peer) + now_ts; keeps send window 0 until established
     c.send_wnd_seq_ = (uint32_t)key + wheel_.now();
     c.seg(0).seq = c.send_wnd_seq_;
+    buildConnHeader(c);
+  }
+  // The connection's frame template and its fixed words' sums (native-order 16-bit words, as header_sums).
+  void buildConnHeader(Conn& c) {
+    using namespace srv_detail;
+    uint8_t* f = c.hdr_;
+    std::memset(f, 0, sizeof c.hdr_);
+    std::memcpy(f, c.peer_mac_, 6);
+    std::memcpy(f + 6, local_mac_, 6);
+    f[12] = 0x08;
+    uint8_t* ip = f + 14;
+    ip[0] = 0x45;
+    wr16(ip + 6, 0x4000);
+    ip[8] = 64;
+    ip[9] = 6;
+    std::memcpy(ip + 12, &local_ip_, 4);
+    std::memcpy(ip + 16, &c.peer_ip_, 4);
+    std::memcpy(ip + 20, &c.local_port_, 2);
+    std::memcpy(ip + 22, &c.peer_port_, 2);
+    auto halves = [](uint32_t x) { return (x & 0xffffu) + (x >> 16); };
+    const uint32_t addr = halves(local_ip_) + halves(c.peer_ip_);
+    c.hdr_ip_sum_ = 0x0045u + 0x0040u + 0x0640u + addr;
+    c.hdr_tcp_sum_ = addr + 0x0600u + c.local_port_ + c.peer_port_;
   }
   void onSyn(Conn& c, const uint8_t* eth, const pn_result& r) { // TcpConn.h:339-375
     const uint8_t* opt = eth + 54;
@@ -1320,6 +1348,32 @@ class TcpEngine {
       tx_fill_[tx_cur_].push_back(tx_n_ - 1);
     }
   }
+  // header() for a frame of connection c, from its template: the fields that vary written over it, and (header only)
+  // both checksums from the template's fixed sums plus those fields.  The same bytes as header().
+  void connHeader(const Conn& c, uint8_t* f, uint32_t seq, uint32_t ack, uint8_t doff_words, uint8_t flags,
+                  uint16_t window, uint32_t tcp_len) {
+    using namespace srv_detail;
+    std::memcpy(f, c.hdr_, sizeof c.hdr_);
+    uint8_t* ip = f + 14;
+    uint8_t* tcp = ip + 20;
+    wr16(ip + 2, (uint16_t)(20 + tcp_len));
+    wr32(tcp + 4, seq);
+    wr32(tcp + 8, ack);
+    tcp[12] = (uint8_t)(doff_words << 4);
+    tcp[13] = flags;
+    wr16(tcp + 14, window);
+    if (doff_words == 5 && tcp_len == 20) {
+      auto halves = [](uint32_t x) -> uint64_t { return (x & 0xffffu) + (x >> 16); };
+      const uint16_t ip_sum = csum_fold(c.hdr_ip_sum_ + 0x2800u);
+      const uint16_t tcp_sum = csum_fold(c.hdr_tcp_sum_ + 0x1400u + halves(__builtin_bswap32(seq)) +
+                                         halves(__builtin_bswap32(ack)) + (0x50u | (uint32_t)flags << 8) +
+                                         __builtin_bswap16(window));
+      std::memcpy(ip + 10, &ip_sum, 2);
+      std::memcpy(tcp + 16, &tcp_sum, 2);
+    } else {
+      tx_fill_[tx_cur_].push_back(tx_n_ - 1);
+    }
+  }
   // A segment of connection c (TcpConn::sendBuf, TcpConn.h:310-323): ack = what was received
   // so far (updateLastAck, TcpConn.h:838-843), window = free receive buffer.
   void emit(Conn& c, uint32_t seq, Kind k, const uint8_t* payload, uint32_t len) {
@@ -1329,26 +1383,24 @@ class TcpEngine {
     const uint16_t win = (uint16_t)std::min<uint32_t>(65535u, c.rx_.window());
     uint8_t* f = txFrame();
     enum : uint8_t { FIN = 1, SYN = 2, RST = 4, PSH = 8, ACK = 16 };
-    const uint16_t sp = c.local_port_, dp = c.peer_port_;
     switch (k) {
       case kSyn:
       case kSynAck: // MSS option (TcpConn.h:207-214)
-        header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 6, (uint8_t)(SYN | (k == kSynAck ? ACK : 0)), win, 24);
+        connHeader(c, f, seq, ack, 6, (uint8_t)(SYN | (k == kSynAck ? ACK : 0)), win, 24);
         f[54] = 2;
         f[55] = 4;
         srv_detail::wr16(f + 56, (uint16_t)PN_RECV_MSS);
         break;
       case kData:
       case kFinAck:
-        header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, (uint8_t)(PSH | ACK | (k == kFinAck ? FIN : 0)), win,
-               20 + len);
+        connHeader(c, f, seq, ack, 5, (uint8_t)(PSH | ACK | (k == kFinAck ? FIN : 0)), win, 20 + len);
         if (len) {
           std::memcpy(f + 54, payload, len);
           ++tx_data_n_;
         }
         break;
-      case kAck: header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, PSH | ACK, win, 20); break;
-      case kRstAck: header(f, c.peer_mac_, c.peer_ip_, sp, dp, seq, ack, 5, RST | PSH | ACK, win, 20); break;
+      case kAck: connHeader(c, f, seq, ack, 5, PSH | ACK, win, 20); break;
+      case kRstAck: connHeader(c, f, seq, ack, 5, RST | PSH | ACK, win, 20); break;
     }
   }
   // Core::rspRst (Core.h:400-423): answer a segment nobody owns.  RSTs and TIME_WAIT ACKs
