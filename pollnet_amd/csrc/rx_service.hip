@@ -4,7 +4,7 @@
 // answering a doorbell ≈2.7 µs (bench/bench_doorbell, profiles/r05/latency/).
 //
 // Protocol.  Two mailbox slots of one 64-B line each (pinned host memory; post k uses slot k & 1).  The host
-// fills a slot's fields, its first word (gen) and last word (seq) = k, seq last with a release store.  Wave 0 of
+// fills a slot's fields, then its first word (gen) and last word (seq) = k with release stores.  Wave 0 of
 // the kernel polls only the slot of the next post (one 64-B read per poll: 16 lanes x 4 B), accepts it when gen
 // and seq both read k, and publishes (waves << 32) | k in a device word: a post runs on one wave per group of
 // frames (at most all of them; svc_fpw sizes the groups).  A one-wave post wave 0 classifies alone; for a larger
@@ -25,7 +25,7 @@ using pn_internal::hip_err;
 using pn_internal::set_err;
 
 struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its device copy
-  uint32_t gen;              // = seq, stored first
+  uint32_t gen;              // = seq, stored after the fields
   uint32_t n;                // frames, or PN_SERVICE_STOP
   uint32_t verify;           // pn_set_verify's setting at the post
   uint32_t max_conn;
@@ -34,8 +34,8 @@ struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its devi
   const pn_conn_entry* tbl;
   uint64_t mask;
   uint32_t n_entries;
-  uint32_t fpw; // frames per group (svc_fpw)
-  uint32_t pad;
+  uint32_t fpw;   // frames per group (svc_fpw)
+  uint32_t check; // svc_check: k ^ the xor of words 1-13, so a read that mixed two posts' words is refused
   uint32_t seq; // stored last (release)
 };
 static_assert(sizeof(SvcPost) == 64, "one line per post");
@@ -73,6 +73,14 @@ inline uint32_t svc_fpw(uint32_t n, uint32_t waves, bool verify) {
   uint32_t fpw = verify ? 8u : kFramesPerWave;
   while (fpw < kFramesPerWave && (n + fpw - 1) / fpw > waves) fpw <<= 1;
   return fpw;
+}
+
+// The slot's check word for post k over its words 1-13 (n .. fpw).
+inline uint32_t svc_check(const SvcPost* p, uint32_t k) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+  uint32_t x = k;
+  for (int i = 1; i <= 13; i++) x ^= w[i];
+  return x;
 }
 
 // the waves a post runs on: one per group, at most all (the host computes the same)
@@ -143,7 +151,11 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       // the next post's slot, one 64-B read: lane i holds word i
       const uint32_t* slot = reinterpret_cast<const uint32_t*>(s.mail + (want & 1));
       const uint32_t v = lane < 16 ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-      if (__builtin_amdgcn_readlane(v, 0) != want || __builtin_amdgcn_readlane(v, 15) != want) {
+      uint32_t x = want; // the check word over words 1-13 (svc_check)
+#pragma unroll
+      for (int i = 1; i <= 13; i++) x ^= (uint32_t)__builtin_amdgcn_readlane(v, i);
+      if (__builtin_amdgcn_readlane(v, 0) != want || __builtin_amdgcn_readlane(v, 15) != want ||
+          (uint32_t)__builtin_amdgcn_readlane(v, 14) != x) {
         if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
           if (lane == 0) {
             __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -353,8 +365,9 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   }
   const uint32_t k = v->seq + 1;
   SvcPost* p = v->mail + (k & 1);
-  __atomic_store_n(&p->seq, 0u, __ATOMIC_RELAXED); // a half-written slot never reads as post k
-  __atomic_store_n(&p->gen, k, __ATOMIC_RELAXED);
+  // the fields and their check word first, then gen and seq = k, each a release store: the slot still holds post
+  // k - 2 (done), so until gen and seq both read k it is not post k; and should the line's read be split into pieces
+  // read at different times, a mix of two posts' fields fails the check and the kernel reads the slot again
   p->n = n;
   p->verify = ctx->verify_tcp ? 1u : 0u;
   p->max_conn = ctx->max_conn;
@@ -365,6 +378,8 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   p->n_entries = ctx->n_entries;
   p->fpw = svc_fpw(n, v->waves, p->verify != 0);
   v->post_act[k & 1] = svc_active(n, p->fpw, v->waves);
+  p->check = svc_check(p, k);
+  __atomic_store_n(&p->gen, k, __ATOMIC_RELEASE);
   __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
   v->seq = k;
   if (post_id) *post_id = k;
@@ -409,10 +424,10 @@ int pn_service_close(pn_service* v) {
     if (!svc_post_done(v, v->seq)) rc = pn_service_wait(v, 0);
     const uint32_t k = v->seq + 1;
     SvcPost* p = v->mail + (k & 1);
-    __atomic_store_n(&p->seq, 0u, __ATOMIC_RELAXED);
-    __atomic_store_n(&p->gen, k, __ATOMIC_RELAXED);
     p->n = PN_SERVICE_STOP;
     v->post_act[k & 1] = 0;
+    p->check = svc_check(p, k);
+    __atomic_store_n(&p->gen, k, __ATOMIC_RELEASE);
     __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
     v->seq = k;
   }
