@@ -180,7 +180,7 @@ class RxConn {
           // exactly the next bytes and nothing pending: hand over the frame's own bytes
           const uint32_t left = h.onData(*this, data, (uint32_t)n);
           segs_[0].first = segs_[0].second - left;
-          std::memcpy(recv_buf_ + segs_[0].first, data + n - left, left);
+          if (left) std::memcpy(recv_buf_ + segs_[0].first, data + n - left, left); // the common case keeps nothing
         } else {
           std::memcpy(recv_buf_ + loc, data, (uint32_t)n);
           if (i == 0) {
