@@ -439,9 +439,13 @@ static Run runRef(uint32_t n_flows, uint32_t polls, bool echo = false) {
 
 static std::string json(const Run& r) {
   char b[448];
-  if (!r.err.empty() && !r.ok) {
-    std::snprintf(b, sizeof b, "{\"error\": \"%s\"}", r.err.c_str());
-    return b;
+  if (!r.err.empty() && !r.ok) { // the message whole, quotes and backslashes escaped (it may quote a frame or a path)
+    std::string e = "{\"error\": \"";
+    for (const char ch : r.err) {
+      if (ch == '"' || ch == '\\') e += '\\';
+      e += (ch >= 0x20 ? ch : ' ');
+    }
+    return e + "\"}";
   }
   std::snprintf(b, sizeof b,
                 "{\"mframes_per_s\": %.3f, \"gbit_per_s\": %.1f, \"us_per_poll\": %.1f, \"acks_per_frame\": %.3f, "
