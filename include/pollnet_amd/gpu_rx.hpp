@@ -36,6 +36,15 @@ inline uint64_t conn_hash_key(uint32_t ip_be, uint16_t port_be) {
   return (ip << 15) | (p & 0x7fff) | ((p & 0x8000) << 32);
 }
 
+// The key of a frame's remote end: its IP source address and TCP source port (ip_hdr + 12, tcp_hdr = ip + 20).
+inline uint64_t frame_key(const uint8_t* eth) {
+  uint32_t ip_be;
+  uint16_t port_be;
+  std::memcpy(&ip_be, eth + 14 + 12, 4);
+  std::memcpy(&port_be, eth + 14 + 20, 2);
+  return conn_hash_key(ip_be, port_be);
+}
+
 // A record's checksum verdicts: both OK, or the IP one OK where the TCP sum was not computed (the release
 // path, pn_set_verify(ctx, 0): PN_F_TCP_UNCHECKED).
 inline bool checksums_ok(uint16_t flags) {
@@ -164,12 +173,13 @@ class GpuRx {
   // dispatched on the host.
   // recv_handler(uint64_t key, const pn_result& rec, const uint8_t* eth, uint32_t miss_entry_idx)
   // tw_handler(uint64_t key, uint32_t tw_id, const uint8_t* eth, const pn_result& rec)
-  template <class RecvHandler, class TwHandler>
+  // kHitKey = false: a hit's key is not computed (0 is passed; the caller derives it from eth if it needs it)
+  template <bool kHitKey = true, class RecvHandler, class TwHandler>
   const char* pollBatch(const uint8_t* host_slots, uint32_t n, const ConnTable& table, RecvHandler&& recv_handler,
                         TwHandler&& tw_handler) {
     if (mode_ == Mode::ZeroCopy)
       if (const char* e = check_pinned(host_slots)) return e;
-    return run(
+    return run<kHitKey>(
         n, table, [&](uint32_t k) { return launch(host_slots, n, k); },
         [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; }, recv_handler, tw_handler);
   }
@@ -211,7 +221,7 @@ class GpuRx {
     if (e) drain();
     return e;
   }
-  template <class RecvHandler, class TwHandler>
+  template <bool kHitKey = true, class RecvHandler, class TwHandler>
   const char* complete(const uint8_t* host_slots, uint32_t n, uint32_t b, const ConnTable& table,
                        RecvHandler&& recv_handler, TwHandler&& tw_handler) {
     if (n > cap_ || b > 1) return "complete: n > max_batch or buffer > 1";
@@ -220,7 +230,7 @@ class GpuRx {
       return e;
     }
     auto eth_of = [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; };
-    walk(h_res_[b], 0, n, table, eth_of, recv_handler, tw_handler);
+    walk<kHitKey>(h_res_[b], 0, n, table, eth_of, recv_handler, tw_handler);
     return nullptr;
   }
 
@@ -241,14 +251,14 @@ class GpuRx {
   // chunk k is dispatched; eth_of(i) = frame i's Ethernet header in host memory.
   // An error leaves no chunk in flight: the stream is drained before returning, so the
   // next call may reuse the pinned buffers at once.
-  template <class Launch, class EthOf, class RecvHandler, class TwHandler>
+  template <bool kHitKey = true, class Launch, class EthOf, class RecvHandler, class TwHandler>
   const char* run(uint32_t n, const ConnTable& table, Launch&& launch_k, EthOf&& eth_of, RecvHandler& recv_handler,
                   TwHandler& tw_handler) {
-    const char* e = run_chunks(n, table, launch_k, eth_of, recv_handler, tw_handler);
+    const char* e = run_chunks<kHitKey>(n, table, launch_k, eth_of, recv_handler, tw_handler);
     if (e) drain();
     return e;
   }
-  template <class Launch, class EthOf, class RecvHandler, class TwHandler>
+  template <bool kHitKey, class Launch, class EthOf, class RecvHandler, class TwHandler>
   const char* run_chunks(uint32_t n, const ConnTable& table, Launch& launch_k, EthOf& eth_of, RecvHandler& recv_handler,
                          TwHandler& tw_handler) {
     if (n == 0) return nullptr;
@@ -259,22 +269,18 @@ class GpuRx {
         if (const char* e = launch_k(k + 1)) return e;
       if (const char* e = wait_done(k & 1)) return e;
       const uint32_t base = k * cap_, m = std::min(cap_, n - base);
-      walk(h_res_[k & 1], base, m, table, eth_of, recv_handler, tw_handler);
+      walk<kHitKey>(h_res_[k & 1], base, m, table, eth_of, recv_handler, tw_handler);
     }
     return nullptr;
   }
   // Dispatch records res[0, m) of frames base.. in order.
-  template <class EthOf, class RecvHandler, class TwHandler>
+  template <bool kHitKey, class EthOf, class RecvHandler, class TwHandler>
   void walk(const pn_result* res, uint32_t base, uint32_t m, const ConnTable& table, EthOf& eth_of,
             RecvHandler& recv_handler, TwHandler& tw_handler) {
     for (uint32_t i = 0; i < m; i++) {
       const uint8_t* eth = eth_of(base + i);
       const pn_result& r = res[i];
-      uint32_t ip_be;
-      uint16_t port_be;
-      std::memcpy(&ip_be, eth + 14 + 12, 4);  // ip_hdr->src_ip
-      std::memcpy(&port_be, eth + 14 + 20, 2); // tcp_hdr->src_port (tcp = ip + 20)
-      const uint64_t key = conn_hash_key(ip_be, port_be);
+      const uint64_t key = (kHitKey || (r.flags & (PN_F_HIT | PN_F_TW)) != PN_F_HIT) ? frame_key(eth) : 0;
       if (r.flags & PN_F_TW) {
         tw_handler(key, r.conn_id - max_conn_, eth, r);
       } else {

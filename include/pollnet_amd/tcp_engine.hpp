@@ -407,7 +407,7 @@ class GpuBackend {
   const char* launch(uint32_t half, uint32_t n, const ConnTable&) { return rx_.submit(rxSlots(half), n, half); }
   template <class F>
   const char* collect(uint32_t half, uint32_t n, const ConnTable& t, F&& f) {
-    return rx_.complete(
+    return rx_.template complete<false>(
         rxSlots(half), n, half, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
         [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
   }
@@ -416,7 +416,7 @@ class GpuBackend {
   // f(key, rec, eth) for the n frames of the RX ring, in ring order.
   template <class F>
   const char* classify(uint32_t n, const ConnTable& t, F&& f) {
-    return rx_.pollBatch(
+    return rx_.template pollBatch<false>(
         rx_ring_, n, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
         [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
   }
@@ -884,6 +884,8 @@ class TcpEngine {
   }
 
   // ---- one received frame (Core::pollNet RX branch + the endpoint's recv handler) ----
+  // key: the frame's connHashKey, which the backends pass for TIME_WAIT records and misses only (a hit's connection
+  // is its conn_id; the key is derived from the frame here where a hit needs it)
   template <class HH>
   void onFrame(HH& h, uint64_t key, const pn_result& rec, const uint8_t* eth) {
     if (rec.flags & (PN_F_NOT_TCP | PN_F_TRUNC | PN_F_BADOFF)) return;
@@ -894,6 +896,7 @@ class TcpEngine {
     // pipelined, after the launch): probe the live table
     if ((Backend::kSnapshot || kRxPipeline) && tver_ != disp_ver_) {
       ++re_resolved_;
+      key = frame_key(eth);
       uint32_t conn_id = PN_MISS;
       const bool hit = table_.find(key, nullptr, &conn_id);
       r.conn_id = conn_id;

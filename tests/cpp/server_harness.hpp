@@ -98,9 +98,10 @@ struct OracleBackend {
   }
   template <class F>
   const char* collect(uint32_t half, uint32_t n, const pollnet_amd::ConnTable&, F&& f) {
-    for (uint32_t i = 0; i < n; i++) {
+    for (uint32_t i = 0; i < n; i++) { // as GpuBackend: a hit's key is not computed (the engine derives it)
       const uint8_t* eth = rxSlots(half) + (size_t)i * kStride + kFrameOff;
-      f(keyOf(eth), recs[half][i], eth);
+      const pn_result& r = recs[half][i];
+      f((r.flags & (PN_F_HIT | PN_F_TW)) == PN_F_HIT ? 0 : keyOf(eth), r, eth);
     }
     return nullptr;
   }
