@@ -146,15 +146,18 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   uint32_t last = s.last;
   uint64_t t0 = wall_clock64();
   for (;;) {
+    uint32_t v = 0;         // the post's 64-B line, lane i holding word i (lanes 0-15)
+    uint32_t k = 0, act = 0; // the post and its wave count
+    bool run = false;       // this wave classifies groups of post k
     if (w == 0) {
-      const uint32_t want = last + 1;
-      // the next post's slot, one 64-B read: lane i holds word i
-      const uint32_t* slot = reinterpret_cast<const uint32_t*>(s.mail + (want & 1));
-      const uint32_t v = lane < 16 ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-      uint32_t x = want; // the check word over words 1-13 (svc_check)
+      k = last + 1;
+      // the next post's slot, one 64-B read
+      const uint32_t* slot = reinterpret_cast<const uint32_t*>(s.mail + (k & 1));
+      v = lane < 16 ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+      uint32_t x = k; // the check word over words 1-13 (svc_check)
 #pragma unroll
       for (int i = 1; i <= 13; i++) x ^= (uint32_t)__builtin_amdgcn_readlane(v, i);
-      if (__builtin_amdgcn_readlane(v, 0) != want || __builtin_amdgcn_readlane(v, 15) != want ||
+      if (__builtin_amdgcn_readlane(v, 0) != k || __builtin_amdgcn_readlane(v, 15) != k ||
           (uint32_t)__builtin_amdgcn_readlane(v, 14) != x) {
         if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
           if (lane == 0) {
@@ -169,24 +172,44 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
       const uint32_t n = __builtin_amdgcn_readlane(v, 1);
       if (n == PN_SERVICE_STOP) {
-        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)kSvcStop << 32) | want, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)kSvcStop << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      const KArgs a = svc_args(v, s);
-      const uint32_t act = svc_active(n, a.fpw, W);
-      const bool verify = __builtin_amdgcn_readlane(v, 2) != 0;
-      if (act == 1) { // one wave's work: classify, then let the others see it go by
-        svc_run<MIS, COOP>(a, verify, 0, 1, want, s.done_words, lane);
-        if (lane == 0) __hip_atomic_store(&s.dev->cur, (1ull << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[want & 1])[lane] = v;
+      act = svc_active(n, __builtin_amdgcn_readlane(v, 13), W);
+      if (act > 1) { // the post's other waves read it from the device copy
+        if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[k & 1])[lane] = v;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)act << 32) | want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        svc_run<MIS, COOP>(a, verify, 0, act, want, s.done_words, lane);
-        svc_count(s.dev, act, want, lane);
-        // the next post only once every wave of this one is done (its device copy may then be reused)
+        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)act << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      run = true;
+    } else {
+      const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      k = __builtin_amdgcn_readfirstlane((uint32_t)c);
+      act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
+      if (k == kSvcIdle || act == kSvcStop) return;
+      if (k == last) {
+        // the limit is wave 0's plus a margin (a safety net: wave 0 always publishes kSvcIdle first)
+        if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) return;
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
+      if (w < act) { // this wave runs on post k: wave 0 waits for it before the next post, so k is current
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[k & 1]);
+        v = lane < 16 ? cp[lane] : 0u;
+        run = true;
+      }
+    }
+    if (run) { // one call site for every wave (the classify code is inlined once per path)
+      svc_run<MIS, COOP>(svc_args(v, s), __builtin_amdgcn_readlane(v, 2) != 0, w, act, k, s.done_words + w, lane);
+      if (act > 1) svc_count(s.dev, act, k, lane);
+    }
+    if (w == 0) {
+      if (act == 1) { // one wave's work, done: let the others see it go by
+        if (lane == 0) __hip_atomic_store(&s.dev->cur, (1ull << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else { // the next post only once every wave of this one is done (its device copy may then be reused)
         while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
-               want) {
+               k) {
           if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) { // a wave that never finishes: give up
             if (lane == 0) __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             return;
@@ -195,27 +218,8 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
-      last = want;
-    } else {
-      const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t d = __builtin_amdgcn_readfirstlane((uint32_t)c), act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
-      if (d == kSvcIdle || act == kSvcStop) return;
-      if (d == last) {
-        // the limit is wave 0's plus a margin (a safety net: wave 0 always publishes kSvcIdle first)
-        if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) return;
-        __builtin_amdgcn_s_sleep(2);
-        continue;
-      }
-      if (w < act) { // this wave runs on post d: wave 0 waits for it before the next post, so d is current
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[d & 1]);
-        const uint32_t v = lane < 16 ? cp[lane] : 0u;
-        const KArgs a = svc_args(v, s);
-        svc_run<MIS, COOP>(a, __builtin_amdgcn_readlane(v, 2) != 0, w, act, d, s.done_words + w, lane);
-        svc_count(s.dev, act, d, lane);
-      }
-      last = d;
     }
+    last = k;
     t0 = wall_clock64();
   }
 }

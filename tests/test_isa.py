@@ -61,6 +61,21 @@ def test_no_waterfall_loops(src):
     assert not bad, f"{len(bad)} kernels with a divergent descriptor (waterfall loop), e.g. {bad[0]}"
 
 
+def test_service_kernel_waterfalls_only_its_record_store():
+    """The resident service kernel (rx_service.hip) inlines the classify of both paths beside its own loop state, and
+    at that SGPR pressure the compiler keeps the record store's block index in a VGPR: one waterfall loop per kernel,
+    around that store, one iteration (the value is uniform).  Taking the classify out of line removes it but costs
+    more: 64 frames 3.5-3.8 -> 4.8-5.2 us on the release path, 7.5-8.2 -> 9.7-10.5 verified
+    (profiles/r05/service/inline_vs_call_ab.txt).  Pinned here so that a second one shows up."""
+    ks = _kernels(_asm("rx_service.hip"))
+    assert len(ks) == 16
+    for k, body in ks.items():
+        at = [i for i, l in enumerate(body) if re.match(r"\s+v_cmp_eq_u64_e\d+ vcc, s\[", l)]
+        assert len(at) <= 1, (k, len(at))
+        for i in at:
+            assert any("buffer_store_dwordx4" in l for l in body[i:i + 14]), k
+
+
 def test_rx_window_loads_issued_together():
     ks = _kernels(_asm("rx_kernel.hip"))
     # the strided production kernels with the cooperative window (COOP = 1, IDX = 0)
