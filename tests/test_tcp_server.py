@@ -140,3 +140,22 @@ def test_server_bench_release_pair_cpu():
     if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "conn_efvitcpserver.inc")):
         ref = line["reference_server_release_build"]
         assert ref["mframes_per_s"] > 0 and ref["acks_per_frame"] == pytest.approx(0.5, abs=0.01)
+
+
+def test_server_bench_echo_cpu_legs():
+    """bench_tcp_server echo (the reference example's echo server: every delivery written back, the peers
+    acknowledging it): the sequential twin and the reference's own server echo every byte they receive (no
+    refused write, no RST); the GPU legs need a GPU and are skipped here (they report an error without one)."""
+    import json
+
+    if not os.path.exists(SRVBENCH):
+        subprocess.run(["make", "-C", ROOT, "bench/bench_tcp_server"], check=True, capture_output=True)
+    p = subprocess.run([SRVBENCH, "256", "30", "echo"], capture_output=True, text=True, timeout=300)
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    twin = line["cpu_echo_512_release_path"]
+    assert "error" not in twin, twin
+    assert twin["echo_payload_gbit_per_s"] > 0
+    if os.path.exists(os.path.join(ROOT, "oracle", "_ref", "conn_efvitcpserver.inc")):
+        ref = line["reference_server_echo_release_build"]
+        assert "error" not in ref, ref
+        assert ref["echo_payload_gbit_per_s"] > 0
