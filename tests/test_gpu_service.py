@@ -175,7 +175,7 @@ def test_service_argument_checks(torch):
 
 def test_service_soak_random_posts_and_relaunches(torch):
     """1,500 posts of random size (1 .. 4,096 frames) at random offsets into one pinned ring, verified or release
-    path at random, one or two outstanding, with idle gaps longer than idle_ms (2 ms) between some of them so the
+    path at random (switched with posts in flight: each post carries the setting at its post), one or two outstanding, with idle gaps longer than idle_ms (2 ms) between some of them so the
     kernel ends and is relaunched many times, some posts landing while it ends.  Every post's records equal the
     oracle's, and every launch ended by itself or at close."""
     rng = np.random.default_rng(0x50A4)
@@ -203,10 +203,7 @@ def test_service_soak_random_posts_and_relaunches(torch):
                 if len(pending) == 2 or (pending and rng.random() < 0.5):
                     check(pending.pop(0))
                 verify = bool(rng.random() < 0.5)
-                if not pending:  # the verify setting is the ctx's at the post: change it only with nothing in flight
-                    ctx.set_verify(verify)
-                else:
-                    verify = pending[-1][4]
+                ctx.set_verify(verify)  # each post carries the setting at its post, posts in flight included
                 n = int(rng.integers(1, 4097))
                 first = int(rng.integers(0, N - n + 1))
                 o = k & 1
