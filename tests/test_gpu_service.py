@@ -221,3 +221,37 @@ def test_service_soak_random_posts_and_relaunches(torch):
             svc.close()
     finally:
         ctx.close()
+
+
+def test_service_table_change_with_a_post_in_flight(torch):
+    """pn_set_conn_table with one post outstanding (allowed: the table is double-buffered): the post in flight is
+    classified against the table it was posted with, the next post against the new one."""
+    p, s = _frames(3, 4096)
+    table = pa.gen_conn_table(p)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            host = _pinned(torch, s)
+            r = [torch.zeros(4096 * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            exp_old = _expected(s, 4096, table)
+            for _ in range(20):  # repeated, so some of the changes land while the first post is still running
+                old = svc.post(host, 4096, r[0])
+                key = int(pa.conn_hash_key(int(s[0, FRAME_OFF + 26:FRAME_OFF + 30].view("<u4")[0]),
+                                           int(s[0, FRAME_OFF + 34:FRAME_OFF + 36].view("<u2")[0])))
+                t2 = pa.gen_conn_table(p)
+                t2.delete(key)
+                ctx.set_conn_table(t2)
+                new = svc.post(host, 4096, r[1])
+                svc.wait(old)
+                svc.wait(new)
+                assert np.array_equal(r[0].numpy().view(pa.RESULT_DTYPE), exp_old)
+                exp_new = _expected(s, 4096, t2)
+                assert np.array_equal(r[1].numpy().view(pa.RESULT_DTYPE), exp_new)
+                assert not np.array_equal(exp_new, exp_old)
+                ctx.set_conn_table(table)
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
