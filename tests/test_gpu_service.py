@@ -255,3 +255,34 @@ def test_service_table_change_with_a_post_in_flight(torch):
             svc.close()
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_service_max_post_equals_pn_classify(torch, cfg):
+    """One post of PN_SERVICE_MAX_FRAMES (1 Mi) frames in device memory, both paths: its records equal pn_classify's
+    on the same frames (the bench's full-size parity is pinned to the oracle through pn_classify)."""
+    n = 1 << 20
+    p = pa.rx.GenParams.for_config(cfg)
+    host = np.empty((n, STRIDE), np.uint8)
+    pa.gen_frames(p, n, STRIDE, FRAME_OFF, first_index=0, threads=16, out=host)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(pa.gen_conn_table(p))
+        dev = torch.from_numpy(host.reshape(-1)).cuda()
+        del host
+        a = torch.empty(n * 16, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            for verify in (True, False):
+                ctx.set_verify(verify)
+                a.fill_(0x5A)
+                b.fill_(0xA5)
+                ctx.classify(dev, STRIDE, FRAME_OFF, n, a, torch.cuda.current_stream())
+                torch.cuda.synchronize()
+                svc.classify(dev, n, b)
+                assert torch.equal(a, b), verify
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
