@@ -46,6 +46,9 @@ struct RefCliConf { // pollnet's EfviTcpClient Conf
 struct ProdCliConf : RefCliConf {
   static const uint32_t RxBatch = 64; // the reference's 64 events per pollNet (Core.h:498)
 };
+struct ProdCliConfResident : ProdCliConf {
+  static const bool RxResident = true; // each poll's classify posted to the resident service (pn_service_*)
+};
 
 // The scripted server, as the client's link: fill() = the server's frames for this tick, send() = a client
 // frame (handled when the poll ends: a wire one poll long).
@@ -323,9 +326,9 @@ static Run runRef(uint64_t seed) {
   return r;
 }
 
-template <class Backend>
+template <class Backend, class Conf = ProdCliConf>
 static Run runProd(uint64_t seed, bool drop_bad = true) {
-  using Cli = GpuTcpClient<ProdCliConf, ScriptServer, Backend>;
+  using Cli = GpuTcpClient<Conf, ScriptServer, Backend>;
   auto cli = std::make_unique<Cli>();
   Run r;
   CliHandler<typename Cli::Conn>::pat = 0;
@@ -377,7 +380,7 @@ int main(int argc, char** argv) {
     for (size_t p = 0; (p = ref.log.find("connected n", p)) != std::string::npos; p++) connected++;
     for (size_t p = 0; (p = ref.log.find("connect failed", p)) != std::string::npos; p++) failed++;
     for (auto& f : ref.out) rsts += (f[47] & 4) != 0, data += f.size() > 54;
-    char what[64];
+    char what[96];
     std::snprintf(what, sizeof what, "script %u: twin vs reference", k);
     fail += compare(what, ref, runProd<OracleBackend>(seed));
     if (gpu) {
@@ -385,6 +388,10 @@ int main(int argc, char** argv) {
       fail += compare(what, ref, runProd<GpuBackend>(seed));
       std::snprintf(what, sizeof what, "script %u: GpuTcpClient (GPU, release path) vs reference", k);
       fail += compare(what, ref, runProd<GpuBackend>(seed, false));
+      std::snprintf(what, sizeof what, "script %u: GpuTcpClient (GPU, resident service) vs reference", k);
+      fail += compare(what, ref, runProd<GpuBackend, ProdCliConfResident>(seed));
+      std::snprintf(what, sizeof what, "script %u: GpuTcpClient (GPU, resident, release path) vs reference", k);
+      fail += compare(what, ref, runProd<GpuBackend, ProdCliConfResident>(seed, false));
     }
   }
   std::printf("exercised (reference side): %zu connections, %zu connect failures, %zu client RSTs, %zu data frames\n",

@@ -77,8 +77,12 @@ def test_client_twin_equals_reference_client():
 
 @pytest.mark.gpu
 def test_gpu_client_equals_reference_client():
+    """The same 8 scripts through GpuTcpClient on the GPU: per-poll classify, the release path, and the
+    classify posted to the resident service (Conf::RxResident) on both paths."""
     p = subprocess.run([_bin("test_ref_client"), "gpu", "8"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
     assert p.stdout.count("GpuTcpClient (GPU) vs reference") == 8 and "DIFFERENT" not in p.stdout, p.stdout
     assert p.stdout.count("GpuTcpClient (GPU, release path) vs reference") == 8, p.stdout
+    assert p.stdout.count("GpuTcpClient (GPU, resident service) vs reference") == 8, p.stdout
+    assert p.stdout.count("GpuTcpClient (GPU, resident, release path) vs reference") == 8, p.stdout
     assert p.stdout.rstrip().endswith("PASS"), p.stdout
