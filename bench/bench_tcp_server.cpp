@@ -11,7 +11,7 @@
 // bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
-//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|twin_timed|echo]   prints one JSON line; exit 0 = all data delivered
+//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|resident_pair|twin_timed|echo]   prints one JSON line; exit 0 = all data delivered
 //         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512 (also pipelined),
 //         GPU pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
 //         checksum summed) — bench.py's secondary.tcp_server_poll)
@@ -503,6 +503,11 @@ int main(int argc, char** argv) {
 #ifdef PN_BENCH_REF
     leg("reference_server_release_build", runRef(n_flows, polls));
 #endif
+  } else if (argc > 3 && std::strcmp(argv[3], "resident_pair") == 0) { // the drop-in's best leg beside the reference
+    leg("gpu_rxbatch_512_pipelined_resident_release_path", runOne<512, GpuBackend, 0, true, true>(n_flows, polls, false));
+#ifdef PN_BENCH_REF
+    leg("reference_server_release_build", runRef(n_flows, polls));
+#endif
   } else if (argc > 3 && std::strcmp(argv[3], "quick") == 0) { // bench.py's secondary leg
     leg("gpu_rxbatch_512", runOne<512, GpuBackend>(n_flows, polls));
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
@@ -538,6 +543,7 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
   }
   if (argc <= 3 || (std::strcmp(argv[3], "quick") != 0 && std::strcmp(argv[3], "release_pair") != 0 &&
+                    std::strcmp(argv[3], "resident_pair") != 0 &&
                     std::strcmp(argv[3], "twin_timed") != 0 && std::strcmp(argv[3], "echo") != 0)) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
