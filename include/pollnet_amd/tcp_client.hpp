@@ -150,7 +150,7 @@ class GpuTcpClient : public TcpEngine<Conf, ClientIConf<Conf>, Link, Backend, Gp
   }
   template <class HH>
   bool onHandshake(HH& h, Conn& c, const pn_result& r, const uint8_t* eth) { // SYN-SENT, TcpClient.h:86-98
-    const bool ack_ok = (r.flags & PN_F_ACK) && Base::ackNum(eth) == c.seg(c.send_next_).seq;
+    const bool ack_ok = (r.flags & PN_F_ACK) && Base::ackNum(eth) == c.next_seq_;
     if (!ack_ok) {
       this->rspRst(eth, r);
       return false;

@@ -554,7 +554,7 @@ class TcpEngine {
     // peer's window edge (TcpConn.h:189-192).
     uint32_t getImmediatelySendable() const {
       if (data_next_ != send_next_) return 0;
-      const int32_t wnd = (int32_t)(send_wnd_seq_ - segs_[send_next_ & (kSendBufCnt - 1)].seq - data_next_size_);
+      const int32_t wnd = (int32_t)(send_wnd_seq_ - next_seq_ - data_next_size_);
       return std::min((uint32_t)std::max(0, wnd), getSendable());
     }
     // TcpConn::sendv (TcpConn.h:63-70): the pieces appended in order, the last one pushed.
@@ -621,6 +621,7 @@ class TcpEngine {
     std::unique_ptr<Seg[]> segs_;
     std::unique_ptr<uint8_t[]> data_;
     uint32_t send_una_ = 0, send_next_ = 0, data_next_ = 0, data_next_size_ = 0, recover_ = 0;
+    uint32_t next_seq_ = 0; // seg(send_next_).seq, kept here so that an ACK reads no segment entry
     uint32_t smss_ = 536, send_wnd_seq_ = 0, rto_ = 1000, srtt_ = 0, rttvar_ = 0, dup_ack_cnt_ = 0, retries_ = 0;
     bool established_ = false, fin_sent_ = true, fin_received_ = true, fast_re_ = false, in_recover_ = false;
     TimerNode timers_[4]; // resend, delayed ACK, user 0 (send timeout), user 1 (recv timeout)
@@ -960,7 +961,7 @@ class TcpEngine {
     c.rx_.resetRecv();
     // genISN (TcpConn.h:856-858): connHashKey(peer) + now_ts; keeps send window 0 until established
     c.send_wnd_seq_ = (uint32_t)key + wheel_.now();
-    c.seg(0).seq = c.send_wnd_seq_;
+    c.seg(0).seq = c.next_seq_ = c.send_wnd_seq_;
     buildConnHeader(c);
   }
   // The connection's frame template and its fixed words' sums (native-order 16-bit words, as header_sums).
@@ -1132,7 +1133,7 @@ class TcpEngine {
     s.send_ts = wheel_.now();
     if (c.send_next_ == c.send_una_) wheel_.add(c.rto_, &c.timers_[0]);
     const uint32_t seq = s.seq;
-    c.seg(++c.send_next_).seq = seq + inc;
+    c.seg(++c.send_next_).seq = c.next_seq_ = seq + inc;
   }
   void advanceData(Conn& c) {
     c.data_next_++;
@@ -1191,7 +1192,7 @@ class TcpEngine {
   // case the reference would drop, a buffer still in the NIC's TX queue, does not exist here.
   void sendAck(Conn& c, bool immediate) {
     if (kDelayedAckMS == 0 || immediate) {
-      emit(c, c.seg(c.send_next_).seq, kAck, nullptr, 0);
+      emit(c, c.next_seq_, kAck, nullptr, 0);
       return;
     }
     if (c.timers_[1].unlinked()) wheel_.add(std::max(1u, kDelayedAckMS), &c.timers_[1]);
@@ -1216,7 +1217,7 @@ class TcpEngine {
   // TcpConn::close (TcpConn.h:92-102): RST if established, then release the entry.
   void closeConn(Conn& c) {
     if (c.isClosed()) return;
-    if (c.established_) emit(c, c.seg(c.send_next_).seq, kRstAck, nullptr, 0);
+    if (c.established_) emit(c, c.next_seq_, kRstAck, nullptr, 0);
     onClose(c, false);
   }
 
@@ -1247,7 +1248,7 @@ class TcpEngine {
     tw.peer_ip = c.peer_ip_;
     tw.peer_port = c.peer_port_;
     tw.local_port = c.local_port_;
-    tw.seq_num = c.seg(c.send_next_).seq;
+    tw.seq_num = c.next_seq_;
     tw.ack_num = c.rx_.ackSeq();
     wheel_.add(kTimeWaitTimeout, &tw.timer);
   }

@@ -134,7 +134,7 @@ class GpuTcpServer : public TcpEngine<Conf, ServerIConf<Conf>, Link, Backend, Gp
       return false;
     }
     if (!(r.flags & PN_F_ACK)) return false;
-    if (Base::ackNum(eth) != c.seg(c.send_next_).seq) {
+    if (Base::ackNum(eth) != c.next_seq_) {
       this->rspRst(eth, r);
       return false;
     }
