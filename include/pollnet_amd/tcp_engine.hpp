@@ -749,6 +749,8 @@ class TcpEngine {
     if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1,
                                  kRxPipeline ? 2 : 1, srv_detail::opt_RxResident<Conf>::value))
       return e;
+    tx_base_[0] = be_.txSlots(0) + Backend::kFrameOff; // each TX batch's first frame
+    tx_base_[1] = kRxPipeline ? be_.txSlots(1) + Backend::kFrameOff : tx_base_[0];
     free_conns_.clear();
     for (uint32_t i = kMaxConn; i-- > 0;) free_conns_.push_back(i); // Core.h:315: conns[i] = i
     free_tws_.clear();
@@ -795,14 +797,14 @@ class TcpEngine {
   // The link gets frames [0, n) of a TX batch, in order.
   void sendTx(uint32_t half, uint32_t n) {
     for (uint32_t i = 0; i < n; i++) {
-      const uint8_t* f = be_.txSlots(half) + (size_t)i * Backend::kStride + Backend::kFrameOff;
+      const uint8_t* f = tx_base_[half] + (size_t)i * Backend::kStride;
       link_.send(f, 14 + srv_detail::rd16(f + 16));
     }
   }
   bool txOnHost() const { return tx_data_n_ < kTxGpuMin; }
   void fillTxHost(uint32_t half, uint32_t n) { // the frames header() left unsummed (header-only ones are done)
     for (const uint32_t i : tx_fill_[half])
-      srv_detail::fill_tcp_checksums(be_.txSlots(half) + (size_t)i * Backend::kStride + Backend::kFrameOff);
+      srv_detail::fill_tcp_checksums(tx_base_[half] + (size_t)i * Backend::kStride);
     tx_fill_[half].clear();
     tx_host_frames_ += n;
   }
@@ -1315,7 +1317,7 @@ class TcpEngine {
   enum Kind { kSyn, kSynAck, kData, kFinAck, kAck, kRstAck };
   uint8_t* txFrame() {
     if (tx_n_ == kTxBatch) flushTx();
-    return be_.txSlots(tx_cur_) + (size_t)tx_n_++ * Backend::kStride + Backend::kFrameOff;
+    return tx_base_[tx_cur_] + (size_t)tx_n_++ * Backend::kStride;
   }
   void header(uint8_t* f, const uint8_t* dst_mac, uint32_t dst_ip, uint16_t src_port, uint16_t dst_port, uint32_t seq,
               uint32_t ack, uint8_t doff_words, uint8_t flags, uint16_t window, uint32_t tcp_len) {
@@ -1452,6 +1454,7 @@ class TcpEngine {
   uint64_t tver_ = 1, synced_ver_ = 0, disp_ver_ = 0, fl_ver_[2] = {0, 0};
   uint32_t cur_ = 0, fl_n_[2] = {0, 0};
   uint32_t tx_cur_ = 0, tx_fl_n_ = 0; // TX batch being built; frames of the other one in its fill (pipelined)
+  uint8_t* tx_base_[2] = {nullptr, nullptr}; // be_.txSlots(half) + kFrameOff, set at init
   uint32_t tx_data_n_ = 0;            // payload-bearing frames in the batch being built
   std::vector<uint32_t> tx_fill_[2];  // per TX batch: the frames whose checksums are filled at flush
   bool tx_fl_host_ = false;           // the batch in its fill was summed on the host
