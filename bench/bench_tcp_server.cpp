@@ -11,11 +11,12 @@
 // bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
-//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|resident_pair|twin_timed|echo]   prints one JSON line; exit 0 = all data delivered
+//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|resident_pair|resident_pair_cold|twin_timed|echo]   prints one JSON line; exit 0 = all data delivered
 //         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512 (also pipelined),
 //         GPU pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
 //         checksum summed) — bench.py's secondary.tcp_server_poll)
 #include <arpa/inet.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -46,6 +47,8 @@ static const uint8_t kServerMac[6] = {2, 0, 0, 0, 0, 1};
 static const uint32_t kPayload = 1460;
 
 // The peers and the NIC: n_flows clients, frames written into the server's RX ring.
+static bool g_cold = false; // resident_pair_cold: every leg's link leaves its frames out of the caches
+
 struct BenchLink {
   enum Phase { Syn, Ack, Data, Idle } phase = Idle;
   uint32_t n_flows = 0;
@@ -57,6 +60,7 @@ struct BenchLink {
   uint64_t acks = 0, rsts = 0, synacks = 0, other = 0;
   // echo workload: the peers acknowledge every byte the server sent them (their next frames carry it)
   bool echo = false;
+  bool cold = false; // frames flushed from the CPU caches after each fill (resident_pair_cold)
   std::vector<uint32_t> flow_of_port; // port -> flow + 1
   std::vector<uint64_t> srv_data;     // payload bytes the server sent each flow
   uint64_t echo_bytes = 0, echo_frames = 0;
@@ -174,6 +178,10 @@ struct BenchLink {
       poll_no++;
       data_frames += n;
     }
+    if (cold) // as a NIC's DMA leaves them: every line of the frames written this fill out of the caches
+      for (uint32_t i = 0; i < n; i++)
+        for (uint32_t b = 0; b < off + 1514; b += 64) _mm_clflush(slots + (size_t)i * stride + b);
+    if (cold) _mm_sfence();
     fill_s += secs(t0, Clock::now());
     return n;
   }
@@ -305,6 +313,7 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   srv->setDropBadChecksum(verify);
   Handler h;
   BenchLink& link = srv->link();
+  link.cold = g_cold;
   h.echo = link.echo = kEcho;
   link.phase = BenchLink::Syn;
   srv->poll(h);
@@ -385,6 +394,7 @@ static Run runRef(uint32_t n_flows, uint32_t polls, bool echo = false) {
   Run out;
   using Srv = efvitcp::EfviTcpServer<RefBenchConf>;
   auto link = std::make_unique<BenchLink>();
+  link->cold = g_cold;
   link->setup(n_flows);
   efvitcp::RefEnv& env = efvitcp::refEnv();
   env.link = link.get();
@@ -503,7 +513,10 @@ int main(int argc, char** argv) {
 #ifdef PN_BENCH_REF
     leg("reference_server_release_build", runRef(n_flows, polls));
 #endif
-  } else if (argc > 3 && std::strcmp(argv[3], "resident_pair") == 0) { // the drop-in's best leg beside the reference
+  } else if (argc > 3 && (std::strcmp(argv[3], "resident_pair") == 0 || std::strcmp(argv[3], "resident_pair_cold") == 0)) {
+    // the drop-in's best leg beside the reference; _cold: the frames out of the CPU caches after each fill, as a NIC's
+    // DMA leaves them (without DDIO), for both
+    g_cold = std::strcmp(argv[3], "resident_pair_cold") == 0;
     leg("gpu_rxbatch_512_pipelined_resident_release_path", runOne<512, GpuBackend, 0, true, true>(n_flows, polls, false));
 #ifdef PN_BENCH_REF
     leg("reference_server_release_build", runRef(n_flows, polls));
@@ -543,7 +556,7 @@ int main(int argc, char** argv) {
     leg("gpu_rxbatch_16384_pipelined", runOne<16384, GpuBackend, 0, true>(n_flows, polls / 4));
   }
   if (argc <= 3 || (std::strcmp(argv[3], "quick") != 0 && std::strcmp(argv[3], "release_pair") != 0 &&
-                    std::strcmp(argv[3], "resident_pair") != 0 &&
+                    std::strcmp(argv[3], "resident_pair") != 0 && std::strcmp(argv[3], "resident_pair_cold") != 0 &&
                     std::strcmp(argv[3], "twin_timed") != 0 && std::strcmp(argv[3], "echo") != 0)) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
