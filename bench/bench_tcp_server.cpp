@@ -181,7 +181,7 @@ struct BenchLink {
     if (cold) // as a NIC's DMA leaves them: every line of the frames written this fill out of the caches
       for (uint32_t i = 0; i < n; i++)
         for (uint32_t b = 0; b < off + 1514; b += 64) _mm_clflush(slots + (size_t)i * stride + b);
-    if (cold) _mm_sfence();
+    if (cold) _mm_mfence(); // the flushes done inside the fill (the link's time), not in the server's
     fill_s += secs(t0, Clock::now());
     return n;
   }
