@@ -602,6 +602,12 @@ def server_poll():
         line = json.loads(r.stdout.strip().splitlines()[-1])
         if r.returncode != 0:
             line["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
+        # the best GPU leg beside the reference with every frame flushed from the CPU caches after the link writes
+        # it, as a NIC's DMA leaves it (resident_pair_cold); server-only rates drop the flushes' time
+        rc = subprocess.run([exe, "256", "1000", "resident_pair_cold"], capture_output=True, text=True, timeout=120)
+        line["cold"] = json.loads(rc.stdout.strip().splitlines()[-1])
+        if rc.returncode != 0:
+            line["cold"]["error"] = f"exit {rc.returncode}: {rc.stderr[-300:]}"
         return line
     except Exception as ex:  # measured extra; never blocks the bench line
         return {"error": repr(ex)}
@@ -895,6 +901,10 @@ def summary(out):
                                                             "mframes_per_s"),
             "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s"),
             "server_reference_release_mfps": g(sec, "tcp_server_poll", "reference_server_release_build", "mframes_per_s"),
+            "server_cold_frames_resident_vs_reference_mfps": [
+                g(sec, "tcp_server_poll", "cold", "gpu_rxbatch_512_pipelined_resident_release_path",
+                  "mframes_per_s_server_only"),
+                g(sec, "tcp_server_poll", "cold", "reference_server_release_build", "mframes_per_s_server_only")],
             "zero_copy_64_us_notify_vs_service": [g(sec, "small_batch_latency", "zero_copy", "64", "signal_us"),
                                                   g(sec, "small_batch_latency", "zero_copy", "64", "service_us")],
             "zero_copy_64_release_us_notify_vs_service": [
