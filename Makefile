@@ -138,10 +138,10 @@ $(TCPRXBENCH): bench/bench_tcp_rx.cpp tests/cpp/segframes.hpp include/pollnet_am
 
 # GpuTcpServer::poll throughput (handshake, RX, ACKs) on the GPU vs the same server on the sequential backend
 # (with the reference's own server as the release-path CPU leg where its text is present: oracle/ref_server.hpp)
-$(SRVBENCH): bench/bench_tcp_server.cpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp \
+$(SRVBENCH): bench/bench_tcp_server.cpp bench/sampler.hpp tests/cpp/segframes.hpp tests/cpp/server_harness.hpp include/pollnet_amd/tcp_server.hpp \
   include/pollnet_amd/tcp_engine.hpp include/pollnet_amd/rx_conn.hpp include/pollnet_amd/gpu_rx.hpp $(HDRS) $(LIB) $(ORACLE) \
   $(if $(HAVE_REF_TEXT),oracle/ref_server.hpp $(CONN_INCS))
-	$(HOSTHIP) -O3 -std=c++17 -Wall -Wno-unused-result -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
+	$(HOSTHIP) -O3 -g -std=c++17 -Wall -Wno-unused-result -o $@ $< -Lpollnet_amd -lpollnet_amd -Loracle -loracle \
 	  -Wl,-rpath,'$$ORIGIN/../pollnet_amd' -Wl,-rpath,'$$ORIGIN/../oracle'
 
 # TX fill at small batch sizes, one in-place launch vs two phases (variant 41: make TUNING=1; not in `all`)

@@ -602,12 +602,15 @@ def server_poll():
         line = json.loads(r.stdout.strip().splitlines()[-1])
         if r.returncode != 0:
             line["error"] = f"exit {r.returncode}: {r.stderr[-300:]}"
-        # the best GPU leg beside the reference with every frame flushed from the CPU caches after the link writes
-        # it, as a NIC's DMA leaves it (resident_pair_cold); server-only rates drop the flushes' time
-        rc = subprocess.run([exe, "256", "1000", "resident_pair_cold"], capture_output=True, text=True, timeout=120)
-        line["cold"] = json.loads(rc.stdout.strip().splitlines()[-1])
-        if rc.returncode != 0:
-            line["cold"]["error"] = f"exit {rc.returncode}: {rc.stderr[-300:]}"
+        # the best GPU leg beside the reference with the frames where a NIC leaves them: written by
+        # another core of the CCD (resident_pair_l3: DDIO / cache injection, L3 or a neighbour's L2), and flushed from
+        # the CPU caches after the link writes them (resident_pair_cold: DMA to DRAM); server-only rates drop the
+        # link's time (its writes, flushes, the hand-off to the writer core)
+        for key, mode in (("l3", "resident_pair_l3"), ("cold", "resident_pair_cold")):
+            rc = subprocess.run([exe, "256", "1000", mode], capture_output=True, text=True, timeout=120)
+            line[key] = json.loads(rc.stdout.strip().splitlines()[-1])
+            if rc.returncode != 0:
+                line[key]["error"] = f"exit {rc.returncode}: {rc.stderr[-300:]}"
         return line
     except Exception as ex:  # measured extra; never blocks the bench line
         return {"error": repr(ex)}
@@ -653,66 +656,95 @@ def small_batch_latency():
         return {"error": repr(ex)}
 
 
-def secondary_tx(torch, pa, n, steps, stream):
+def secondary_tx(torch, pa, n, steps, stream, rounds=6):
     """TX checksum fill (pn_tx_fill, PN_TX_TCP) over C2 batches with both checksum fields
     scrambled, at the ring layout (frame_off 2) and efvitcp's SendBuf layout (frame_off 14 =
     offsetof(SendBuf, eth_hdr), Core.h:147-156).  Algorithmic bytes per frame = tot_len read
-    + 4 B written (1,504).  Correctness: the first 4096 frames equal the oracle's fill, and
-    every filled frame equals the generator's original except the ones it built with a
-    flipped payload bit (every 1024th)."""
+    + 4 B written (1,504).  Both layouts run on the SAME two resident buffers: the frames are moved
+    between the offsets in place (the HBM pages stay), and the timing alternates the layouts over
+    `rounds` rounds (order reversed every round), so their ratio is the layout's cost alone, not
+    where a batch landed in HBM.  Correctness: the first 4096 frames equal the oracle's fill, and
+    every filled frame equals the generator's original except the ones it built with a flipped
+    payload bit (every 1024th)."""
     from oracle import pyoracle as orc
+    from pollnet_amd import tuning as tn  # measurement-only library
 
     ctx = pa.RxContext(torch.cuda.current_device())
     out = {}
     p = pa.rx.GenParams.for_config(2)
     host = np.empty((n, STRIDE), dtype=np.uint8)
+    bufs = []
+    for b in range(2):
+        pa.gen_frames(p, n, STRIDE, 2, first_index=b * n, threads=min(16, cpu_threads()), out=host)
+        bufs.append(torch.from_numpy(host.reshape(-1)).cuda())
+    del host
+    span = 1514 + 8  # the frame and its pad byte, moved as one piece
+    cur = [2]
+
+    def place(off):  # the frames of both buffers to frame_off `off`, in place
+        if off != cur[0]:
+            for d in bufs:
+                v = d.view(n, STRIDE)
+                v[:, off:off + span] = v[:, cur[0]:cur[0] + span].clone()
+            cur[0] = off
+            torch.cuda.synchronize()
+
+    def fill(d, off):
+        ctx.tx_fill(d, STRIDE, off, n, None, pa.PN_TX_TCP, stream)
+
+    checks = {}
     for off in (2, 14):
-        bufs = []
-        for b in range(2):
-            pa.gen_frames(p, n, STRIDE, off, first_index=b * n, threads=min(16, cpu_threads()), out=host)
-            d = torch.from_numpy(host.reshape(-1)).cuda()
-            if b == 0:
-                orig = d.clone()
-                exp = host[:4096].copy()
-            v = d.view(n, STRIDE)
-            v[:, off + 24:off + 26] = 0x5A  # ip checksum
-            v[:, off + 50:off + 52] = 0xA5  # tcp checksum
-            bufs.append(d)
-        ctx.tx_fill(bufs[0], STRIDE, off, n, None, pa.PN_TX_TCP, stream)
+        place(off)
+        v = bufs[0].view(n, STRIDE)
+        orig = bufs[0].clone()
+        exp = v[:4096].cpu().numpy().copy()
+        v[:, off + 24:off + 26] = 0x5A  # ip checksum
+        v[:, off + 50:off + 52] = 0xA5  # tcp checksum
+        fill(bufs[0], off)
         torch.cuda.synchronize()
         diff = (bufs[0].view(n, STRIDE) != orig.view(n, STRIDE)).any(dim=1)
         bad = torch.nonzero(diff).flatten().cpu().numpy()
-        got = bufs[0][: 4096 * STRIDE].cpu().numpy().reshape(4096, STRIDE)
+        got = v[:4096].cpu().numpy()
         exp[:, off + 24:off + 26] = 0x5A
         exp[:, off + 50:off + 52] = 0xA5
         orc.tx_fill_batch(exp, STRIDE, off, 4096, None, orc.TX_TCP)
-        from pollnet_amd import tuning as tn  # measurement-only library
-
-        ks, abl = [], []
-        for _ in range(5):  # product and ablated ceiling alternately (the ceiling's fields are garbage;
-            # the fill recomputes both from the frame bytes, so the product's timing is unaffected)
-            ks.append(time_launches(torch, lambda d: ctx.tx_fill(d, STRIDE, off, n, None, pa.PN_TX_TCP, stream), bufs,
-                                    steps, stream))
-            abl.append(time_launches(torch, lambda d: tn.calib_tx_ablated(ctx, d, STRIDE, off, n, stream), bufs, steps,
-                                     stream))
-        kern, kabl = statistics.median(ks), statistics.median(abl)
+        checks[off] = {"first_4096_vs_oracle": bool(np.array_equal(got, exp)),
+                       "frames_changed_vs_valid_original": int(len(bad)),
+                       "only_corrupted_frames_differ": bool(len(bad) == n // 1024 and np.all(bad % 1024 == bad[0] % 1024))}
+        del orig
+    ks = {2: [], 14: []}
+    abl = {2: [], 14: []}
+    for r in range(rounds):  # product and ablated ceiling alternately (the ceiling's fields are garbage; the fill
+        # recomputes both from the frame bytes, so the product's timing is unaffected)
+        for off in ((2, 14) if r % 2 == 0 else (14, 2)):
+            place(off)
+            ks[off].append(time_launches(torch, lambda d: fill(d, off), bufs, steps, stream))
+            abl[off].append(time_launches(torch, lambda d: tn.calib_tx_ablated(ctx, d, STRIDE, off, n, stream), bufs,
+                                          steps, stream))
+    for off in (2, 14):
+        kern, kabl = statistics.median(ks[off]), statistics.median(abl[off])
         algo = 1504 * n
         tr = load_pmc("tx_c2_n1048576", f"frame_off_{off}")
         out[f"frame_off_{off}"] = {
             "kernel": "tx_fill_kernel + tx_patch_kernel (one pn_tx_fill call)", "frames": n, "resident_batches": 2,
-            "kernel_ms": round(kern, 5), "gbit_per_s": round(8 * 1514 * n / (kern * 1e-3) / 1e9, 1),
+            "kernel_ms": round(kern, 5), "kernel_ms_rounds": [round(x, 5) for x in ks[off]],
+            "gbit_per_s": round(8 * 1514 * n / (kern * 1e-3) / 1e9, 1),
             "algorithmic_bytes_per_launch": algo, "achieved_gbs": round(algo / (kern * 1e-3) / 1e9, 1),
             "frac": round(algo / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "ablated_kernel_ms": round(kabl, 5), "kernel_vs_ablated_ceiling": round(kabl / kern, 4),
-            "at_ceiling_within_spread": abs(1 - kabl / kern) <= max((max(ks) - min(ks)) / kern, 0.002),
+            "at_ceiling_within_spread": abs(1 - kabl / kern) <= max((max(ks[off]) - min(ks[off])) / kern, 0.002),
             **pmc_fields(tr),
             "write_requests_per_frame": None if not (tr and tr["code_current"]) else tr.get("ea_write_requests_per_frame"),
             "write_64B_per_frame": None if not (tr and tr["code_current"]) else tr.get("ea_write_64B_per_frame"),
-            "first_4096_vs_oracle": bool(np.array_equal(got, exp)),
-            "frames_changed_vs_valid_original": int(len(bad)),
-            "only_corrupted_frames_differ": bool(len(bad) == n // 1024 and np.all(bad % 1024 == bad[0] % 1024))}
-        del bufs, orig
-        torch.cuda.empty_cache()
+            **checks[off]}
+    r14 = [a / b for a, b in zip(ks[14], ks[2])]
+    out["same_buffers_off14_over_off2"] = {
+        "ratio_median": round(statistics.median(r14), 4), "ratio_per_round": [round(x, 4) for x in r14],
+        "write_requests_per_frame_off2_off14": [out["frame_off_2"]["write_requests_per_frame"],
+                                               out["frame_off_14"]["write_requests_per_frame"]],
+        "note": "the same two resident buffers at both layouts (frames moved in place), rounds alternating the order"}
+    del bufs
+    torch.cuda.empty_cache()
     ctx.close()
     return out
 
@@ -748,6 +780,55 @@ def secondary_release_path(torch, pa, ctx, frames_b, res, n, steps, stream):
             "records_equal_full_path_less_tcp_verdict": ok,
             "note": "pn_set_verify(ctx, 0) on the rotating C2 batches: one 128-B header line read per frame (the "
                     "64-B window block inside it), no TCP checksum; DESIGN §4"}
+
+
+def secondary_service_large_post(torch, pa, ctx, frames_b, res, n, stream, reps=15):
+    """A 1-Mi-frame post to the resident classify service (pn_service_*) against pn_classify on the same
+    rotating device-resident C2 batches, verified and release path: host wall clock from the post (launch) to the
+    records being complete (pn_service_wait / stream sync), median of `reps`.  The service as opened by default
+    (the latency tier + helper waves launched with a large post) and with the latency tier alone (large_waves 64,
+    the round-5 service).  Every post's records must equal pn_classify's."""
+    out = {"frames": n, "reps": reps,
+           "note": "host wall clock post -> complete (service) vs launch -> stream sync (pn_classify), device memory"}
+    out_b = torch.empty_like(res)
+    for verify in (True, False):
+        ctx.set_verify(verify)
+        try:
+            leg = {}
+
+            def classify_once(k):
+                t = time.perf_counter()
+                ctx.classify(frames_b[k % len(frames_b)], STRIDE, FRAME_OFF, n, res, stream)
+                torch.cuda.synchronize()
+                return time.perf_counter() - t
+
+            for k in range(3):
+                classify_once(k)
+            leg["pn_classify_ms"] = round(statistics.median(classify_once(k) for k in range(reps)) * 1e3, 4)
+            for name, lw in (("service_default", 0), ("service_latency_tier_only", pa.PN_SERVICE_WAVES)):
+                svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=1000, large_waves=lw)
+                try:
+                    def post_once(k):
+                        t = time.perf_counter()
+                        svc.post(frames_b[k % len(frames_b)], n, out_b)
+                        svc.wait()
+                        return time.perf_counter() - t
+
+                    for k in range(3):
+                        post_once(k)
+                    ms = statistics.median(post_once(k) for k in range(reps)) * 1e3
+                    ctx.classify(frames_b[0], STRIDE, FRAME_OFF, n, res, stream)
+                    torch.cuda.synchronize()
+                    svc.post(frames_b[0], n, out_b)
+                    svc.wait()
+                    leg[name] = {"ms": round(ms, 4), "vs_pn_classify": round(ms / leg["pn_classify_ms"], 3),
+                                 "records_equal_pn_classify": bool(torch.equal(out_b, res))}
+                finally:
+                    svc.close()
+            out["verified" if verify else "release_path"] = leg
+        finally:
+            ctx.set_verify(True)
+    return out
 
 
 def secondary_c4_shard(torch, pa, ctx_dev, steps, R, stream):
@@ -883,8 +964,12 @@ def summary(out):
             "tx_off2_frac": g(sec, "tx_fill", "frame_off_2", "frac"), "tx_off14_frac": g(sec, "tx_fill", "frame_off_14", "frac"),
             "tx_off2_ms": g(sec, "tx_fill", "frame_off_2", "kernel_ms"),
             "tx_off14_ms": g(sec, "tx_fill", "frame_off_14", "kernel_ms"),
+            "tx_off14_over_off2_same_buffers": g(sec, "tx_fill", "same_buffers_off14_over_off2", "ratio_median"),
             "match_streams_ms": g(sec, "match_streams", "kernel_ms"),
             "release_path_ms": g(sec, "c2_release_path", "kernel_ms"),
+            "service_1mi_post_vs_pn_classify_verified_release": [
+                g(sec, "service_large_post", "verified", "service_default", "vs_pn_classify"),
+                g(sec, "service_large_post", "release_path", "service_default", "vs_pn_classify")],
             "server_512_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512", "mframes_per_s"),
             "server_512_release_mfps": g(sec, "tcp_server_poll", "gpu_rxbatch_512_release_path", "mframes_per_s"),
             "server_cpu_512_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512", "mframes_per_s"),
@@ -901,6 +986,13 @@ def summary(out):
                                                             "mframes_per_s"),
             "server_cpu_512_release_mfps": g(sec, "tcp_server_poll", "cpu_rxbatch_512_release_path", "mframes_per_s"),
             "server_reference_release_mfps": g(sec, "tcp_server_poll", "reference_server_release_build", "mframes_per_s"),
+            "server_hot_frames_resident_vs_reference_mfps": [
+                g(sec, "tcp_server_poll", "gpu_rxbatch_512_pipelined_resident_release_path", "mframes_per_s_server_only"),
+                g(sec, "tcp_server_poll", "reference_server_release_build", "mframes_per_s_server_only")],
+            "server_l3_frames_resident_vs_reference_mfps": [
+                g(sec, "tcp_server_poll", "l3", "gpu_rxbatch_512_pipelined_resident_release_path",
+                  "mframes_per_s_server_only"),
+                g(sec, "tcp_server_poll", "l3", "reference_server_release_build", "mframes_per_s_server_only")],
             "server_cold_frames_resident_vs_reference_mfps": [
                 g(sec, "tcp_server_poll", "cold", "gpu_rxbatch_512_pipelined_resident_release_path",
                   "mframes_per_s_server_only"),
@@ -1178,6 +1270,10 @@ def run_rank(rank, world, local_rank, args):
             sec["c2_release_path"] = secondary_release_path(torch, pa, ctx, frames_b, res, n, args.steps, stream)
         except Exception as ex:  # measured extra; never blocks the bench line
             sec["c2_release_path"] = {"error": repr(ex)}
+        try:
+            sec["service_large_post"] = secondary_service_large_post(torch, pa, ctx, frames_b, res, n, stream)
+        except Exception as ex:  # measured extra; never blocks the bench line
+            sec["service_large_post"] = {"error": repr(ex)}
         del frames_b[1:]  # the C2 batches rotated above are done; make room for the others
         torch.cuda.empty_cache()
         try:

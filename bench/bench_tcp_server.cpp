@@ -11,15 +11,24 @@
 // bytes and consumes it.  The server ACKs every second segment (TcpConn.h:745-755).  The link
 // plays the NIC: the ring slots keep their frames between polls and only the sequence number
 // and TCP checksum are rewritten (6 bytes per frame; timed separately as `link_fill_share`).
-//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|resident_pair|resident_pair_cold|twin_timed|echo]   prints one JSON line; exit 0 = all data delivered
+//   argv: n_flows (256)  polls (400)  [cpu|quick|release_pair|resident_pair|resident_pair_l3|resident_pair_cold|twin_timed|echo]
+//         prints one JSON line; exit 0 = all data delivered
 //         (cpu: the sequential-backend legs only, no GPU needed; quick: GPU RxBatch 512 (also pipelined),
 //         GPU pipelined 16384 and CPU 512, each verified and on the release path (discard off, no
-//         checksum summed) — bench.py's secondary.tcp_server_poll)
+//         checksum summed) — bench.py's secondary.tcp_server_poll; resident_pair*: the best GPU leg beside the
+//         reference with the frames where a NIC's DMA leaves them: hot (written by the server's own core),
+//         _l3 (written by another core of the same CCD, as DDIO / cache injection leaves them in the L3 or a
+//         neighbour's L2), _cold (flushed to DRAM))
 #include <arpa/inet.h>
 #include <emmintrin.h>
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +40,7 @@
 #include "../include/pollnet_amd/tcp_server.hpp"
 #include "../tests/cpp/segframes.hpp"
 #include "../tests/cpp/server_harness.hpp"
+#include "sampler.hpp"
 // The reference's own server (pollnet's EfviTcpServer over efvitcp's TcpServer / TcpConn, compiled from the text
 // oracle/ref.mk extracts from /root/reference; only the ef_vi plumbing is restated, oracle/ref_server.hpp) as the
 // CPU baseline of the release-path legs, where that text was present at build time.
@@ -48,6 +58,62 @@ static const uint32_t kPayload = 1460;
 
 // The peers and the NIC: n_flows clients, frames written into the server's RX ring.
 static bool g_cold = false; // resident_pair_cold: every leg's link leaves its frames out of the caches
+
+// resident_pair_l3: the link's writes run on another core (the next allowed CPU after the server's, normally a core
+// of the same CCD), so the lines the server then reads come from the shared L3 / that core's L2, as a NIC with
+// DDIO or cache injection leaves them -- between a hot ring (the server's own writes) and a cold one (DRAM).
+struct RemoteWriter {
+  std::thread th;
+  std::atomic<uint64_t> req{0}, done{0};
+  std::atomic<bool> stop{false};
+  void (*fn)(void*) = nullptr;
+  void* arg = nullptr;
+  int cpu_server = -1, cpu_writer = -1;
+  bool start() {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return false;
+    for (int c = 0; c < CPU_SETSIZE; c++)
+      if (CPU_ISSET(c, &set)) {
+        if (cpu_server < 0) cpu_server = c;
+        else if (cpu_writer < 0) cpu_writer = c;
+      }
+    if (cpu_writer < 0) return false;
+    cpu_set_t one;
+    CPU_ZERO(&one);
+    CPU_SET(cpu_server, &one);
+    if (pthread_setaffinity_np(pthread_self(), sizeof one, &one) != 0) return false;
+    th = std::thread([this] {
+      cpu_set_t w;
+      CPU_ZERO(&w);
+      CPU_SET(cpu_writer, &w);
+      pthread_setaffinity_np(pthread_self(), sizeof w, &w);
+      uint64_t seen = 0;
+      while (!stop.load(std::memory_order_acquire)) {
+        const uint64_t r = req.load(std::memory_order_acquire);
+        if (r == seen) {
+          _mm_pause();
+          continue;
+        }
+        fn(arg);
+        seen = r;
+        done.store(r, std::memory_order_release);
+      }
+    });
+    return true;
+  }
+  void run(void (*f)(void*), void* a) { // f(a) on the writer's core; returns when it is done
+    fn = f;
+    arg = a;
+    const uint64_t r = req.load(std::memory_order_relaxed) + 1;
+    req.store(r, std::memory_order_release);
+    while (done.load(std::memory_order_acquire) != r) _mm_pause();
+  }
+  ~RemoteWriter() {
+    stop.store(true, std::memory_order_release);
+    if (th.joinable()) th.join();
+  }
+};
+static RemoteWriter* g_writer = nullptr;
 
 struct BenchLink {
   enum Phase { Syn, Ack, Data, Idle } phase = Idle;
@@ -113,6 +179,19 @@ struct BenchLink {
 
   const char* open(const char*) { return nullptr; }
   uint32_t fill(uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
+    if (!g_writer) return fillHere(slots, stride, off, cap);
+    struct Job {
+      BenchLink* l;
+      uint8_t* slots;
+      uint32_t stride, off, cap, n;
+    } j{this, slots, stride, off, cap, 0};
+    const double before = fill_s;
+    const auto t0 = Clock::now();
+    g_writer->run([](void* a) { auto* x = static_cast<Job*>(a); x->n = x->l->fillHere(x->slots, x->stride, x->off, x->cap); }, &j);
+    fill_s = before + secs(t0, Clock::now()); // the link's time as the server's core sees it (handshake included)
+    return j.n;
+  }
+  uint32_t fillHere(uint8_t* slots, uint32_t stride, uint32_t off, uint32_t cap) {
     const auto t0 = Clock::now();
     uint32_t n = 0;
     if (phase == Syn || phase == Ack) {
@@ -331,9 +410,11 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   for (uint32_t p = 0; p < warm; p++) srv->poll(h);
   const uint64_t bytes0 = h.bytes, acks0 = link.acks, echo0 = link.echo_bytes;
   link.fill_s = 0;
+  pn_sampler::start(std::is_same_v<Backend, GpuBackend> ? "gpu" : "twin");
   const auto t0 = Clock::now();
   for (uint32_t p = 0; p < polls; p++) srv->poll(h);
   const double t = secs(t0, Clock::now());
+  pn_sampler::stop();
   const uint64_t timed_bytes = h.bytes - bytes0;
   if (kEcho) out.echo_gbps = (link.echo_bytes - echo0) * 8.0 / t / 1e9;
   link.phase = BenchLink::Idle;
@@ -427,9 +508,11 @@ static Run runRef(uint32_t n_flows, uint32_t polls, bool echo = false) {
   for (uint32_t p = 0; p < warm; p++) srv->poll(h);
   const uint64_t bytes0 = h.bytes, acks0 = link->acks, frames0 = link->data_frames, echo0 = link->echo_bytes;
   link->fill_s = 0;
+  pn_sampler::start("reference");
   const auto t0 = Clock::now();
   for (uint32_t p = 0; p < ref_polls; p++) srv->poll(h);
   const double t = secs(t0, Clock::now());
+  pn_sampler::stop();
   const uint64_t frames = link->data_frames - frames0;
   if (echo) out.echo_gbps = (link->echo_bytes - echo0) * 8.0 / t / 1e9;
   out.mfps = frames / t / 1e6;
@@ -513,10 +596,21 @@ int main(int argc, char** argv) {
 #ifdef PN_BENCH_REF
     leg("reference_server_release_build", runRef(n_flows, polls));
 #endif
-  } else if (argc > 3 && (std::strcmp(argv[3], "resident_pair") == 0 || std::strcmp(argv[3], "resident_pair_cold") == 0)) {
-    // the drop-in's best leg beside the reference; _cold: the frames out of the CPU caches after each fill, as a NIC's
-    // DMA leaves them (without DDIO), for both
+  } else if (argc > 3 && (std::strcmp(argv[3], "resident_pair") == 0 || std::strcmp(argv[3], "resident_pair_cold") == 0 ||
+                           std::strcmp(argv[3], "resident_pair_l3") == 0)) {
+    // the drop-in's best leg beside the reference, with the frames hot (the link writes them on the server's core),
+    // _l3: written by another core (as a NIC with DDIO / cache injection leaves them), _cold: out of the CPU caches
+    // after each fill (a NIC's DMA without DDIO); the same for both legs
     g_cold = std::strcmp(argv[3], "resident_pair_cold") == 0;
+    static RemoteWriter writer;
+    if (std::strcmp(argv[3], "resident_pair_l3") == 0) {
+      if (!writer.start()) {
+        std::fprintf(stderr, "resident_pair_l3: needs two allowed CPUs\n");
+        return 2;
+      }
+      g_writer = &writer;
+      lines += "\"cpus_server_writer\": [" + std::to_string(writer.cpu_server) + ", " + std::to_string(writer.cpu_writer) + "]";
+    }
     leg("gpu_rxbatch_512_pipelined_resident_release_path", runOne<512, GpuBackend, 0, true, true>(n_flows, polls, false));
 #ifdef PN_BENCH_REF
     leg("reference_server_release_build", runRef(n_flows, polls));
@@ -557,6 +651,7 @@ int main(int argc, char** argv) {
   }
   if (argc <= 3 || (std::strcmp(argv[3], "quick") != 0 && std::strcmp(argv[3], "release_pair") != 0 &&
                     std::strcmp(argv[3], "resident_pair") != 0 && std::strcmp(argv[3], "resident_pair_cold") != 0 &&
+                    std::strcmp(argv[3], "resident_pair_l3") != 0 &&
                     std::strcmp(argv[3], "twin_timed") != 0 && std::strcmp(argv[3], "echo") != 0)) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));

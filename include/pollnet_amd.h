@@ -266,25 +266,41 @@ int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
                       const uint16_t* lens, uint32_t mode, void* stream, uint32_t* done_word, uint32_t token);
 
 /* ---- resident classify service: no launch per batch (round 5) ----
- * pn_service_open launches a kernel that stays on the GPU (PN_SERVICE_WAVES one-wave workgroups, on a stream of its
- * own) and classifies every batch the host posts afterwards, with the same code and records as pn_classify on the
- * layout given at open (strided slots).  A post is a few stores into pinned host memory that the kernel polls, so a
- * batch starts ~1-2 us after it is posted instead of a launch's ~7 us (bench/bench_doorbell).
+ * pn_service_open launches a kernel that stays on the GPU (PN_SERVICE_WAVES one-wave workgroups on a stream of its
+ * own, the latency tier) and classifies every batch the host posts afterwards, with the same code and records as
+ * pn_classify on the layout given at open (strided slots).  A post is a few stores into pinned host memory that the
+ * kernel polls, so a batch starts ~1-2 us after it is posted instead of a launch's ~7 us (bench/bench_doorbell;
+ * DESIGN.md §13).
  *   pn_service_post: frames (pinned host or device memory, 16-B aligned), n in [1, PN_SERVICE_MAX_FRAMES], results
  *     (pinned host or device memory, 16-B aligned).  The ctx's conn table and pn_set_verify setting at the post are
- *     used.  At most two posts outstanding; non-blocking; *post_id (may be NULL) names the post.
+ *     used.  At most two posts outstanding (a third is refused, PN_EINVAL); non-blocking; *post_id (may be NULL)
+ *     names the post.  Frames and results must stay valid until the post completes.
  *   pn_service_wait: spins until post post_id's records are visible to the host (as pn_classify_notify's word);
  *     posts complete in order; post_id 0 = the last post.
  *   pn_service_close: waits for outstanding posts, stops the kernel, frees the service (before pn_close).
- * After idle_ms (1..10000) without a post the kernel ends by itself (every wait inside it has a wall-clock limit);
- * the next post relaunches it.  pn_set_conn_table may be called with at most one post outstanding (the table is
- * double-buffered; the post in flight keeps reading its buffer).  One thread per service, as per ctx.
+ * Post size.  Up to 4096 frames a post runs on the latency tier (a 64-frame post on one wave, no cross-wave step).
+ * Above, the post also runs on helper waves, a grid launched with the post on a second stream of the service (in all
+ * PN_SERVICE_WAVES_PER_CU waves per CU, 64-frame groups): the chip is not held while the service idles, and a
+ * 1-Mi-frame post runs at pn_classify's rate (DESIGN.md §13 has the measured figures), so a caller need not switch
+ * entry points by batch size.
+ * Timers.  After idle_ms (1..10000) without a post the kernel ends by itself; the next post (or wait) relaunches it.
+ * A post in flight has its own limit (8 s from its acceptance): should one of its waves never finish, the kernel ends
+ * and the host's next wait relaunches it, which runs the post again.  So the kernel always ends.
+ * Conn table.  pn_set_conn_table may be called at any time, posts outstanding or not: each post keeps classifying
+ * against the table it was posted with; a set that would overwrite or free the buffer an outstanding post reads waits
+ * for that post first (at most one post's run).  One thread per service, as per ctx.
+ * pn_service_open_ex: the same with a large post's wave count given (0 = the default above; else in
+ * [PN_SERVICE_WAVES, PN_SERVICE_MAX_WAVES]; PN_SERVICE_WAVES = no helpers, the latency tier alone).
  * Replaces the launch of the reference's per-poll work with its own busy-poll style (Core.h:494-498). */
 typedef struct pn_service pn_service;
-#define PN_SERVICE_WAVES 64u
+#define PN_SERVICE_WAVES 64u        /* the latency tier: every post of up to 4096 frames */
+#define PN_SERVICE_WAVES_PER_CU 8u  /* a large post's default wave count: this many per CU (2048 on a 256-CU MI355X) */
+#define PN_SERVICE_MAX_WAVES 4096u
 #define PN_SERVICE_MAX_FRAMES (1u << 20)
 #define PN_SERVICE_STOP 0xFFFFFFFFu /* internal: the stop post */
 int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, pn_service** out);
+int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, uint32_t large_waves,
+                       pn_service** out);
 int pn_service_post(pn_service* svc, const void* frames, uint32_t n, void* results, uint32_t* post_id);
 int pn_service_wait(pn_service* svc, uint32_t post_id);
 int pn_service_close(pn_service* svc);

@@ -20,6 +20,10 @@ from .rx import (  # noqa: F401
     STREAM_FILTER_DTYPE,
     PN_NO_STREAM,
     PN_MAX_STREAM_FILTERS,
+    PN_SERVICE_WAVES,
+    PN_SERVICE_WAVES_PER_CU,
+    PN_SERVICE_MAX_WAVES,
+    PN_SERVICE_MAX_FRAMES,
     F,
     ConnTable,
     PollnetError,

@@ -41,6 +41,7 @@ struct pn_ctx {
   pn_fence tx;                       // the last launch that used tx_patch
   void* sig_count = nullptr;         // pn_*_notify workgroup counters: [0] classify, [16] tx_fill (64-B apart)
   pn_fence sig[2];
+  std::vector<pn_service*> services; // open resident services (pn_service_*): their posts capture table buffers
   std::string err;
 };
 
@@ -53,6 +54,10 @@ inline int set_err(pn_ctx* ctx, int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+
+// Before pn_set_conn_table overwrites or frees table buffer `buf`: wait for every resident-service post that
+// captured it (rx_service.hip).
+int svc_release_table(pn_ctx* ctx, int buf);
 
 inline int hip_err(pn_ctx* ctx, hipError_t e, const char* what) {
   return set_err(ctx, PN_EHIP, std::string(what) + ": " + hipGetErrorString(e));

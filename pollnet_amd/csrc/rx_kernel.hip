@@ -124,11 +124,15 @@ int pn_set_conn_table(pn_ctx* ctx, const pn_conn_entry* entries, uint32_t n_entr
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   // the snapshot goes to the buffer launches are NOT reading now; its own readers (launches
-  // issued before the previous set) are waited for by event — normally long done — and the
-  // launches reading the current buffer, on any stream, keep running untouched
-  int rc = pn_internal::wait_retired(ctx);
-  if (rc) return rc;
+  // issued before the previous set) are waited for by event — normally long done — as are the
+  // resident-service posts that captured it (by their done words; the service's kernel never
+  // ends between posts, so no event on its stream could say it), and the launches and posts
+  // reading the current buffer, on any stream, keep running untouched
   const int nxt = ctx->tbl_dev ? ctx->cur ^ 1 : ctx->cur;
+  int rc = pn_internal::svc_release_table(ctx, nxt);
+  if (rc) return rc;
+  rc = pn_internal::wait_retired(ctx);
+  if (rc) return rc;
   if (n_entries > ctx->tbl_cap[nxt]) {
     if (ctx->tbl_buf[nxt]) (void)hipFree(ctx->tbl_buf[nxt]);
     ctx->tbl_buf[nxt] = nullptr;

@@ -11,11 +11,21 @@
 // one it first copies the slot to device memory, where the post's other waves read it.  Each wave of the post makes
 // its records system-visible and stores k to its own host done word -- the host waits on the words of the post's
 // waves, no cross-wave step on the way -- and then counts itself done on the device; the last resets the counter
-// and marks the post done for wave 0, which looks for post k + 1 only then.  A stop post (n = PN_SERVICE_STOP)
-// ends every wave.  Every wait has a device-wall-clock limit: after idle_ms without a post wave 0 publishes
-// "idle", stores the launch's epoch to the host's exit word and ends, and the others end on seeing it (or at their
-// own limit); the host relaunches on its next post.  So the kernel always ends.  Only vector memory operations
+// and marks the post done for wave 0, which looks for post k + 1 only then.  A post on more waves than there are
+// done words (a large one, round 6) completes through the count alone: the last of its waves stores k to done word 0.
+// A stop post (n = PN_SERVICE_STOP) ends every wave.  Every wait has a device-wall-clock limit: after idle_ms without
+// a post wave 0 publishes "idle", stores the launch's epoch to the host's exit word and ends, and the others end on
+// seeing it (or at their own limit); the host relaunches on its next post.  A post in flight has a limit of its own
+// (kPostLimitMs from its acceptance, not the idle limit): should a wave of it never finish, wave 0 gives up the same
+// way, exit word included, and the host's relaunch runs the post again.  So the kernel always ends.
+// Large posts (round 6).  The resident kernel is the latency tier: kLatWaves (64) one-wave workgroups, which answer
+// every post of up to 4096 frames and leave the rest of the chip to other kernels while idle.  A post above that
+// also runs on helper waves: a grid the host launches with the post on a stream of its own (a launch's ~7 us is
+// nothing beside a large post's run).  The helpers wait for wave 0 to publish their post, take their share of its
+// groups as waves kLatWaves.. of it, count themselves done like the resident waves, and end.  The slot's fpw word
+// carries the helper count (bits 8+), so wave 0 knows the post's wave count.  Only vector memory operations
 // (global loads / stores / one atomic add).
+#include <algorithm>
 #include <chrono>
 
 #include "rx_classify.hpp"
@@ -34,15 +44,19 @@ struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its devi
   const pn_conn_entry* tbl;
   uint64_t mask;
   uint32_t n_entries;
-  uint32_t fpw;   // frames per group (svc_fpw)
+  uint32_t fpw;   // frames per group (svc_fpw, bits 0-7) | helper waves << 8 (svc_helpers)
   uint32_t check; // svc_check: k ^ the xor of words 1-13, so a read that mixed two posts' words is refused
   uint32_t seq; // stored last (release)
 };
 static_assert(sizeof(SvcPost) == 64, "one line per post");
 
-constexpr uint32_t kExitWord = 96;   // host words: the waves' done words, then the exit word on a line of its own
+constexpr uint32_t kDoneWords = 64; // host words: one done word per wave of a post on at most this many waves,
+constexpr uint32_t kExitWord = 96;   // then the exit word on a line of its own
 constexpr uint32_t kWordsBytes = 512;
-static_assert(PN_SERVICE_WAVES <= 64, "the done words fill [0, 64)");
+constexpr uint32_t kLatWaves = PN_SERVICE_WAVES; // the latency tier: every post of up to 4096 frames runs on these
+static_assert(kLatWaves <= kDoneWords, "a latency-tier post completes through per-wave done words");
+constexpr uint32_t kLatFrames = kLatWaves * kFramesPerWave; // the largest post the tier takes alone
+constexpr uint32_t kPostLimitMs = 8000; // a post in flight (pn_service_wait gives up at 10 s)
 constexpr uint32_t kSvcIdle = 0xFFFFFFFFu; // published as the post when wave 0 ends for lack of posts
 constexpr uint32_t kSvcStop = 0xFFFFFFFFu; // published as the wave count of a stop post
 
@@ -61,6 +75,7 @@ struct SArgs {
   uint32_t* exit_word;  // host: the launch's epoch once it ended for lack of posts
   SvcDev* dev;
   uint64_t idle_ticks; // device wall clock
+  uint64_t post_ticks; // kPostLimitMs
   uint32_t epoch;
   uint32_t last; // the post completed before this launch
   uint32_t stride, ipa_off, avail;
@@ -68,10 +83,11 @@ struct SArgs {
 
 // Frames per group (host, at the post).  The release path reads one header line per frame: 64 frames a wave, so a
 // post of up to 64 frames is wave 0's alone (no cross-wave step at all).  Verifying reads every byte: a small
-// post is spread over more waves (8 frames a group and up, as few waves' worth of streaming as the post allows).
-inline uint32_t svc_fpw(uint32_t n, uint32_t waves, bool verify) {
+// post is spread over more waves of the latency tier (8 frames a group and up, as few waves' worth of streaming as
+// the post allows).  A post above the tier's 64 groups of 64 frames runs 64-frame groups on every wave.
+inline uint32_t svc_fpw(uint32_t n, bool verify) {
   uint32_t fpw = verify ? 8u : kFramesPerWave;
-  while (fpw < kFramesPerWave && (n + fpw - 1) / fpw > waves) fpw <<= 1;
+  while (fpw < kFramesPerWave && (n + fpw - 1) / fpw > kLatWaves) fpw <<= 1;
   return fpw;
 }
 
@@ -87,6 +103,13 @@ inline uint32_t svc_check(const SvcPost* p, uint32_t k) {
 __host__ __device__ __forceinline__ uint32_t svc_active(uint32_t n, uint32_t fpw, uint32_t waves) {
   const uint32_t groups = (n + fpw - 1) / fpw;
   return groups < waves ? groups : waves;
+}
+
+// helper waves of a post (host): none up to kLatFrames, else one per group past the tier's, at most `max`
+inline uint32_t svc_helpers(uint32_t n, uint32_t max) {
+  if (n <= kLatFrames) return 0;
+  const uint32_t groups = (n + kFramesPerWave - 1) / kFramesPerWave;
+  return std::min(groups - kLatWaves, max);
 }
 
 // a post's kernel arguments from its 64-B line held one word per lane (lanes 0-15, SvcPost's layout)
@@ -107,12 +130,12 @@ __device__ __forceinline__ KArgs svc_args(uint32_t v, const SArgs& s) {
   a.ipa_off = s.ipa_off;
   a.avail = s.avail;
   a.offs = nullptr;
-  a.fpw = __builtin_amdgcn_readlane(v, 13);
+  a.fpw = __builtin_amdgcn_readlane(v, 13) & 0xffu;
   return a;
 }
 
-// wave w's groups of the post (round robin over the post's waves), then its records made visible to the host and
-// post k stored to its done word
+// wave w's groups of the post (round robin over the post's waves), then its records made visible to the host and,
+// on a post of at most kDoneWords waves, post k stored to its done word
 template <int MIS, int COOP>
 __device__ __forceinline__ void svc_run(const KArgs& a, bool verify, uint32_t w, uint32_t act, uint32_t k,
                                         uint32_t* done_word, int lane) {
@@ -121,15 +144,21 @@ __device__ __forceinline__ void svc_run(const KArgs& a, bool verify, uint32_t w,
     else classify_group<MIS, COOP, kProdAbl | kHeaderOnly, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
   }
   __threadfence_system();
-  if (lane == 0) __hip_atomic_store(done_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0 && act <= kDoneWords) __hip_atomic_store(done_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// a multi-wave post: count this wave done; the last one resets the count and marks the post done for wave 0
-__device__ __forceinline__ void svc_count(SvcDev* dev, uint32_t act, uint32_t k, int lane) {
+// a multi-wave post: count this wave done; the last one resets the count and marks the post done for wave 0, and
+// for a post on more than kDoneWords waves stores k to done word 0 (every wave's records were made system-visible
+// before its count: the fence pairs them with this store)
+__device__ __forceinline__ void svc_count(SvcDev* dev, uint32_t act, uint32_t k, uint32_t* done_word0, int lane) {
   if (lane == 0) {
     const uint32_t prev = atomicAdd(&dev->count, 1u);
     if (prev == act - 1) {
       dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
+      if (act > kDoneWords) {
+        __threadfence_system();
+        __hip_atomic_store(done_word0, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       __hip_atomic_store(&dev->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -139,16 +168,21 @@ __device__ __forceinline__ void svc_count(SvcDev* dev, uint32_t act, uint32_t k,
 // classifies alone.  A post's waves other than 0 read it from the device copy, which wave 0 overwrites (two posts
 // later) only after every one of them counted itself done, so they always see it whole; the waves a post does not
 // run on only note it went by (from the published word alone: they may skip posts).
+// Timers: wave 0's idle limit runs from the end of the last post (or the launch); a post's limit from its
+// acceptance.  Every other wave ends on wave 0's word; its own limit is only a safety net, measured from the last post
+// it saw go by and longer than anything wave 0 can spend before publishing the next word (a post's limit, then idle).
 template <int MIS, int COOP>
 __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   const int lane = threadIdx.x;
   const uint32_t w = blockIdx.x, W = gridDim.x;
   uint32_t last = s.last;
   uint64_t t0 = wall_clock64();
+  const uint64_t net = s.idle_ticks + (s.idle_ticks >> 1) + s.post_ticks;
   for (;;) {
     uint32_t v = 0;         // the post's 64-B line, lane i holding word i (lanes 0-15)
     uint32_t k = 0, act = 0; // the post and its wave count
     bool run = false;       // this wave classifies groups of post k
+    uint64_t t_acc = 0;     // wave 0: when it accepted post k
     if (w == 0) {
       k = last + 1;
       // the next post's slot, one 64-B read
@@ -170,12 +204,14 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         continue;
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
+      t_acc = wall_clock64();
       const uint32_t n = __builtin_amdgcn_readlane(v, 1);
       if (n == PN_SERVICE_STOP) {
         if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)kSvcStop << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      act = svc_active(n, __builtin_amdgcn_readlane(v, 13), W);
+      const uint32_t fw = __builtin_amdgcn_readlane(v, 13);
+      act = svc_active(n, fw & 0xffu, W + (fw >> 8));
       if (act > 1) { // the post's other waves read it from the device copy
         if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[k & 1])[lane] = v;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -188,8 +224,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
       if (k == kSvcIdle || act == kSvcStop) return;
       if (k == last) {
-        // the limit is wave 0's plus a margin (a safety net: wave 0 always publishes kSvcIdle first)
-        if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) return;
+        if (wall_clock64() - t0 > net) return; // a safety net: wave 0 always publishes kSvcIdle first
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
@@ -202,7 +237,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
     }
     if (run) { // one call site for every wave (the classify code is inlined once per path)
       svc_run<MIS, COOP>(svc_args(v, s), __builtin_amdgcn_readlane(v, 2) != 0, w, act, k, s.done_words + w, lane);
-      if (act > 1) svc_count(s.dev, act, k, lane);
+      if (act > 1) svc_count(s.dev, act, k, s.done_words, lane);
     }
     if (w == 0) {
       if (act == 1) { // one wave's work, done: let the others see it go by
@@ -210,8 +245,11 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       } else { // the next post only once every wave of this one is done (its device copy may then be reused)
         while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
                k) {
-          if (wall_clock64() - t0 > s.idle_ticks + (s.idle_ticks >> 1)) { // a wave that never finishes: give up
-            if (lane == 0) __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          if (wall_clock64() - t_acc > s.post_ticks) { // a wave of the post never finished: give up, and say so
+            if (lane == 0) {
+              __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             return;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -224,21 +262,62 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   }
 }
 
+// The helper waves of large post k: waves kLatWaves + blockIdx.x of it.  They wait for wave 0 to publish k (it does so
+// only once post k - 1 is done, so the device copy and the count are theirs), run their groups, count themselves done
+// and end.  They end at once on "idle" / "stop" or on a later post (the launch that published k is gone: the host
+// relaunches helpers with the kernel), and at their own limit, longer than anything wave 0 can take to publish k.
+template <int MIS, int COOP>
+__global__ __launch_bounds__(kWave) void rx_service_helper_kernel(SArgs s, uint32_t k) {
+  const int lane = threadIdx.x;
+  const uint32_t w = kLatWaves + blockIdx.x;
+  const uint64_t t0 = wall_clock64();
+  const uint64_t net = s.idle_ticks + 2 * s.post_ticks;
+  uint32_t act;
+  for (;;) {
+    const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ck = __builtin_amdgcn_readfirstlane((uint32_t)c);
+    act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
+    if (ck == kSvcIdle || act == kSvcStop || (int32_t)(ck - k) > 0) return;
+    if (ck == k) break;
+    if (wall_clock64() - t0 > net) return;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  if (w >= act) return; // never: the post's wave count includes every helper
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[k & 1]);
+  const uint32_t v = lane < 16 ? cp[lane] : 0u;
+  svc_run<MIS, COOP>(svc_args(v, s), __builtin_amdgcn_readlane(v, 2) != 0, w, act, k, s.done_words, lane);
+  svc_count(s.dev, act, k, s.done_words, lane);
+}
+
 template <int MIS>
 void launch_svc(bool coop, uint32_t waves, const SArgs& a, hipStream_t s) {
   if (coop) hipLaunchKernelGGL((rx_service_kernel<MIS, 1>), dim3(waves), dim3(kWave), 0, s, a);
   else hipLaunchKernelGGL((rx_service_kernel<MIS, 0>), dim3(waves), dim3(kWave), 0, s, a);
 }
+
+template <int MIS>
+void launch_helpers(bool coop, uint32_t helpers, const SArgs& a, uint32_t k, hipStream_t s) {
+  if (coop) hipLaunchKernelGGL((rx_service_helper_kernel<MIS, 1>), dim3(helpers), dim3(kWave), 0, s, a, k);
+  else hipLaunchKernelGGL((rx_service_helper_kernel<MIS, 0>), dim3(helpers), dim3(kWave), 0, s, a, k);
+}
 } // namespace
 
 struct pn_service {
   pn_ctx* ctx = nullptr;
-  hipStream_t stream = nullptr;
-  uint32_t stride = 0, frame_off = 0, waves = 0;
-  uint64_t idle_ticks = 0;
+  hipStream_t stream = nullptr;        // the resident kernel (the latency tier)
+  hipStream_t helper_stream = nullptr; // large posts' helper grids
+  uint32_t stride = 0, frame_off = 0;
+  uint32_t helpers_max = 0;            // helper waves of a large post: its total wave count less the tier's
+  uint32_t post_helpers[2] = {0, 0};   // helper waves of the last two posts (a relaunch launches them again)
+  uint64_t idle_ticks = 0, post_ticks = 0;
   SvcPost* mail = nullptr;    // pinned host: 2 slots
   uint32_t* words = nullptr;  // pinned host: [0, 64) the waves' done words, [kExitWord] exit (its own line)
-  uint32_t post_act[2] = {0, 0}; // waves of the last two posts (slot k & 1): whose words post k completes
+  uint32_t post_words[2] = {0, 0}; // done words of the last two posts (slot k & 1): whose words post k completes
+  // the conn-table buffer each post captured (ctx->tbl_buf[b]): the last post that did, per buffer, so that
+  // pn_set_conn_table waits for it before it overwrites or frees that buffer (svc_release_table)
+  uint32_t tbl_post[2] = {0, 0};
+  bool tbl_used[2] = {false, false};
   SvcDev* dev = nullptr;      // device
   uint32_t seq = 0;           // last post issued
   uint32_t epoch = 0;         // launches so far
@@ -249,46 +328,81 @@ struct pn_service {
 namespace {
 // Launch (or relaunch) the kernel; it starts waiting for post base + 1, base = the last completed post, so posts
 // issued but not yet seen by an ended launch are taken by this one (they are still in their slots).
-int svc_launch(pn_service* v, uint32_t base) {
-  pn_ctx* ctx = v->ctx;
-  SvcDev init{};
-  init.cur = base;
-  init.done = base;
-  hipError_t e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(v->stream); // the previous launch has ended, the state is in place
-  if (e != hipSuccess) return hip_err(ctx, e, "pn_service: device state");
-  ++v->epoch;
+SArgs svc_sargs(const pn_service* v, uint32_t base) {
   SArgs a;
   a.mail = v->mail;
   a.done_words = v->words;
   a.exit_word = v->words + kExitWord;
   a.dev = v->dev;
   a.idle_ticks = v->idle_ticks;
+  a.post_ticks = v->post_ticks;
   a.epoch = v->epoch;
   a.last = base;
   a.stride = v->stride;
   a.ipa_off = (v->frame_off + 14) & ~15u;
   a.avail = v->stride - v->frame_off;
+  return a;
+}
+
+// the helper grid of large post k
+int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
+  const SArgs a = svc_sargs(v, 0);
+  hipStream_t s = v->helper_stream;
   switch ((v->frame_off + 14) & 15) {
-    case 0: launch_svc<0>(v->coop, v->waves, a, v->stream); break;
-    case 2: launch_svc<2>(v->coop, v->waves, a, v->stream); break;
-    case 4: launch_svc<4>(v->coop, v->waves, a, v->stream); break;
-    case 6: launch_svc<6>(v->coop, v->waves, a, v->stream); break;
-    case 8: launch_svc<8>(v->coop, v->waves, a, v->stream); break;
-    case 10: launch_svc<10>(v->coop, v->waves, a, v->stream); break;
-    case 12: launch_svc<12>(v->coop, v->waves, a, v->stream); break;
-    default: launch_svc<14>(v->coop, v->waves, a, v->stream); break;
+    case 0: launch_helpers<0>(v->coop, helpers, a, k, s); break;
+    case 2: launch_helpers<2>(v->coop, helpers, a, k, s); break;
+    case 4: launch_helpers<4>(v->coop, helpers, a, k, s); break;
+    case 6: launch_helpers<6>(v->coop, helpers, a, k, s); break;
+    case 8: launch_helpers<8>(v->coop, helpers, a, k, s); break;
+    case 10: launch_helpers<10>(v->coop, helpers, a, k, s); break;
+    case 12: launch_helpers<12>(v->coop, helpers, a, k, s); break;
+    default: launch_helpers<14>(v->coop, helpers, a, k, s); break;
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return hip_err(v->ctx, e, "pn_service: helper launch");
+  return PN_OK;
+}
+
+int svc_launch(pn_service* v, uint32_t base) {
+  pn_ctx* ctx = v->ctx;
+  // the previous launch's helpers have ended (they end on its "idle" word) before the device state is reset under them
+  hipError_t e = hipStreamSynchronize(v->helper_stream);
+  if (e != hipSuccess) return hip_err(ctx, e, "pn_service: helper grids");
+  SvcDev init{};
+  init.cur = base;
+  init.done = base;
+  e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(v->stream); // the previous launch has ended, the state is in place
+  if (e != hipSuccess) return hip_err(ctx, e, "pn_service: device state");
+  ++v->epoch;
+  const SArgs a = svc_sargs(v, base);
+  switch ((v->frame_off + 14) & 15) {
+    case 0: launch_svc<0>(v->coop, kLatWaves, a, v->stream); break;
+    case 2: launch_svc<2>(v->coop, kLatWaves, a, v->stream); break;
+    case 4: launch_svc<4>(v->coop, kLatWaves, a, v->stream); break;
+    case 6: launch_svc<6>(v->coop, kLatWaves, a, v->stream); break;
+    case 8: launch_svc<8>(v->coop, kLatWaves, a, v->stream); break;
+    case 10: launch_svc<10>(v->coop, kLatWaves, a, v->stream); break;
+    case 12: launch_svc<12>(v->coop, kLatWaves, a, v->stream); break;
+    default: launch_svc<14>(v->coop, kLatWaves, a, v->stream); break;
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "pn_service: launch");
   v->running = true;
+  // posts issued but not completed (still in their slots) run again on this launch: their helpers with them
+  for (uint32_t k = base + 1; (int32_t)(v->seq - k) >= 0; ++k)
+    if (v->post_helpers[k & 1]) {
+      const int rc = svc_launch_helpers(v, k, v->post_helpers[k & 1]);
+      if (rc) return rc;
+    }
   return PN_OK;
 }
 
-// post k (one of the last two) is complete once every wave it ran on stored k (or later) to its done word
+// post k (one of the last two) is complete once every done word it completes through holds k (or later): one per
+// wave it ran on, or word 0 alone for a post on more than kDoneWords waves
 bool svc_post_done(const pn_service* v, uint32_t k) {
-  const uint32_t act = v->post_act[k & 1];
-  for (uint32_t w = 0; w < act; ++w)
+  const uint32_t words = v->post_words[k & 1];
+  for (uint32_t w = 0; w < words; ++w)
     if ((int32_t)(__atomic_load_n(v->words + w, __ATOMIC_ACQUIRE) - k) < 0) return false;
   return true;
 }
@@ -302,37 +416,74 @@ uint32_t svc_done(const pn_service* v) {
 bool svc_exited(const pn_service* v) { return __atomic_load_n(v->words + kExitWord, __ATOMIC_ACQUIRE) == v->epoch; }
 
 void svc_free(pn_service* v) {
+  if (v->ctx) {
+    auto& l = v->ctx->services;
+    l.erase(std::remove(l.begin(), l.end(), v), l.end());
+  }
   if (v->mail) (void)hipHostFree(v->mail);
   if (v->words) (void)hipHostFree(v->words);
   if (v->dev) (void)hipFree(v->dev);
   if (v->stream) (void)hipStreamDestroy(v->stream);
+  if (v->helper_stream) (void)hipStreamDestroy(v->helper_stream);
   delete v;
 }
 } // namespace
 
+// pn_set_conn_table is about to overwrite (or free) table buffer `buf`: every post of the ctx's services that captured
+// it must be complete first.  Only one of the last two posts can still be running; an older one is done by
+// construction (post k was issued only once post k - 2 was).
+int pn_internal::svc_release_table(pn_ctx* ctx, int buf) {
+  for (pn_service* v : ctx->services) {
+    if (!v->tbl_used[buf]) continue;
+    const uint32_t id = v->tbl_post[buf];
+    if ((int32_t)(v->seq - id) < 2 && !svc_post_done(v, id)) {
+      const int rc = pn_service_wait(v, id);
+      if (rc) return rc;
+    }
+    v->tbl_used[buf] = false;
+  }
+  return PN_OK;
+}
+
 extern "C" {
 
 int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, pn_service** out) {
+  return pn_service_open_ex(ctx, slot_stride, frame_off, idle_ms, 0, out);
+}
+
+int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, uint32_t large_waves,
+                       pn_service** out) {
   if (!ctx || !out) return set_err(ctx, PN_EINVAL, "pn_service_open: ctx / out is NULL");
   *out = nullptr;
   if ((slot_stride & 15) || slot_stride > 65536 || (frame_off & 1) || slot_stride < frame_off + 96)
     return set_err(ctx, PN_EINVAL, "pn_service_open: slot_stride/frame_off violate the layout contract");
   if (idle_ms == 0 || idle_ms > 10000) return set_err(ctx, PN_EINVAL, "pn_service_open: idle_ms must be in [1, 10000]");
+  if (large_waves && (large_waves < PN_SERVICE_WAVES || large_waves > PN_SERVICE_MAX_WAVES))
+    return set_err(ctx, PN_EINVAL, "pn_service_open: large_waves must be 0 or in [PN_SERVICE_WAVES, PN_SERVICE_MAX_WAVES]");
   hipError_t e = hipSetDevice(ctx->device);
   if (e != hipSuccess) return hip_err(ctx, e, "hipSetDevice");
   int khz = 0;
   e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device);
   if (e != hipSuccess || khz <= 0) return hip_err(ctx, e, "pn_service_open: wall clock rate");
+  int cus = 0;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+  if (e != hipSuccess || cus <= 0) return hip_err(ctx, e, "pn_service_open: CU count");
   pn_service* v = new pn_service();
   v->ctx = ctx;
   v->stride = slot_stride;
   v->frame_off = frame_off;
-  v->waves = PN_SERVICE_WAVES;
+  // a large post: the latency tier plus helpers, enough waves to stream it at pn_classify's rate
+  const uint32_t total = large_waves ? large_waves
+                                     : std::max<uint32_t>(kLatWaves, std::min<uint32_t>(PN_SERVICE_MAX_WAVES,
+                                                                                      (uint32_t)cus * PN_SERVICE_WAVES_PER_CU));
+  v->helpers_max = total - kLatWaves;
   v->idle_ticks = (uint64_t)khz * idle_ms;
+  v->post_ticks = (uint64_t)khz * kPostLimitMs;
   // the cooperative window needs a 16-B chunk before it inside the slot (frame_off >= 2); the frames' 16-B
   // alignment is checked per post
   v->coop = (slot_stride % 16) == 0 && ((frame_off + 14) & ~15u) >= 16;
   if ((e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking)) != hipSuccess ||
+      (e = hipStreamCreateWithFlags(&v->helper_stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void**)&v->mail, 2 * sizeof(SvcPost), hipHostMallocDefault)) != hipSuccess ||
       (e = hipHostMalloc((void**)&v->words, kWordsBytes, hipHostMallocDefault)) != hipSuccess ||
       (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess) {
@@ -347,6 +498,7 @@ int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint3
     svc_free(v);
     return rc;
   }
+  ctx->services.push_back(v);
   *out = v;
   return PN_OK;
 }
@@ -380,8 +532,18 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   p->tbl = ctx->tbl_dev;
   p->mask = ctx->mask;
   p->n_entries = ctx->n_entries;
-  p->fpw = svc_fpw(n, v->waves, p->verify != 0);
-  v->post_act[k & 1] = svc_active(n, p->fpw, v->waves);
+  const uint32_t fpw = svc_fpw(n, p->verify != 0), helpers = svc_helpers(n, v->helpers_max);
+  p->fpw = fpw | helpers << 8;
+  const uint32_t act = svc_active(n, fpw, kLatWaves + helpers);
+  // a large post's helpers first (they wait for wave 0 to publish it): should the launch fail, nothing was posted
+  if (helpers) {
+    const int rc = svc_launch_helpers(v, k, helpers);
+    if (rc) return rc;
+  }
+  v->post_helpers[k & 1] = helpers;
+  v->post_words[k & 1] = act <= kDoneWords ? act : 1u;
+  v->tbl_post[ctx->cur] = k; // pn_set_conn_table waits for this post before it reuses the buffer
+  v->tbl_used[ctx->cur] = true;
   p->check = svc_check(p, k);
   __atomic_store_n(&p->gen, k, __ATOMIC_RELEASE);
   __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
@@ -422,20 +584,21 @@ int pn_service_wait(pn_service* v, uint32_t post_id) {
 int pn_service_close(pn_service* v) {
   if (!v) return PN_OK;
   pn_ctx* ctx = v->ctx;
-  int rc = PN_OK;
+  // the outstanding posts first (a launch that ended before it took them is relaunched), then the stop
+  int rc = svc_post_done(v, v->seq) ? PN_OK : pn_service_wait(v, 0);
   if (v->running && !svc_exited(v)) {
-    // wait for the outstanding posts, then post the stop
-    if (!svc_post_done(v, v->seq)) rc = pn_service_wait(v, 0);
     const uint32_t k = v->seq + 1;
     SvcPost* p = v->mail + (k & 1);
     p->n = PN_SERVICE_STOP;
-    v->post_act[k & 1] = 0;
+    v->post_words[k & 1] = 0;
+    v->post_helpers[k & 1] = 0;
     p->check = svc_check(p, k);
     __atomic_store_n(&p->gen, k, __ATOMIC_RELEASE);
     __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
     v->seq = k;
   }
-  const hipError_t e = hipStreamSynchronize(v->stream); // the kernel ends at the stop or its idle limit
+  hipError_t e = hipStreamSynchronize(v->stream); // the kernel ends at the stop or its idle limit
+  if (e == hipSuccess) e = hipStreamSynchronize(v->helper_stream); // helpers end on the stop
   if (e != hipSuccess && rc == PN_OK) rc = hip_err(ctx, e, "pn_service_close");
   svc_free(v);
   return rc;

@@ -122,10 +122,13 @@ _pn_sync = _sig("pn_sync", _i32, _vp)
 _pn_set_verify = _sig("pn_set_verify", _i32, _vp, _i32)
 _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _vp, _u32, _vp, _vp)
 _pn_service_open = _sig("pn_service_open", _i32, _vp, _u32, _u32, _u32, _c.POINTER(_vp))
+_pn_service_open_ex = _sig("pn_service_open_ex", _i32, _vp, _u32, _u32, _u32, _u32, _c.POINTER(_vp))
 _pn_service_post = _sig("pn_service_post", _i32, _vp, _vp, _u32, _vp, _vp)
 _pn_service_wait = _sig("pn_service_wait", _i32, _vp, _u32)
 _pn_service_close = _sig("pn_service_close", _i32, _vp)
 PN_SERVICE_WAVES = 64
+PN_SERVICE_WAVES_PER_CU = 8
+PN_SERVICE_MAX_WAVES = 4096
 PN_SERVICE_MAX_FRAMES = 1 << 20
 
 # The seeded workload generator lives in its own library (include/pollnet_amd_gen.h), outside
@@ -397,22 +400,32 @@ def wire_bytes(slots: np.ndarray, slot_stride: int, frame_off: int, n: int) -> i
 
 class RxService:
     """The resident classify service (pn_service_*): one launch, then batches posted through pinned host memory
-    and classified by the kernel already on the GPU.  Frames / results: pinned host or device memory."""
+    and classified by the kernel already on the GPU.  Frames / results: pinned host or device memory.
+    large_waves: a large post's wave count (pn_service_open_ex; 0 = the default, PN_SERVICE_WAVES_PER_CU per CU).
+    Each post's frames and results objects are held until the post is waited for (or the service closed): the
+    kernel reads and writes them until then."""
 
-    def __init__(self, ctx: RxContext, slot_stride: int, frame_off: int, idle_ms: int = 200):
+    def __init__(self, ctx: RxContext, slot_stride: int, frame_off: int, idle_ms: int = 200, large_waves: int = 0):
         h = _vp()
-        _check(_pn_service_open(ctx._h, slot_stride, frame_off, idle_ms, _c.byref(h)), ctx._h, "pn_service_open")
+        _check(_pn_service_open_ex(ctx._h, slot_stride, frame_off, idle_ms, large_waves, _c.byref(h)), ctx._h,
+               "pn_service_open")
         self._h, self._ctx = h, ctx
+        self._inflight = {}  # post id -> (frames, results): alive until the post completes
 
     def post(self, frames, n: int, results) -> int:
         """Non-blocking; returns the post's id (posts complete in order)."""
         pid = _u32(0)
         _check(_pn_service_post(self._h, _ptr(frames), n, _ptr(results), _c.byref(pid)), self._ctx._h, "pn_service_post")
+        self._inflight[pid.value] = (frames, results)
         return pid.value
 
     def wait(self, post_id: int = 0):
         """Until post post_id's records are visible (0: the last post)."""
         _check(_pn_service_wait(self._h, post_id), self._ctx._h, "pn_service_wait")
+        # posts complete in order: every post up to the one waited for is done
+        last = post_id or max(self._inflight, default=0)
+        for k in [k for k in self._inflight if ((last - k) & 0xFFFFFFFF) < 0x80000000]:
+            del self._inflight[k]
 
     def classify(self, frames, n: int, results):
         self.post(frames, n, results)
@@ -421,7 +434,10 @@ class RxService:
     def close(self):
         if getattr(self, "_h", None):
             h, self._h = self._h, None
-            _check(_pn_service_close(h), self._ctx._h, "pn_service_close")
+            try:
+                _check(_pn_service_close(h), self._ctx._h, "pn_service_close")
+            finally:
+                self._inflight.clear()
 
     def __del__(self):
         try:

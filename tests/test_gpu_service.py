@@ -286,3 +286,232 @@ def test_service_max_post_equals_pn_classify(torch, cfg):
             svc.close()
     finally:
         ctx.close()
+
+
+# ---- round 6: the conn-table contract with posts outstanding, the post limit, large posts ----
+
+@pytest.fixture(scope="module")
+def big(torch):
+    """1 Mi C3 frames in pinned host memory (zero copy: a verified post of them runs for tens of ms over PCIe)."""
+    n = 1 << 20
+    p = pa.rx.GenParams.for_config(3)
+    host = _pinned(torch, np.zeros((n, STRIDE), np.uint8))
+    pa.gen_frames(p, n, STRIDE, FRAME_OFF, first_index=0, threads=16, out=host.numpy().reshape(n, STRIDE))
+    return p, host, n
+
+
+def _flow_key(s, i):
+    return int(pa.conn_hash_key(int(s[i, FRAME_OFF + 26:FRAME_OFF + 30].view("<u4")[0]),
+                                int(s[i, FRAME_OFF + 34:FRAME_OFF + 36].view("<u2")[0])))
+
+
+def test_service_table_changes_during_a_large_post(torch, big):
+    """pn_set_conn_table during outstanding 1-Mi posts: two changes during one post (the second lands on the buffer
+    the post reads: it waits for the post), then three changes during two posts, the last one growing n_entries (a
+    new, larger buffer: the old one is freed only once the post reading it is done).  Every post's records equal the
+    oracle's under the table it was posted with (rx_service.hip svc_release_table; Core.h:178-182, 558-682)."""
+    p, host, n = big
+    s = host.numpy().reshape(n, STRIDE)
+    t0 = pa.gen_conn_table(p)
+    tables = [t0]
+    for i in (0, 1, 2):  # each drops a different flow: every change is visible throughout the batch
+        t = pa.gen_conn_table(p, max_tw_cnt=4 * p.max_conn_cnt) if i == 2 else pa.gen_conn_table(p)
+        t.delete(_flow_key(s, 1 + 7 * i))
+        tables.append(t)
+    assert len(tables[3].snapshot()[0]) > len(t0.snapshot()[0])  # the last change grows n_entries
+    exp = {i: _expected(s, n, t) for i, t in enumerate(tables)}
+    for i in range(1, 4):
+        assert not np.array_equal(exp[i], exp[0])
+    res = [torch.zeros(n * 16, dtype=torch.uint8).pin_memory() for _ in range(3)]
+    got = lambda r: r.numpy().view(pa.RESULT_DTYPE)
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(t0)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            # two changes during one post: T1 into the other buffer, T2 back into the post's own
+            a = svc.post(host, n, res[0])
+            ctx.set_conn_table(tables[1])
+            ctx.set_conn_table(tables[2])
+            b = svc.post(host, n, res[1])
+            svc.wait(a)
+            svc.wait(b)
+            assert np.array_equal(got(res[0]), exp[0])
+            assert np.array_equal(got(res[1]), exp[2])
+            # three changes during two posts, the last one growing n_entries
+            ctx.set_conn_table(t0)
+            a = svc.post(host, n, res[0])           # T0
+            ctx.set_conn_table(tables[1])
+            b = svc.post(host, n, res[1])           # T1, two outstanding
+            ctx.set_conn_table(tables[2])           # over T0's buffer: waits for a
+            ctx.set_conn_table(tables[3])           # over T1's buffer, reallocated larger: waits for b
+            svc.wait(a)
+            c = svc.post(host, n, res[2])           # T3
+            svc.wait(b)
+            svc.wait(c)
+            assert np.array_equal(got(res[0]), exp[0])
+            assert np.array_equal(got(res[1]), exp[1])
+            assert np.array_equal(got(res[2]), exp[3])
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+def test_service_third_post_refused(torch, big):
+    """At most two posts outstanding: with two verified 1-Mi posts from pinned host memory in flight (tens of ms of
+    PCIe reads each) a third is refused at once, and the two complete with the oracle's records."""
+    p, host, n = big
+    s = host.numpy().reshape(n, STRIDE)
+    table = pa.gen_conn_table(p)
+    exp = _expected(s, n, table)
+    res = [torch.zeros(n * 16, dtype=torch.uint8).pin_memory() for _ in range(3)]
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            a = svc.post(host, n, res[0])
+            b = svc.post(host, n, res[1])
+            with pytest.raises(pa.PollnetError, match="two posts already outstanding"):
+                svc.post(host, n, res[2])
+            svc.wait(b)
+            assert svc.wait(a) is None  # an id of a completed post returns at once
+            for r in res[:2]:
+                assert np.array_equal(r.numpy().view(pa.RESULT_DTYPE), exp)
+            c = svc.post(host, 4096, res[2])  # both done: posting works again
+            svc.wait(c)
+            assert np.array_equal(res[2].numpy()[: 4096 * 16].view(pa.RESULT_DTYPE), exp[:4096])
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+def test_service_large_post_late_in_the_idle_window(torch, big):
+    """idle_ms = 1: a post arriving ~0.9 ms into the idle window that runs longer than the idle limit (a verified
+    64 Ki-frame post from pinned host memory, ~2 ms) completes -- a post's limit runs from its acceptance, not from
+    the last post -- and the next post after it completes too (the advisor's round-5 finding)."""
+    p, host, n = big
+    s = host.numpy().reshape(n, STRIDE)
+    table = pa.gen_conn_table(p)
+    m = 1 << 16
+    exp = _expected(s[:m], m, table)
+    res = torch.zeros(m * 16, dtype=torch.uint8).pin_memory()
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=1)
+        try:
+            for rep in range(6):
+                svc.classify(host, 64, res)  # the kernel is running, its idle timer just restarted
+                t = time.perf_counter()
+                while time.perf_counter() - t < 0.0009:
+                    pass
+                res.zero_()
+                svc.classify(host, m, res)
+                assert np.array_equal(res.numpy().view(pa.RESULT_DTYPE), exp), rep
+                res.zero_()
+                svc.classify(host, 4096, res)
+                assert np.array_equal(res.numpy()[: 4096 * 16].view(pa.RESULT_DTYPE), exp[:4096]), rep
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("large_waves", [64, 96, 0])
+def test_service_large_posts_with_helpers(torch, big, large_waves):
+    """Posts above the latency tier's 4096 frames run on helper waves launched with them (pn_service_open_ex:
+    large_waves 64 = the tier alone, 96 = 32 helpers, 0 = the default per-CU count): sizes around every boundary,
+    both paths, device-resident and zero copy, two outstanding; records equal the oracle's."""
+    p, host, n = big
+    s = host.numpy().reshape(n, STRIDE)
+    table = pa.gen_conn_table(p)
+    m = 200_000
+    exp = {True: _expected(s[:m], m, table), False: _expected(s[:m], m, table, verify=False)}
+    dev = host[: m * STRIDE].cuda()
+    outs = [torch.zeros(m * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, large_waves=large_waves)
+        try:
+            k = 0
+            for size in (4096, 4097, 4160, 4161, 8192, 65 * 64 * 33 + 5, 131072, m):
+                for verify in (True, False):
+                    for src in (host, dev):
+                        ctx.set_verify(verify)
+                        o = outs[k & 1]
+                        o.zero_()
+                        pid = svc.post(src, size, o)
+                        svc.wait(pid)
+                        got = o.numpy()[: size * 16].view(pa.RESULT_DTYPE)
+                        assert np.array_equal(got, exp[verify][:size]), (size, verify, src.is_cuda)
+                        assert not o.numpy()[size * 16:].any(), "records written past n"
+                        k += 1
+            # two large posts outstanding, then a small one behind them
+            ctx.set_verify(True)
+            a = svc.post(host, m, outs[0])
+            b = svc.post(dev, m, outs[1])
+            svc.wait(a)
+            small = torch.zeros(64 * 16, dtype=torch.uint8).pin_memory()
+            c = svc.post(host, 64, small)
+            svc.wait(c)
+            svc.wait(b)
+            for o in outs:
+                assert np.array_equal(o.numpy().view(pa.RESULT_DTYPE), exp[True])
+            assert np.array_equal(small.numpy().view(pa.RESULT_DTYPE), exp[True][:64])
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
+
+
+def test_service_soak_large_posts_and_relaunches(torch, big):
+    """300 posts of random size up to 40,000 frames (helpers above 4096) with idle gaps past idle_ms (2 ms), so
+    launches end and are relaunched with large posts pending (their helpers relaunched with them): every post's
+    records equal the oracle's."""
+    rng = np.random.default_rng(0x6A11)
+    p, host, n = big
+    N = 1 << 17
+    s = host.numpy().reshape(n, STRIDE)
+    table = pa.gen_conn_table(p)
+    exp = {True: _expected(s[:N], N, table), False: _expected(s[:N], N, table, verify=False)}
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=2)
+        try:
+            outs = [torch.zeros(40000 * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+            pending = []
+
+            def check(item):
+                pid, o, first, size, verify = item
+                svc.wait(pid)
+                got = outs[o].numpy()[: size * 16].view(pa.RESULT_DTYPE)
+                assert np.array_equal(got, exp[verify][first:first + size]), (pid, first, size, verify)
+
+            gaps = 0
+            for k in range(300):
+                if len(pending) == 2 or (pending and rng.random() < 0.5):
+                    check(pending.pop(0))
+                verify = bool(rng.random() < 0.5)
+                ctx.set_verify(verify)
+                size = int(rng.integers(1, 40001)) if rng.random() < 0.7 else int(rng.integers(1, 4097))
+                first = int(rng.integers(0, N - size + 1))
+                o = k & 1
+                if pending and pending[0][1] == o:
+                    check(pending.pop(0))
+                pid = svc.post(host[first * STRIDE:], size, outs[o])
+                pending.append((pid, o, first, size, verify))
+                if rng.random() < 0.1:
+                    time.sleep(float(rng.uniform(0.001, 0.006)))
+                    gaps += 1
+            while pending:
+                check(pending.pop(0))
+            assert gaps > 10
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
