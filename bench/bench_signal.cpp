@@ -58,6 +58,8 @@ int main(int argc, char** argv) {
   uint32_t token = 0;
   pn_service* svc = nullptr;
   if (pn_service_open(ctx, stride, off, 2000, &svc)) return std::fprintf(stderr, "%s\n", pn_last_error(ctx)), 4;
+  uint16_t* h_links = nullptr; // the chain links of a linked post (pn_service_post_linked)
+  if (hipHostMalloc((void**)&h_links, 2 * 1024, hipHostMallocDefault) != hipSuccess) return 3;
   bool ok = true;
   std::string out = "{\"bench\": \"completion_word_vs_stream_sync\", \"frames\": \"C2 1514-B\"";
   // both checksums verified, then the release path (pn_set_verify(ctx, 0): header lines only)
@@ -75,6 +77,9 @@ int main(int argc, char** argv) {
       return pollnet_amd::wait_word(flag, tok, s) == nullptr;
     };
     auto service_once = [&](uint32_t n) { return pn_service_post(svc, fr, n, rec, nullptr) == 0 && pn_service_wait(svc, 0) == 0; };
+    auto linked_once = [&](uint32_t n) {
+      return pn_service_post_linked(svc, fr, n, rec, h_links, nullptr) == 0 && pn_service_wait(svc, 0) == 0;
+    };
     std::string legs;
     for (uint32_t n : {64u, 512u, 1024u}) {
       // records equal: the signalled batch's records (zero-copy: read right after the word) vs sync's
@@ -108,8 +113,8 @@ int main(int argc, char** argv) {
         same_svc = std::memcmp(tmp.data(), h_rec2, 16 * n) == 0;
       }
       ok = ok && same_svc;
-      std::vector<double> ts, tg, tv;
-      for (int w = 0; w < 20; w++) ok = ok && sync_once(n) && signal_once(n) && service_once(n);
+      std::vector<double> ts, tg, tv, tl;
+      for (int w = 0; w < 20; w++) ok = ok && sync_once(n) && signal_once(n) && service_once(n) && linked_once(n);
       ok = ok && hipStreamSynchronize(s) == hipSuccess;
       for (uint32_t r = 0; r < reps && ok; r++) {
         auto t0 = Clock::now();
@@ -121,15 +126,20 @@ int main(int argc, char** argv) {
         auto t3 = Clock::now();
         ok = ok && service_once(n);
         auto t4 = Clock::now();
+        ok = ok && linked_once(n);
+        auto t5 = Clock::now();
+        tl.push_back(std::chrono::duration<double, std::micro>(t5 - t4).count());
         ts.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
         tg.push_back(std::chrono::duration<double, std::micro>(t2 - t1).count());
         tv.push_back(std::chrono::duration<double, std::micro>(t4 - t3).count());
       }
       if (!ok) break;
-      char buf[320];
+      char buf[384];
       std::snprintf(buf, sizeof buf,
-                    "%s\"%u\": {\"sync_us\": %.2f, \"signal_us\": %.2f, \"service_us\": %.2f, \"records_equal\": %s}",
-                    legs.empty() ? "" : ", ", n, median(ts), median(tg), median(tv), same && same_svc ? "true" : "false");
+                    "%s\"%u\": {\"sync_us\": %.2f, \"signal_us\": %.2f, \"service_us\": %.2f, \"service_linked_us\": %.2f, "
+                    "\"records_equal\": %s}",
+                    legs.empty() ? "" : ", ", n, median(ts), median(tg), median(tv), median(tl),
+                    same && same_svc ? "true" : "false");
       legs += buf;
     }
     out += std::string(", \"") + (zc ? "zero_copy" : "resident") + (verify ? "" : "_release_path") + "\": {" + legs + "}";
@@ -138,6 +148,7 @@ int main(int argc, char** argv) {
   std::printf("%s\n", out.c_str());
   (void)hipStreamSynchronize(s);
   if (pn_service_close(svc)) ok = false;
+  (void)hipHostFree(h_links);
   pn_close(ctx);
   return ok ? 0 : 1;
 }

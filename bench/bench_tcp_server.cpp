@@ -351,7 +351,8 @@ struct TimedOracleBackend : OracleBackend {
   }
 };
 
-template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false, bool kEcho = false>
+template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false, bool kEcho = false,
+          bool kLinks = false>
 struct Conf {
   static const uint32_t RecvBufSize = 65536;
   static const uint32_t MaxConns = 1024;
@@ -365,12 +366,14 @@ struct Conf {
   static const uint32_t RxChunk = kChunk;
   static const bool RxPipeline = kPipe;
   static const bool RxResident = kResident;
+  static const bool RxLinks = kLinks; // with RxResident: the chain links and the in-order fast path
   struct UserData {};
 };
 
 struct Run {
   double mfps = 0, us_poll = 0, acks_per_frame = 0, fill_share = 0, classify_share = 0, tx_share = 0;
   double ns_classify = -1, ns_dispatch = -1; // TimedOracleBackend: per frame, in launch() / collect()
+  double in_order_share = -1;                 // frames through the in-order fast path (chain links), of all
   double echo_gbps = -1;                      // echo workload: payload bits the server sent back per second
   bool ok = false;
   std::string err;
@@ -379,10 +382,10 @@ struct Run {
 // verify = false: the checksum discard off, as the reference's release build runs (no checksum verified);
 // the GPU backend then classifies from each frame's header lines only (pn_set_verify)
 template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false,
-          bool kEcho = false>
+          bool kEcho = false, bool kLinks = false>
 static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   Run out;
-  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident, kEcho>, BenchLink, Backend>;
+  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident, kEcho, kLinks>, BenchLink, Backend>;
   auto srv = std::make_unique<Server>();
   srv->link().setup(n_flows);
   if (!srv->initWithLink("10.0.0.1", 1234)) {
@@ -425,13 +428,14 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   out.us_poll = t * 1e6 / polls;
   out.acks_per_frame = (double)(link.acks - acks0) / frames;
   out.fill_share = link.fill_s / t;
+  if (kResident && kLinks) out.in_order_share = (double)srv->inOrderFrames() / (double)link.data_frames;
   // the legs on their own, same frames: classify (+ the record walk, no dispatch) and the
   // TX checksum fill of one poll's ACKs
   const uint32_t n = (kBatch / n_flows) * n_flows, acks = (uint32_t)(out.acks_per_frame * n + 0.5);
   auto& be = srv->backend();
   const auto c0 = Clock::now();
   for (uint32_t p = 0; p < polls; p++)
-    if (be.classify(n, srv->table(), [](uint64_t, const pn_result&, const uint8_t*) {})) break;
+    if (be.classify(n, srv->table(), [](uint64_t, const pn_result&, const uint8_t*, uint16_t = 0) {})) break;
   const auto c1 = Clock::now();
   // the TX leg as the engine runs it for a poll's ACKs: header-only frames get their sums as they are built (part
   // of the dispatch), so only a batch for pn_tx_fill (TxGpuMinDataFrames 0) is timed here
@@ -546,22 +550,27 @@ static std::string json(const Run& r) {
                 "\"tx_fill_share\": %.3f}",
                 r.mfps, r.mfps * 1514 * 8 / 1e3, r.us_poll, r.acks_per_frame, r.fill_share,
                 r.fill_share < 1 ? r.mfps / (1 - r.fill_share) : 0.0, r.classify_share, r.tx_share);
+  std::string o(b);
+  if (r.in_order_share >= 0) {
+    o.pop_back();
+    char x[96];
+    std::snprintf(x, sizeof x, ", \"in_order_fast_path_share\": %.3f}", r.in_order_share);
+    o += x;
+  }
   if (r.echo_gbps >= 0) {
-    std::string o(b);
     o.pop_back();
     char x[96];
     std::snprintf(x, sizeof x, ", \"echo_payload_gbit_per_s\": %.2f}", r.echo_gbps);
     return o + x;
   }
   if (r.ns_dispatch >= 0) {
-    std::string o(b);
     o.pop_back();
     char x[160];
     std::snprintf(x, sizeof x, ", \"ns_per_frame_total\": %.2f, \"ns_per_frame_classify\": %.2f, \"ns_per_frame_dispatch\": %.2f}",
                   r.mfps > 0 ? 1e3 / r.mfps : 0.0, r.ns_classify, r.ns_dispatch);
     return o + x;
   }
-  return b;
+  return o;
 }
 
 int main(int argc, char** argv) {
@@ -590,6 +599,9 @@ int main(int argc, char** argv) {
 #endif
   } else if (argc > 3 && std::strcmp(argv[3], "twin_timed") == 0) { // the host dispatch alone (profiling)
     leg("cpu_rxbatch_512_pipelined_release_path_timed", runOne<512, TimedOracleBackend, 0, true>(n_flows, polls, false));
+    // the same with the chain links (the oracle's, as the resident service's linked posts): the in-order fast path
+    leg("cpu_rxbatch_512_pipelined_linked_release_path_timed",
+        runOne<512, TimedOracleBackend, 0, true, true, false, true>(n_flows, polls, false));
   } else if (argc > 3 && std::strcmp(argv[3], "release_pair") == 0) { // one pair on its own (profiling the host side)
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
     leg("cpu_rxbatch_512_pipelined_release_path_timed", runOne<512, TimedOracleBackend, 0, true>(n_flows, polls, false));
@@ -612,6 +624,9 @@ int main(int argc, char** argv) {
       lines += "\"cpus_server_writer\": [" + std::to_string(writer.cpu_server) + ", " + std::to_string(writer.cpu_writer) + "]";
     }
     leg("gpu_rxbatch_512_pipelined_resident_release_path", runOne<512, GpuBackend, 0, true, true>(n_flows, polls, false));
+    // the same with the chain links (Conf::RxLinks): the GPU's chain pass in each post, the in-order fast path
+    leg("gpu_rxbatch_512_pipelined_resident_linked_release_path",
+        runOne<512, GpuBackend, 0, true, true, false, true>(n_flows, polls, false));
 #ifdef PN_BENCH_REF
     leg("reference_server_release_build", runRef(n_flows, polls));
 #endif

@@ -302,6 +302,19 @@ int pn_service_open(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint3
 int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, uint32_t idle_ms, uint32_t large_waves,
                        pn_service** out);
 int pn_service_post(pn_service* svc, const void* frames, uint32_t n, void* results, uint32_t* post_id);
+/* pn_service_post with the post's chain links (round 6): links (host or device memory, n u16, 2-B aligned) gets, per
+ * frame i, d > 0 when frame i - d is the previous frame of the same connection in the post (among records with
+ * PN_F_HIT and not PN_F_TW) and frame i continues it in order: both frames clean (PN_F_ACK, PN_F_IP_OK and PN_F_TCP_OK
+ * or PN_F_TCP_UNCHECKED; no SYN, FIN, RST, NOT_TCP, TRUNC, BADOFF, IHL_NE_5), both with payload, seq_i = seq_j +
+ * payload_len_j, and equal payload_off, ack number, window, destination address and port; else 0.  A host that
+ * processed frame i - d and left the connection untouched since can take frame i's data without re-checking it
+ * against the connection.  Computed on the GPU after the records, in the same post (the links are
+ * visible when pn_service_wait returns); n <= PN_LINK_MAX_FRAMES; with max_conn_cnt > PN_LINK_MAX_CONNS every link
+ * is 0.  The chain's statement: oracle/pn_oracle.c orc_chain_links. */
+#define PN_LINK_MAX_FRAMES 1024u
+#define PN_LINK_MAX_CONNS 4096u
+int pn_service_post_linked(pn_service* svc, const void* frames, uint32_t n, void* results, uint16_t* links,
+                           uint32_t* post_id);
 int pn_service_wait(pn_service* svc, uint32_t post_id);
 int pn_service_close(pn_service* svc);
 

@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
+#include <type_traits>
 
 #include "../pollnet_amd.h"
 
@@ -125,8 +126,10 @@ class GpuRx {
   // the chunk pollBatch() classifies per launch (two chunks are in flight at once).
   // resident (ZeroCopy only): the chunks go to the resident classify service (pn_service_*: one launch, then a post
   // per chunk through pinned memory) instead of a launch each; resident_idle_ms: how long it stays without a post.
+  // links (resident, max_batch <= PN_LINK_MAX_FRAMES): each post also returns its chain links
+  // (pn_service_post_linked), handed to a recv_handler that takes a fifth argument.
   const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, Mode mode = Mode::Copy,
-                   bool resident = false, uint32_t resident_idle_ms = 100) {
+                   bool resident = false, uint32_t resident_idle_ms = 100, bool links = false) {
     destruct();
     if (max_batch == 0) return "max_batch must be > 0";
     if (pn_open(device, &ctx_)) return pn_last_error(nullptr);
@@ -156,8 +159,13 @@ class GpuRx {
       use_word_[b] = false;
       if (hipEventCreateWithFlags(&done_[b], hipEventDisableTiming) != hipSuccess) return "hipEventCreate failed";
     }
+    links_ = links && svc_ && max_batch <= PN_LINK_MAX_FRAMES;
+    for (int b = 0; b < 2 && links_; b++)
+      if (hipHostMalloc((void**)&h_links_[b], sizeof(uint16_t) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
+        return "hipHostMalloc(links) failed";
     return nullptr;
   }
+  bool links() const { return links_; }
 
   // Snapshot the host table to the device (after add/del/enterTW).
   const char* syncTable(const ConnTable& t) {
@@ -202,6 +210,7 @@ class GpuRx {
       if (pn_classify_indexed(ctx_, ring, h_offs_[b], eth_mod16, m, avail, h_res_[b], stream_)) return pn_last_error(ctx_);
       if (hipEventRecord(done_[b], stream_) != hipSuccess) return "hipEventRecord failed";
       use_word_[b] = false;
+      linked_[b] = false;
       return nullptr;
     };
     return run(
@@ -230,7 +239,7 @@ class GpuRx {
       return e;
     }
     auto eth_of = [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; };
-    walk<kHitKey>(h_res_[b], 0, n, table, eth_of, recv_handler, tw_handler);
+    walk<kHitKey>(h_res_[b], linked_[b] ? h_links_[b] : nullptr, 0, n, table, eth_of, recv_handler, tw_handler);
     return nullptr;
   }
 
@@ -269,14 +278,17 @@ class GpuRx {
         if (const char* e = launch_k(k + 1)) return e;
       if (const char* e = wait_done(k & 1)) return e;
       const uint32_t base = k * cap_, m = std::min(cap_, n - base);
-      walk<kHitKey>(h_res_[k & 1], base, m, table, eth_of, recv_handler, tw_handler);
+      walk<kHitKey>(h_res_[k & 1], linked_[k & 1] ? h_links_[k & 1] : nullptr, base, m, table, eth_of, recv_handler, tw_handler);
     }
     return nullptr;
   }
-  // Dispatch records res[0, m) of frames base.. in order.
+  // Dispatch records res[0, m) of frames base.. in order (with their chain links, when the post returned them and
+  // the handler takes them: recv_handler(key, rec, eth, miss_entry_idx, link)).
   template <bool kHitKey, class EthOf, class RecvHandler, class TwHandler>
-  void walk(const pn_result* res, uint32_t base, uint32_t m, const ConnTable& table, EthOf& eth_of,
-            RecvHandler& recv_handler, TwHandler& tw_handler) {
+  void walk(const pn_result* res, const uint16_t* links, uint32_t base, uint32_t m, const ConnTable& table,
+            EthOf& eth_of, RecvHandler& recv_handler, TwHandler& tw_handler) {
+    constexpr bool kTakesLink =
+        std::is_invocable_v<RecvHandler&, uint64_t, const pn_result&, const uint8_t*, uint32_t, uint16_t>;
     for (uint32_t i = 0; i < m; i++) {
       const uint8_t* eth = eth_of(base + i);
       const pn_result& r = res[i];
@@ -286,7 +298,8 @@ class GpuRx {
       } else {
         uint32_t idx = PN_MISS;
         if (!(r.flags & PN_F_HIT)) table.find(key, &idx, nullptr);
-        recv_handler(key, r, eth, idx);
+        if constexpr (kTakesLink) recv_handler(key, r, eth, idx, links ? links[i] : (uint16_t)0);
+        else recv_handler(key, r, eth, idx);
       }
     }
   }
@@ -316,8 +329,11 @@ class GpuRx {
   const char* launch_at(const uint8_t* src, uint32_t m, uint32_t b) {
     use_word_[b] = false;
     post_[b] = 0;
+    linked_[b] = svc_ && links_;
     if (svc_) // resident service: a post, no launch
-      return pn_service_post(svc_, src, m, h_res_[b], &post_[b]) ? pn_last_error(ctx_) : nullptr;
+      return pn_service_post_linked(svc_, src, m, h_res_[b], links_ ? h_links_[b] : nullptr, &post_[b])
+                 ? pn_last_error(ctx_)
+                 : nullptr;
     if (mode_ == Mode::ZeroCopy && m <= PN_NOTIFY_MAX_FRAMES) { // small batch: completion by a pinned word
       tok_[b] = ++next_tok_;
       if (pn_classify_notify(ctx_, src, stride_, off_, m, h_res_[b], stream_, &h_word_[16 * b], tok_[b]))
@@ -348,6 +364,8 @@ class GpuRx {
       if (h_res_[b]) (void)hipHostFree(h_res_[b]);
       if (h_offs_[b]) (void)hipHostFree(h_offs_[b]);
       h_offs_[b] = nullptr;
+      if (h_links_[b]) (void)hipHostFree(h_links_[b]);
+      h_links_[b] = nullptr;
       if (d_res_[b]) (void)hipFree(d_res_[b]);
       if (d_frames_[b]) (void)hipFree(d_frames_[b]);
       done_[b] = nullptr;
@@ -375,6 +393,8 @@ class GpuRx {
   uint32_t tok_[2] = {0, 0}, next_tok_ = 0;
   bool use_word_[2] = {false, false};
   pn_service* svc_ = nullptr;       // resident classify service (ZeroCopy, init's `resident`)
+  uint16_t* h_links_[2] = {nullptr, nullptr}; // pinned: each buffer's chain links (init's `links`)
+  bool links_ = false, linked_[2] = {false, false}; // links on; buffer b's batch came with them
   uint32_t post_[2] = {0, 0};       // buffer b's outstanding service post (0: none)
   uint32_t stride_ = 0, off_ = 0, cap_ = 0, max_conn_ = 0;
 };

@@ -39,6 +39,12 @@
 
 #include "../pollnet_amd.h"
 
+// The per-segment path is a handful of small steps called once per frame; forced inline, it is one straight run
+// of code per frame (the host dispatch).
+#ifndef PN_HOT
+#define PN_HOT __attribute__((always_inline))
+#endif
+
 namespace pollnet_amd {
 
 namespace detail {
@@ -117,10 +123,41 @@ class RxConn {
   uint32_t recentTs() const { return recent_ts_; }
   uint32_t lastAckSeq() const { return last_ack_seq_; } // the ack number last sent (updateLastAck)
 
+  // The in-order fast path's state test (TcpEngine::inOrder): a segment of len > 0 payload bytes starting at seq is
+  // exactly the next in-order data with nothing held, no hole, no FIN, no timestamps, and fits the buffer -- the case
+  // onSegment hands to onData zero-copy without touching its extent list.
+  bool inOrderReady(uint32_t seq, uint32_t len) const {
+    return !closed_ && !fin_received_ && !hasTs() && n_segs_ == 1 && segs_[0].first == segs_[0].second &&
+           seq == recv_buf_seq_ + segs_[0].second && len - 1 < kBufSize - segs_[0].second;
+  }
+  // onSegment for a segment that passed inOrderReady and whose ACK field changes nothing (the caller's proof): steps
+  // 7 and the ACK policy only, as onSegment runs them for it (TcpConn.h:700-764).
+  template <class Handler>
+  PN_HOT RxAck onInOrder(Handler& h, const uint8_t* data, uint32_t n) {
+    RxAck out;
+    pending_ack_ = true;
+    segs_[0].second += n;
+    const uint32_t left = h.onData(*this, data, n);
+    segs_[0].first = segs_[0].second - left;
+    if (left) std::memcpy(recv_buf_ + segs_[0].first, data + n - left, left);
+    slide();
+    if (segs_[0].second == kBufSize) { // full of unconsumed data: cannot proceed
+      h.onReset(*this);
+      out.rst = true;
+      close();
+      return out;
+    }
+    if (pending_ack_) { // (a reply onData sent carried the ACK: ackSent() cleared it)
+      out.send = true;
+      out.immediate = ackSeq() - last_ack_seq_ >= 2 * rmss();
+    }
+    return out;
+  }
+
   // One classified segment of this connection.  eth: the frame (host memory);
   // rec: its pn_result.
   template <class Handler>
-  RxAck onSegment(Handler& h, const uint8_t* eth, const pn_result& rec) {
+  PN_HOT RxAck onSegment(Handler& h, const uint8_t* eth, const pn_result& rec) {
     RxAck out;
     if (closed_) return out;
     const bool fin = rec.flags & PN_F_FIN, rst = rec.flags & PN_F_RST;
@@ -174,7 +211,8 @@ class RxConn {
         pending_ack_ = true;
         if (n_segs_ > 1) immediate = true; // a hole existed
         uint32_t i = 0;
-        if (merge(loc, loc_end, &i)) immediate = true; // a new hole was opened
+        if (n_segs_ == 1 && loc == segs_[0].second) segs_[0].second = loc_end; // in order, no hole: merge's result
+        else if (merge(loc, loc_end, &i)) immediate = true;                   // a new hole was opened
         if (segs_[0].second != loc_end) fin_ok = false;
         if (segs_[0].first == loc && segs_[0].second == loc_end) {
           // exactly the next bytes and nothing pending: hand over the frame's own bytes
@@ -268,7 +306,7 @@ class RxConn {
   // Advance the window once at least one RMSS was consumed (receiver-side SWS
   // avoidance, TcpConn.h:726-740): rebase to 0 when nothing is held, else shift the
   // held bytes down once half the buffer is consumed.
-  void slide() {
+  PN_HOT void slide() {
     const uint32_t consumed = segs_[0].first;
     if (consumed < rmss()) return;
     if (consumed == segs_[n_segs_ - 1].second) {

@@ -81,6 +81,11 @@ PN_CONF_OPT(RxPipeline, bool, false)        // throughput mode: a poll's frames 
                                             // previous poll's are dispatched (one poll of added latency)
 PN_CONF_OPT(RxResident, bool, false)        // the classify runs in the resident service (pn_service_*): a post
                                             // per poll through pinned memory instead of a launch
+PN_CONF_OPT(RxLinks, bool, false)           // with RxResident: each post also returns its chain links
+                                            // (pn_service_post_linked) and a frame that continues its connection's
+                                            // previous one takes the in-order fast path.  Off by default: the GPU's
+                                            // chain pass lengthens a 512-frame post more than the fast path saves
+                                            // on the host
 PN_CONF_OPT(DelayedAckMS, uint32_t, 10)     // EfviTcp.h:189
 PN_CONF_OPT(Device, int, 0)
 PN_CONF_OPT(ReferenceLiteralTable, bool, false) // PN_TABLE_REFERENCE_LITERAL: the reference's rehash, defect kept
@@ -367,14 +372,16 @@ class GpuBackend {
   // GPU while the host dispatches the current one; 0 = one launch per poll).  rx_halves = 2:
   // two RX rings of rx_cap slots for launch/collect (one in flight while the other fills).
   // tx_halves = 2: two TX batches (one filled on the GPU while the other is built).
+  // links (with resident): the service returns each post's chain links, passed to f as a fourth argument
   const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1,
-                   uint32_t tx_halves = 1, bool resident = false) {
+                   uint32_t tx_halves = 1, bool resident = false, bool links = false) {
     drain();
     if (rx_ring_) (void)hipHostFree(rx_ring_);
     if (tx_ring_) (void)hipHostFree(tx_ring_);
     rx_ring_ = tx_ring_ = nullptr;
     const uint32_t chunk = rx_chunk && rx_chunk < rx_cap ? rx_chunk : rx_cap;
-    if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy, resident)) return e;
+    if (const char* e = rx_.init(device, kStride, kFrameOff, chunk, GpuRx::Mode::ZeroCopy, resident, 100, links))
+      return e;
     if (pn_set_verify(rx_.ctx(), verify_ ? 1 : 0)) return pn_last_error(rx_.ctx());
     // the TX fill has a stream of its own: pipelined, it runs beside the next batch's classify
     if (!tx_stream_ && hipStreamCreateWithFlags(&tx_stream_, hipStreamNonBlocking) != hipSuccess)
@@ -403,22 +410,25 @@ class GpuBackend {
     return nullptr;
   }
   // Pipelined RX: launch classifies the first n slots of one half against the snapshot on the
-  // device (syncTable); collect waits for it and calls f(key, rec, eth) in ring order.
+  // device (syncTable); collect waits for it and calls f(key, rec, eth, link) in ring order (link: the frame's chain
+  // link, 0 without links).
   const char* launch(uint32_t half, uint32_t n, const ConnTable&) { return rx_.submit(rxSlots(half), n, half); }
   template <class F>
   const char* collect(uint32_t half, uint32_t n, const ConnTable& t, F&& f) {
     return rx_.template complete<false>(
-        rxSlots(half), n, half, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
-        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
+        rxSlots(half), n, half, t,
+        [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t, uint16_t link) { f(key, r, eth, link); },
+        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth, (uint16_t)0); });
   }
   uint8_t* txSlots(uint32_t half = 0) { return tx_ring_ + (size_t)half * tx_cap_ * kStride; }
   const char* syncTable(const ConnTable& t) { return rx_.syncTable(t); }
-  // f(key, rec, eth) for the n frames of the RX ring, in ring order.
+  // f(key, rec, eth, link) for the n frames of the RX ring, in ring order.
   template <class F>
   const char* classify(uint32_t n, const ConnTable& t, F&& f) {
     return rx_.template pollBatch<false>(
-        rx_ring_, n, t, [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t) { f(key, r, eth); },
-        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth); });
+        rx_ring_, n, t,
+        [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint32_t, uint16_t link) { f(key, r, eth, link); },
+        [&](uint64_t key, uint32_t, const uint8_t* eth, const pn_result& r) { f(key, r, eth, (uint16_t)0); });
   }
   // IP + TCP checksums of the first n slots of a TX batch (PN_TX_TCP: SendBuf::setOptDataLen,
   // Core.h:157-163).  fillTx waits for them; fillTxLaunch / fillTxWait split the same call
@@ -622,6 +632,8 @@ class TcpEngine {
     std::unique_ptr<uint8_t[]> data_;
     uint32_t send_una_ = 0, send_next_ = 0, data_next_ = 0, data_next_size_ = 0, recover_ = 0;
     uint32_t next_seq_ = 0; // seg(send_next_).seq, kept here so that an ACK reads no segment entry
+    uint64_t ack_frame_ = ~0ull; // frame_idx_ of the last frame whose ACK field this connection processed (inOrder)
+    uint32_t ack_in_ = 0;        // that frame's ack number
     uint32_t smss_ = 536, send_wnd_seq_ = 0, rto_ = 1000, srtt_ = 0, rttvar_ = 0, dup_ack_cnt_ = 0, retries_ = 0;
     bool established_ = false, fin_sent_ = true, fin_received_ = true, fast_re_ = false, in_recover_ = false;
     TimerNode timers_[4]; // resend, delayed ACK, user 0 (send timeout), user 1 (recv timeout)
@@ -638,6 +650,8 @@ class TcpEngine {
   Backend& backend() { return be_; } // measurement: the per-frame legs timed on their own
   // Records re-resolved on the host because the table changed after their snapshot.
   uint64_t reResolved() const { return re_resolved_; }
+  // Frames that took the in-order fast path on their chain link (RxLinks).
+  uint64_t inOrderFrames() const { return in_order_; }
   // Drop checksum-failed frames before they touch any state (what the NIC's RX checksum
   // offload does for efvitcp: ef_vi delivers them as RX_DISCARD).  Default on.  Off, the frames
   // are trusted as the reference's release build trusts them (Core::checksum is debug-only,
@@ -747,7 +761,8 @@ class TcpEngine {
     std::memcpy(local_mac_, link_.localMac(), 6);
     if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
     if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1,
-                                 kRxPipeline ? 2 : 1, srv_detail::opt_RxResident<Conf>::value))
+                                 kRxPipeline ? 2 : 1, srv_detail::opt_RxResident<Conf>::value,
+                                 srv_detail::opt_RxResident<Conf>::value && srv_detail::opt_RxLinks<Conf>::value))
       return e;
     tx_base_[0] = be_.txSlots(0) + Backend::kFrameOff; // each TX batch's first frame
     tx_base_[1] = kRxPipeline ? be_.txSlots(1) + Backend::kFrameOff : tx_base_[0];
@@ -858,7 +873,9 @@ class TcpEngine {
         synced_ver_ = tver_;
       }
     }
-    auto frame = [&](uint64_t key, const pn_result& r, const uint8_t* eth) { onFrame(h, key, r, eth); };
+    auto frame = [&](uint64_t key, const pn_result& r, const uint8_t* eth, uint16_t link = 0) {
+      onFrame(h, key, r, eth, link);
+    };
     if constexpr (kRxPipeline) {
       // launch this poll's frames; send what the previous poll built (its checksum fill ran
       // meanwhile); dispatch the previous poll's frames while this poll's are classified; start
@@ -889,8 +906,11 @@ class TcpEngine {
   // ---- one received frame (Core::pollNet RX branch + the endpoint's recv handler) ----
   // key: the frame's connHashKey, which the backends pass for TIME_WAIT records and misses only (a hit's connection
   // is its conn_id; the key is derived from the frame here where a hit needs it)
+  // link: the frame's chain link (pn_service_post_linked), 0 = none
   template <class HH>
-  void onFrame(HH& h, uint64_t key, const pn_result& rec, const uint8_t* eth) {
+  PN_HOT void onFrame(HH& h, uint64_t key, const pn_result& rec, const uint8_t* eth, uint16_t link = 0) {
+    ++frame_idx_;
+    if (link && inOrder(h, rec, eth, link)) return;
     if (rec.flags & (PN_F_NOT_TCP | PN_F_TRUNC | PN_F_BADOFF)) return;
     if (!self().accepts(eth)) return; // the NIC filter (Core.h:335-383)
     if (drop_bad_ && !checksums_ok(rec.flags)) return;
@@ -957,6 +977,7 @@ class TcpEngine {
     // (EfviTcp.h:208-211), so a server's new connection reports the previous one's error until
     // its own (the client's is set by connect's result, EfviTcp.h:122)
     c.established_ = c.fin_sent_ = c.fin_received_ = c.fast_re_ = c.in_recover_ = false;
+    c.ack_frame_ = ~0ull;
     c.send_una_ = c.send_next_ = c.data_next_size_ = c.dup_ack_cnt_ = c.retries_ = 0;
     c.data_next_ = 1;
     c.smss_ = 536;
@@ -1031,7 +1052,7 @@ class TcpEngine {
     HH& h;
     Conn& c;
     const uint8_t* eth;
-    uint32_t onData(RxConn<IConf>&, const uint8_t* d, uint32_t n) { // EfviTcp.h:136-139, 301-304
+    PN_HOT uint32_t onData(RxConn<IConf>&, const uint8_t* d, uint32_t n) { // EfviTcp.h:136-139, 301-304
       if (kRecvTimeoutMs) s.setUserTimer(c, 1, kRecvTimeoutMs);
       return h.data(c, d, n);
     }
@@ -1046,13 +1067,48 @@ class TcpEngine {
       c.err_ = "connection reset";
       h.disconnect(c);
     }
-    void onAckField(RxConn<IConf>&, bool no_text) { s.onAck(c, eth, no_text); }
+    PN_HOT void onAckField(RxConn<IConf>&, bool no_text) {
+      c.ack_frame_ = s.frame_idx_; // the in-order fast path's proof that this frame's ack field was applied
+      s.onAck(c, eth, no_text);
+    }
   };
 
   template <class HH>
-  void onPack(HH& h, Conn& c, const uint8_t* eth, const pn_result& r) {
+  PN_HOT void onPack(HH& h, Conn& c, const uint8_t* eth, const pn_result& r) {
     PackAdapter<HH> a{*this, h, c, eth};
-    const RxAck ack = c.rx_.onSegment(a, eth, r);
+    afterSegment(h, c, c.rx_.onSegment(a, eth, r));
+  }
+
+  // The in-order fast path (round 6).  The GPU's chain link says this frame continues frame
+  // j = frame_idx_ - link, the previous frame of the same connection in the batch, exactly: clean flags, payload,
+  // seq = j's seq + payload_len, and the same payload offset, ack number, window and destination.  When j's ACK field
+  // was processed (ack_frame_: so j also passed the NIC filter and the checksum discard), the record is the
+  // snapshot's and the table unchanged, and the connection is still where an in-order segment leaves it --
+  // established, no FIN either way, nothing held or out of order -- and the same ack field changes nothing
+  // (TcpConn.h:536-665: the window no wider than j's made it, una not advanced by j's ack number, nothing queued
+  // that the window admits; what j's own handler sent since is checked here, not assumed), then TcpConn::onPack's
+  // remaining steps are exactly: the payload to onData zero-copy, the window slide, the ACK decision
+  // (TcpConn.h:700-764).  Anything else takes the full path (false).
+  template <class HH>
+  PN_HOT bool inOrder(HH& h, const pn_result& r, const uint8_t* eth, uint16_t link) {
+    if (tver_ != disp_ver_ || r.conn_id >= kMaxConn) return false; // the links are the batch-start table's
+    Conn& c = conns_[r.conn_id];
+    if (c.ack_frame_ != frame_idx_ - link || !c.established_ || c.fin_sent_) return false;
+    // onAck with j's ack number again: una would not move, and sendQueued would send nothing
+    if (c.send_una_ != c.send_next_ && (int32_t)(c.ack_in_ - c.seg(c.send_una_ + 1).seq) >= 0) return false;
+    const uint32_t queued = c.data_next_ == c.send_next_ ? c.data_next_size_ : c.smss_;
+    if (queued && (int32_t)(c.next_seq_ + queued - c.send_wnd_seq_) <= 0) return false;
+    const uint32_t len = (uint32_t)(int32_t)r.payload_len;
+    if (!c.rx_.inOrderReady(r.seq, len)) return false;
+    PackAdapter<HH> a{*this, h, c, eth};
+    c.ack_frame_ = frame_idx_; // its ACK field is j's: processed (as a no-op)
+    afterSegment(h, c, c.rx_.onInOrder(a, eth + r.payload_off, len));
+    ++in_order_;
+    return true;
+  }
+
+  template <class HH>
+  PN_HOT void afterSegment(HH& h, Conn& c, const RxAck ack) {
     if (c.rx_.closed() && !c.isClosed()) { // RST accepted, or receive buffer full (TcpConn.h:526-531, 741-745)
       if (ack.rst)
         closeConn(c); // close(): RST to the peer
@@ -1072,8 +1128,9 @@ class TcpEngine {
   }
 
   // Step 5: the ACK field (TcpConn.h:536-665; pollnet: no cwnd, no window scaling).
-  void onAck(Conn& c, const uint8_t* eth, bool no_text) {
+  PN_HOT void onAck(Conn& c, const uint8_t* eth, bool no_text) {
     const uint32_t ack_num = ackNum(eth);
+    c.ack_in_ = ack_num; // (inOrder)
     bool window_updated = false;
     if (!c.fin_sent_) {
       const uint32_t w = ack_num + srv_detail::rd16(eth + 34 + 14);
@@ -1111,8 +1168,13 @@ class TcpEngine {
     sendQueued(c);
   }
 
-  // Transmit queued segments the window now admits (TcpConn.h:646-660).
-  void sendQueued(Conn& c) {
+  // Transmit queued segments the window now admits (TcpConn.h:646-660).  Nothing queued (the common case: the
+  // segment being built is the next to send and empty) ends it before the loop, inline.
+  PN_HOT void sendQueued(Conn& c) {
+    if (c.data_next_ == c.send_next_ && !c.data_next_size_) return;
+    sendQueuedLoop(c);
+  }
+  void sendQueuedLoop(Conn& c) {
     while (uint32_t size = (c.data_next_ == c.send_next_ ? c.data_next_size_ : c.smss_)) {
       typename Conn::Seg& s = c.seg(c.send_next_);
       if ((int32_t)(s.seq + size - c.send_wnd_seq_) > 0) break;
@@ -1192,7 +1254,7 @@ class TcpEngine {
   // complete, and sendPartial / sendFin keep data_next <= send_una + ConnSendBufCnt - 1: that range
   // is never empty and getAckBuf never fails — the ACK (and close()'s RST) always goes out.  The one
   // case the reference would drop, a buffer still in the NIC's TX queue, does not exist here.
-  void sendAck(Conn& c, bool immediate) {
+  PN_HOT void sendAck(Conn& c, bool immediate) {
     if (kDelayedAckMS == 0 || immediate) {
       emit(c, c.next_seq_, kAck, nullptr, 0);
       return;
@@ -1460,6 +1522,8 @@ class TcpEngine {
   bool tx_fl_host_ = false;           // the batch in its fill was summed on the host
   uint64_t tx_host_frames_ = 0, tx_gpu_frames_ = 0;
   uint64_t re_resolved_ = 0;
+  uint64_t frame_idx_ = 0; // frames dispatched (onFrame) since init: a frame's place for the chain links
+  uint64_t in_order_ = 0;  // frames that took the in-order fast path
   bool ready_ = false, drop_bad_ = true;
   const char* err_ = "Closed";
 };

@@ -348,3 +348,38 @@ void orc_classify_batch_unverified(const uint8_t* slots, uint32_t slot_stride, u
                                    pn_result* out, int n_threads) {
   run_batch(slots, slot_stride, frame_off, n, tbl, n_entries, mask, max_conn, out, n_threads, 3);
 }
+
+/* ---- chain links (pn_service_post_linked) ---- */
+static int orc_chain_usable(const pn_result* r) {
+  const uint32_t f = r->flags;
+  const uint32_t need = PN_F_HIT | PN_F_ACK | PN_F_IP_OK;
+  const uint32_t none = PN_F_TW | PN_F_SYN | PN_F_FIN | PN_F_RST | PN_F_NOT_TCP | PN_F_TRUNC | PN_F_BADOFF | PN_F_IHL_NE_5;
+  return (f & need) == need && (f & none) == 0 && (f & (PN_F_TCP_OK | PN_F_TCP_UNCHECKED)) != 0 && r->payload_len > 0;
+}
+
+void orc_chain_links(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n, const pn_result* recs,
+                     uint32_t max_conn, uint32_t max_frames, uint32_t max_conns, uint16_t* links) {
+  memset(links, 0, (size_t)n * sizeof(uint16_t));
+  if (n > max_frames || max_conn > max_conns || n == 0) return;
+  uint32_t* last = (uint32_t*)malloc((size_t)(max_conn ? max_conn : 1) * sizeof(uint32_t)); /* 1 + index, 0 = none */
+  memset(last, 0, (size_t)(max_conn ? max_conn : 1) * sizeof(uint32_t));
+  for (uint32_t i = 0; i < n; i++) {
+    const pn_result* r = &recs[i];
+    if ((r->flags & (PN_F_HIT | PN_F_TW)) != PN_F_HIT || r->conn_id >= max_conn) continue;
+    const uint32_t pj = last[r->conn_id];
+    last[r->conn_id] = i + 1;
+    if (!pj) continue;
+    const uint32_t j = pj - 1;
+    const pn_result* q = &recs[j];
+    if (!orc_chain_usable(r) || !orc_chain_usable(q)) continue;
+    if (r->seq != q->seq + (uint32_t)q->payload_len || r->payload_off != q->payload_off) continue;
+    const uint8_t* ei = slots + (size_t)i * slot_stride + frame_off;
+    const uint8_t* ej = slots + (size_t)j * slot_stride + frame_off;
+    /* ack number (tcp + 8), window (tcp + 14), destination address (ip + 16) and port (tcp + 2), IHL 5 */
+    if (memcmp(ei + 42, ej + 42, 4) || memcmp(ei + 48, ej + 48, 2) || memcmp(ei + 30, ej + 30, 4) ||
+        memcmp(ei + 36, ej + 36, 2))
+      continue;
+    links[i] = (uint16_t)(i - j);
+  }
+  free(last);
+}

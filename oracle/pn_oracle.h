@@ -85,6 +85,15 @@ void orc_classify_batch_unverified(const uint8_t* slots, uint32_t slot_stride, u
                                    const pn_conn_entry* tbl, uint32_t n_entries, uint64_t mask, uint32_t max_conn,
                                    pn_result* out, int n_threads);
 
+/* Chain links over a classified batch (pn_service_post_linked): links[i] = d > 0 when frame i - d is
+ * the previous frame of frame i's connection in the batch (records with PN_F_HIT and not PN_F_TW) and frame i
+ * continues it in order -- the case TcpConn::onPack hands to onData zero-copy without touching its segment list
+ * (TcpConn.h:650-725): both clean, both with payload, seq contiguous, equal payload offset, ack number, window,
+ * destination address and port.  Frame i at slots + i * slot_stride + frame_off.  All 0 when n > max_frames or
+ * max_conn > max_conns (the GPU pass's LDS bounds, PN_LINK_MAX_FRAMES / PN_LINK_MAX_CONNS). */
+void orc_chain_links(const uint8_t* slots, uint32_t slot_stride, uint32_t frame_off, uint32_t n, const pn_result* recs,
+                     uint32_t max_conn, uint32_t max_frames, uint32_t max_conns, uint16_t* links);
+
 /* ---- TX checksum generation (pn_tx_oracle.c) ---- */
 /* n frames built the way a reference sender builds them (incremental CSum state:
  * TcpConn.h:149-323, 771-785; Core.h:157-163, 385-446; Efvi.h:405-411, 590-636).

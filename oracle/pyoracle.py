@@ -150,6 +150,20 @@ def classify_batch(slots: np.ndarray, stride: int, frame_off: int, n: int, entri
     return out
 
 
+_chain = _sig("orc_chain_links", None, _vp, _u32, _u32, _u32, _vp, _u32, _u32, _u32, _vp)
+LINK_MAX_FRAMES, LINK_MAX_CONNS = 1024, 4096  # PN_LINK_MAX_FRAMES / PN_LINK_MAX_CONNS
+
+
+def chain_links(slots: np.ndarray, stride: int, frame_off: int, n: int, recs: np.ndarray, max_conn: int,
+                max_frames: int = LINK_MAX_FRAMES, max_conns: int = LINK_MAX_CONNS) -> np.ndarray:
+    """orc_chain_links: the u16 chain link of each frame of a classified batch (pn_service_post_linked)."""
+    assert slots.dtype == np.uint8 and slots.flags.c_contiguous and slots.size >= n * stride
+    r = np.ascontiguousarray(recs[:n], dtype=RESULT_DTYPE)
+    out = np.zeros(n, np.uint16)
+    _chain(slots.ctypes.data, stride, frame_off, n, r.ctypes.data, max_conn, max_frames, max_conns, out.ctypes.data)
+    return out
+
+
 # ---------------- the reference itself: TcpStream.h (oracle/_ref) ----------------
 _ref = None
 

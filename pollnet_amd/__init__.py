@@ -24,6 +24,8 @@ from .rx import (  # noqa: F401
     PN_SERVICE_WAVES_PER_CU,
     PN_SERVICE_MAX_WAVES,
     PN_SERVICE_MAX_FRAMES,
+    PN_LINK_MAX_FRAMES,
+    PN_LINK_MAX_CONNS,
     F,
     ConnTable,
     PollnetError,

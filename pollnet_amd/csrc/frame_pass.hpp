@@ -85,6 +85,10 @@ enum : int { kAblEarlyStore = 1 << 23 };
 // product (pn_set_verify(ctx, 0)): no segment stream and no TCP verdict -- the header lines only, as the
 // reference's release path reads them (Core::checksum is debug-only, Core.h:448-478)
 enum : int { kHeaderOnly = 1 << 24 };
+// product (the resident service, round 6): besides its record, each frame's chain fields go to KArgs::aux (device
+// scratch, when set) -- the record again and the ack number, destination address, window and destination port --
+// for the post's chain pass (rx_service.hip chain_pass)
+enum : int { kChainAux = 1 << 25 };
 constexpr int kProdAbl = kExactRange | kCoopProbe | kGroupProbe | kSkipEmptyLoads | kSkipWaveGate | kPipeStream;
 
 // Header window of lane `lane`'s slot for a strided layout (slot r of the wave at

@@ -70,6 +70,13 @@ struct KArgs {
   uint32_t sig_token = 0;
 };
 
+// The resident service's arguments (kChainAux): KArgs and where each frame's chain entries go.  A classify
+// instantiated with kChainAux is only ever given one of these (the production launches keep KArgs as it is, so their
+// kernel arguments and code are unchanged).
+struct KArgsAux : KArgs {
+  u32x4* aux = nullptr; // two 16-B entries per frame (device scratch), or nullptr
+};
+
 // Conn-table lookup carried from the home-slot load to its resolution.
 struct Probe {
   uint64_t key;
@@ -286,7 +293,7 @@ __device__ __forceinline__ FrameState header_phase(const Window& h, uint32_t eth
 // ---- phase 3: fold and write the record on the frame's lane ----
 template <int MIS, int ABL, int SAUX>
 __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f, const uint8_t* win, bool bad_off,
-                                       u32x4* lds_rec) {
+                                       u32x4* lds_rec, uint32_t cx_ack = 0, uint32_t cx_wport = 0) {
   uint32_t flags = st.flags;
   uint32_t tcp_fold = 0xffff;
   if constexpr ((ABL & kHeaderOnly) != 0) { // the release path: no TCP sum (the IP header is in the window)
@@ -321,6 +328,13 @@ __device__ __forceinline__ void finish(const KArgs& a, FrameState st, uint32_t f
   rec.z = (uint32_t)data_off | ((uint32_t)(data_end - data_off) << 16);
   rec.w = flags | (tcp_fold << 16);
   if (bad_off) rec = u32x4{PN_MISS, 0, 0, PN_F_BADOFF}; // outside the launch's alignment class: not parsed
+  if constexpr (ABL & kChainAux) {
+    u32x4* aux = static_cast<const KArgsAux&>(a).aux;
+    if (aux) {
+      aux[2 * f] = rec;
+      aux[2 * f + 1] = u32x4{cx_ack, st.dst_ip, cx_wport, 0u};
+    }
+  }
   if (lds_rec) { // grouped launches write the workgroup's records in one burst at its end
     *lds_rec = rec;
   } else if constexpr (ABL & (kAblNoStore | kAblEarlyStore)) {
@@ -526,7 +540,13 @@ __device__ __forceinline__ void classify_group(const KArgs& a, const uint32_t wa
     }
   }
   if constexpr (ABL & kLateProbe) probe_finish<ABL>(st.probe, live && !bad_off, a, st.conn_id, st.flags);
-  if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
+  if constexpr (ABL & kChainAux) { // the ack number and window << 16 | destination port, as stored
+    if (live)
+      finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr, h.template u32<MIS + 28>(),
+                             h.template u16<MIS + 22>() | (h.template u16<MIS + 34>() << 16));
+  } else {
+    if (live) finish<MIS, ABL, SAUX>(a, st, f, win, bad_off, lds_recs ? lds_recs + lane : nullptr);
+  }
 }
 
 // GRP = 1: one 64-frame group per workgroup, records stored as each group finishes.

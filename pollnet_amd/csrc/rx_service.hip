@@ -36,15 +36,15 @@ using pn_internal::set_err;
 
 struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its device copy
   uint32_t gen;              // = seq, stored after the fields
-  uint32_t n;                // frames, or PN_SERVICE_STOP
-  uint32_t verify;           // pn_set_verify's setting at the post
+  uint32_t n;                // frames | kPostVerify | kPostLinks, or PN_SERVICE_STOP
+  uint32_t fpw;              // frames per group (svc_fpw, bits 0-7) | helper waves << 8 (svc_helpers)
   uint32_t max_conn;
   const uint8_t* frames;
   pn_result* out;
   const pn_conn_entry* tbl;
-  uint64_t mask;
+  uint16_t* links;           // pn_service_post_linked: the chain links (host or device memory), else nullptr
+  uint32_t mask;             // tbl_mask (< n_entries: 32 bits)
   uint32_t n_entries;
-  uint32_t fpw;   // frames per group (svc_fpw, bits 0-7) | helper waves << 8 (svc_helpers)
   uint32_t check; // svc_check: k ^ the xor of words 1-13, so a read that mixed two posts' words is refused
   uint32_t seq; // stored last (release)
 };
@@ -57,6 +57,8 @@ constexpr uint32_t kLatWaves = PN_SERVICE_WAVES; // the latency tier: every post
 static_assert(kLatWaves <= kDoneWords, "a latency-tier post completes through per-wave done words");
 constexpr uint32_t kLatFrames = kLatWaves * kFramesPerWave; // the largest post the tier takes alone
 constexpr uint32_t kPostLimitMs = 8000; // a post in flight (pn_service_wait gives up at 10 s)
+constexpr uint32_t kPostVerify = 1u << 30, kPostLinks = 1u << 29, kPostN = (1u << 21) - 1; // the n word
+constexpr uint32_t kLinkFrames = PN_LINK_MAX_FRAMES, kLinkConns = PN_LINK_MAX_CONNS;
 constexpr uint32_t kSvcIdle = 0xFFFFFFFFu; // published as the post when wave 0 ends for lack of posts
 constexpr uint32_t kSvcStop = 0xFFFFFFFFu; // published as the wave count of a stop post
 
@@ -71,6 +73,7 @@ struct alignas(64) SvcDev { // device memory, set by the host before every launc
 
 struct SArgs {
   const SvcPost* mail;  // host: the two mailbox slots
+  u32x4* scratch;       // device: per mailbox slot, kLinkFrames x 2 chain entries (kChainAux)
   uint32_t* done_words; // host: per wave, the last post it finished its groups of
   uint32_t* exit_word;  // host: the launch's epoch once it ended for lack of posts
   SvcDev* dev;
@@ -113,54 +116,188 @@ inline uint32_t svc_helpers(uint32_t n, uint32_t max) {
 }
 
 // a post's kernel arguments from its 64-B line held one word per lane (lanes 0-15, SvcPost's layout)
-__device__ __forceinline__ KArgs svc_args(uint32_t v, const SArgs& s) {
+__device__ __forceinline__ KArgsAux svc_args(uint32_t v, const SArgs& s, uint32_t k) {
   // readlane returns int: each word through uint32_t, or a low word with bit 31 set would sign-extend
   auto u64 = [&](int lo) {
     return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, lo + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane(v, lo);
   };
-  KArgs a;
-  a.n = __builtin_amdgcn_readlane(v, 1);
+  KArgsAux a;
+  const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
+  a.n = nw & kPostN;
+  a.fpw = __builtin_amdgcn_readlane(v, 2) & 0xffu;
   a.max_conn = __builtin_amdgcn_readlane(v, 3);
   a.frames = reinterpret_cast<const uint8_t*>(u64(4));
   a.out = reinterpret_cast<pn_result*>(u64(6));
   a.tbl = reinterpret_cast<const pn_conn_entry*>(u64(8));
-  a.mask = u64(10);
-  a.n_entries = __builtin_amdgcn_readlane(v, 12);
+  a.mask = (uint32_t)__builtin_amdgcn_readlane(v, 12);
+  a.n_entries = __builtin_amdgcn_readlane(v, 13);
   a.stride = s.stride;
   a.ipa_off = s.ipa_off;
   a.avail = s.avail;
   a.offs = nullptr;
-  a.fpw = __builtin_amdgcn_readlane(v, 13) & 0xffu;
+  // a linked post's frames also leave their chain entries in the slot's scratch
+  a.aux = (nw & kPostLinks) ? s.scratch + (size_t)(k & 1) * kLinkFrames * 2 : nullptr;
   return a;
 }
 
-// wave w's groups of the post (round robin over the post's waves), then its records made visible to the host and,
-// on a post of at most kDoneWords waves, post k stored to its done word
-template <int MIS, int COOP>
-__device__ __forceinline__ void svc_run(const KArgs& a, bool verify, uint32_t w, uint32_t act, uint32_t k,
-                                        uint32_t* done_word, int lane) {
-  for (uint32_t g = w; g * a.fpw < a.n; g += act) {
-    if (verify) classify_group<MIS, COOP, kProdAbl, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
-    else classify_group<MIS, COOP, kProdAbl | kHeaderOnly, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
-  }
-  __threadfence_system();
-  if (lane == 0 && act <= kDoneWords) __hip_atomic_store(done_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+__device__ __forceinline__ uint16_t* svc_links(uint32_t v) {
+  return reinterpret_cast<uint16_t*>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, 11) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane(v, 10));
 }
 
-// a multi-wave post: count this wave done; the last one resets the count and marks the post done for wave 0, and
-// for a post on more than kDoneWords waves stores k to done word 0 (every wave's records were made system-visible
-// before its count: the fence pairs them with this store)
-__device__ __forceinline__ void svc_count(SvcDev* dev, uint32_t act, uint32_t k, uint32_t* done_word0, int lane) {
-  if (lane == 0) {
-    const uint32_t prev = atomicAdd(&dev->count, 1u);
-    if (prev == act - 1) {
-      dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
-      if (act > kDoneWords) {
-        __threadfence_system();
-        __hip_atomic_store(done_word0, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      __hip_atomic_store(&dev->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+// ---- chain links (round 6): the in-order successor structure of a post, for the host's fast path ----
+// links[i] = d > 0 when frame j = i - d is the previous frame of the same connection in the post (records with
+// PN_F_HIT and not PN_F_TW; other frames are not part of any chain) and frame i continues it exactly: both frames
+// are clean (ACK; no SYN, FIN, RST; no NOT_TCP / TRUNC / BADOFF / IHL_NE_5; IP_OK and TCP_OK or TCP_UNCHECKED),
+// both carry payload, seq_i = seq_j + payload_len_j, and payload offset, ack number, window, destination address and
+// port are equal.  Else 0.  The oracle's statement is orc_chain_links (oracle/pn_oracle.c).
+constexpr uint32_t kCleanNeed = PN_F_HIT | PN_F_ACK | PN_F_IP_OK;
+constexpr uint32_t kCleanNone = PN_F_TW | PN_F_SYN | PN_F_FIN | PN_F_RST | PN_F_NOT_TCP | PN_F_TRUNC | PN_F_BADOFF |
+                                PN_F_IHL_NE_5;
+
+struct ChainLds {
+  uint32_t last[kLinkConns]; // 1 + the last frame of each connection so far (0: none)
+  uint32_t key[kLinkFrames]; // each frame's connection (0xFFFFFFFF: in no chain), to reset `last` after the pass
+  uint32_t seq_end[kLinkFrames];
+  u32x4 fields[kLinkFrames]; // ack, dst_ip, window | dst_port, payload_off | usable << 16
+};
+
+__device__ __forceinline__ ChainLds& chain_lds() {
+  __shared__ ChainLds c;
+  return c;
+}
+
+// every entry of the table: none (at launch; each pass resets what it used)
+__device__ __forceinline__ void chain_init(int lane) {
+  ChainLds& c = chain_lds();
+  for (uint32_t i = lane; i < kLinkConns; i += kWave) c.last[i] = 0u;
+  wave_lds_sync();
+}
+
+// One 64-frame step of the pass: frame i = base + lane with its record and chain fields (rec, fx; i < n when valid).
+__device__ __forceinline__ void chain_step(ChainLds& c, uint32_t base, uint32_t n, uint32_t max_conn, bool on,
+                                           const u32x4& rec, const u32x4& fx, const __amdgpu_buffer_rsrc_t& lr,
+                                           uint64_t below, int lane) {
+  const uint32_t i = base + lane;
+  const bool valid = i < n;
+  const uint32_t flags = rec.w & 0xffffu;
+  const uint32_t len = rec.z >> 16; // payload_len (int16): usable when in (0, 0x8000)
+  const bool member = on && valid && (flags & (PN_F_HIT | PN_F_TW)) == PN_F_HIT && rec.x < max_conn;
+  const bool usable = (flags & kCleanNeed) == kCleanNeed && (flags & kCleanNone) == 0 &&
+                      (flags & (PN_F_TCP_OK | PN_F_TCP_UNCHECKED)) != 0 && len != 0 && len < 0x8000u;
+  const uint32_t key = member ? rec.x : 0u;
+  if (valid) { // this frame's fields, for its successor
+    c.key[i] = member ? key : 0xFFFFFFFFu;
+    c.seq_end[i] = rec.y + len;
+    c.fields[i] = u32x4{fx.x, fx.y, fx.z, (rec.z & 0xffffu) | (usable ? 0x10000u : 0u)};
+  }
+  uint32_t prev = 0; // 1 + the previous frame, 0 = none
+  if (member) prev = c.last[key];
+  wave_lds_sync();
+  if (member) atomicMax(&c.last[key], i + 1);
+  wave_lds_sync();
+  uint64_t todo = __ballot(member && c.last[key] != i + 1); // lanes with a higher lane of their connection
+  while (todo) {
+    const uint32_t leader = (uint32_t)__builtin_ctzll(todo);
+    const uint32_t kk = __builtin_amdgcn_readlane(key, leader);
+    const uint64_t m = __ballot(member && key == kk);
+    todo &= ~m;
+    const uint64_t lower = m & below;
+    if (member && key == kk && lower) prev = base + 64u - (uint32_t)__builtin_clzll(lower); // 1 + that lane
+  }
+  uint32_t d = 0;
+  if (member && usable && prev) {
+    const uint32_t j = prev - 1;
+    const u32x4 pf = c.fields[j];
+    if ((pf.w >> 16) && c.seq_end[j] == rec.y && pf.x == fx.x && pf.y == fx.y && pf.z == fx.z &&
+        (pf.w & 0xffffu) == (rec.z & 0xffffu))
+      d = i - j;
+  }
+  if (valid) __builtin_amdgcn_raw_buffer_store_b16((unsigned short)d, lr, i * 2, 0, 0);
+  wave_lds_sync(); // this step's reads of fields before the next step's writes (other lanes' entries)
+}
+
+// The pass over a post's n frames (their chain entries in scratch `aux`, written by the post's waves and visible to
+// this one), by one wave, in 64-frame steps: each frame's previous frame of its connection comes from the table of
+// last frames -- or, where a connection repeats inside the step, from the highest lane below with the same
+// connection (one ballot round per repeating connection: none in a step of distinct flows, one for a single flow).
+// The entries are loaded 8 steps (512 frames) at a time, all in flight before the first is used: one memory round
+// trip per 512 frames, not one per step.
+__device__ __forceinline__ void chain_pass(const u32x4* aux, uint32_t n, uint32_t max_conn, uint16_t* links, int lane) {
+  constexpr int kChunk = 8;
+  ChainLds& c = chain_lds();
+  const bool on = max_conn <= kLinkConns;
+  const __amdgpu_buffer_rsrc_t lr = frame_rsrc(reinterpret_cast<const uint8_t*>(links), n * 2);
+  const __amdgpu_buffer_rsrc_t ar = frame_rsrc(reinterpret_cast<const uint8_t*>(aux), n * 32);
+  const uint64_t below = (1ull << lane) - 1;
+  for (uint32_t base0 = 0; base0 < n; base0 += kChunk * kWave) {
+    u32x4 rec[kChunk], fx[kChunk];
+#pragma unroll
+    for (int s = 0; s < kChunk; ++s) { // past n: the descriptor's range returns zeros (a miss: in no chain)
+      const uint32_t i = base0 + s * kWave + lane;
+      rec[s] = __builtin_amdgcn_raw_buffer_load_b128(ar, i * 32, 0, 0);
+      fx[s] = __builtin_amdgcn_raw_buffer_load_b128(ar, i * 32 + 16, 0, 0);
     }
+#pragma unroll
+    for (int s = 0; s < kChunk; ++s)
+      if (base0 + s * kWave < n) chain_step(c, base0 + s * kWave, n, max_conn, on, rec[s], fx[s], lr, below, lane);
+  }
+  // the table back to none for the next post (only the connections this one touched)
+  for (uint32_t i = lane; i < n; i += kWave) {
+    const uint32_t k = c.key[i];
+    if (k != 0xFFFFFFFFu) c.last[k] = 0u;
+  }
+  wave_lds_sync();
+}
+
+// wave w's groups of the post (round robin over the post's waves), then its records made visible to the host and,
+// on a post of at most kDoneWords waves without links, post k stored to its done word (a linked post completes after
+// its chain pass, svc_finish)
+// A helper wave (HELPER) makes nothing visible itself: its grid's end does (the host waits for it, svc_post_done),
+// which spares the post one L2 write-back per helper wave.
+template <int MIS, int COOP, bool HELPER = false>
+__device__ __forceinline__ void svc_run(const KArgsAux& a, bool verify, bool linked, uint32_t w, uint32_t act, uint32_t k,
+                                        uint32_t* done_word, int lane) {
+  for (uint32_t g = w; g * a.fpw < a.n; g += act) {
+    if (verify) classify_group<MIS, COOP, kProdAbl | kChainAux, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane, nullptr);
+    else
+      classify_group<MIS, COOP, kProdAbl | kHeaderOnly | kChainAux, kLoadAux, kStoreAux, 0, kLoadAux>(a, g * a.fpw, lane,
+                                                                                                     nullptr);
+  }
+  if constexpr (HELPER) return;
+  __threadfence_system();
+  if (lane == 0 && act <= kDoneWords && !linked)
+    __hip_atomic_store(done_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The wave that completes a post through done word 0 alone (a post on more than kDoneWords waves, or a linked post):
+// a linked post's chain pass first, over the chain entries every wave of the post left in scratch; then k to done word
+// 0 once everything the post writes is visible to the host.
+template <bool PASS>
+__device__ __forceinline__ void svc_finish(const KArgsAux& a, uint16_t* links, uint32_t k, uint32_t* done_word0, int lane) {
+  if constexpr (PASS) {
+    if (a.aux) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // the other waves' chain entries
+      chain_pass(a.aux, a.n, a.max_conn, links, lane);
+    }
+  }
+  __threadfence_system();
+  if (lane == 0) __hip_atomic_store(done_word0, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// a multi-wave post: count this wave done; the last one resets the count, completes the post through done word 0
+// when it has no per-wave words (svc_finish), and marks it done for wave 0 (every wave's records and chain entries
+// were made system-visible before its count: the count's order pairs them with what the last wave does next)
+template <bool PASS>
+__device__ __forceinline__ void svc_count(SvcDev* dev, const KArgsAux& a, uint16_t* links, uint32_t act, uint32_t k,
+                                          uint32_t* done_word0, int lane) {
+  uint32_t prev = 0;
+  if (lane == 0) prev = atomicAdd(&dev->count, 1u);
+  prev = __builtin_amdgcn_readfirstlane(prev);
+  if (prev == act - 1) {
+    if (lane == 0) dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
+    if (act > kDoneWords || a.aux) svc_finish<PASS>(a, links, k, done_word0, lane);
+    if (lane == 0) __hip_atomic_store(&dev->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -178,6 +315,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   uint32_t last = s.last;
   uint64_t t0 = wall_clock64();
   const uint64_t net = s.idle_ticks + (s.idle_ticks >> 1) + s.post_ticks;
+  chain_init(lane); // any wave of the tier may complete a linked post
   for (;;) {
     uint32_t v = 0;         // the post's 64-B line, lane i holding word i (lanes 0-15)
     uint32_t k = 0, act = 0; // the post and its wave count
@@ -205,13 +343,13 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
       t_acc = wall_clock64();
-      const uint32_t n = __builtin_amdgcn_readlane(v, 1);
-      if (n == PN_SERVICE_STOP) {
+      const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
+      if (nw == PN_SERVICE_STOP) {
         if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)kSvcStop << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
-      const uint32_t fw = __builtin_amdgcn_readlane(v, 13);
-      act = svc_active(n, fw & 0xffu, W + (fw >> 8));
+      const uint32_t fw = __builtin_amdgcn_readlane(v, 2);
+      act = svc_active(nw & kPostN, fw & 0xffu, W + (fw >> 8));
       if (act > 1) { // the post's other waves read it from the device copy
         if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[k & 1])[lane] = v;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -236,8 +374,11 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       }
     }
     if (run) { // one call site for every wave (the classify code is inlined once per path)
-      svc_run<MIS, COOP>(svc_args(v, s), __builtin_amdgcn_readlane(v, 2) != 0, w, act, k, s.done_words + w, lane);
-      if (act > 1) svc_count(s.dev, act, k, s.done_words, lane);
+      const KArgsAux a = svc_args(v, s, k);
+      const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
+      svc_run<MIS, COOP>(a, (nw & kPostVerify) != 0, a.aux != nullptr, w, act, k, s.done_words + w, lane);
+      if (act > 1) svc_count<true>(s.dev, a, svc_links(v), act, k, s.done_words, lane);
+      else if (a.aux) svc_finish<true>(a, svc_links(v), k, s.done_words, lane);
     }
     if (w == 0) {
       if (act == 1) { // one wave's work, done: let the others see it go by
@@ -286,8 +427,9 @@ __global__ __launch_bounds__(kWave) void rx_service_helper_kernel(SArgs s, uint3
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[k & 1]);
   const uint32_t v = lane < 16 ? cp[lane] : 0u;
-  svc_run<MIS, COOP>(svc_args(v, s), __builtin_amdgcn_readlane(v, 2) != 0, w, act, k, s.done_words, lane);
-  svc_count(s.dev, act, k, s.done_words, lane);
+  const KArgsAux a = svc_args(v, s, k); // never a linked post (at most kLinkFrames frames: the tier's alone)
+  svc_run<MIS, COOP, true>(a, (__builtin_amdgcn_readlane(v, 1) & kPostVerify) != 0, false, w, act, k, s.done_words, lane);
+  svc_count<false>(s.dev, a, nullptr, act, k, s.done_words, lane);
 }
 
 template <int MIS>
@@ -310,6 +452,7 @@ struct pn_service {
   uint32_t stride = 0, frame_off = 0;
   uint32_t helpers_max = 0;            // helper waves of a large post: its total wave count less the tier's
   uint32_t post_helpers[2] = {0, 0};   // helper waves of the last two posts (a relaunch launches them again)
+  hipEvent_t helper_ev[2] = {nullptr, nullptr}; // the end of each one's helper grid: its records are visible then
   uint64_t idle_ticks = 0, post_ticks = 0;
   SvcPost* mail = nullptr;    // pinned host: 2 slots
   uint32_t* words = nullptr;  // pinned host: [0, 64) the waves' done words, [kExitWord] exit (its own line)
@@ -319,6 +462,7 @@ struct pn_service {
   uint32_t tbl_post[2] = {0, 0};
   bool tbl_used[2] = {false, false};
   SvcDev* dev = nullptr;      // device
+  u32x4* scratch = nullptr;   // device: the chain entries of linked posts, kLinkFrames x 2 per mailbox slot
   uint32_t seq = 0;           // last post issued
   uint32_t epoch = 0;         // launches so far
   bool running = false;       // a launch that has not been seen to end
@@ -331,6 +475,7 @@ namespace {
 SArgs svc_sargs(const pn_service* v, uint32_t base) {
   SArgs a;
   a.mail = v->mail;
+  a.scratch = v->scratch;
   a.done_words = v->words;
   a.exit_word = v->words + kExitWord;
   a.dev = v->dev;
@@ -344,7 +489,8 @@ SArgs svc_sargs(const pn_service* v, uint32_t base) {
   return a;
 }
 
-// the helper grid of large post k
+// the helper grid of large post k, and the event its end completes (the post is done once both its done word and the
+// grid's end are: the helpers leave the write-back of their records to the end of their grid)
 int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
   const SArgs a = svc_sargs(v, 0);
   hipStream_t s = v->helper_stream;
@@ -358,7 +504,9 @@ int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
     case 12: launch_helpers<12>(v->coop, helpers, a, k, s); break;
     default: launch_helpers<14>(v->coop, helpers, a, k, s); break;
   }
-  const hipError_t e = hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && !v->helper_ev[k & 1]) e = hipEventCreateWithFlags(&v->helper_ev[k & 1], hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventRecord(v->helper_ev[k & 1], s);
   if (e != hipSuccess) return hip_err(v->ctx, e, "pn_service: helper launch");
   return PN_OK;
 }
@@ -404,6 +552,7 @@ bool svc_post_done(const pn_service* v, uint32_t k) {
   const uint32_t words = v->post_words[k & 1];
   for (uint32_t w = 0; w < words; ++w)
     if ((int32_t)(__atomic_load_n(v->words + w, __ATOMIC_ACQUIRE) - k) < 0) return false;
+  if (v->post_helpers[k & 1] && hipEventQuery(v->helper_ev[k & 1]) != hipSuccess) return false; // (an error: not done)
   return true;
 }
 
@@ -423,8 +572,11 @@ void svc_free(pn_service* v) {
   if (v->mail) (void)hipHostFree(v->mail);
   if (v->words) (void)hipHostFree(v->words);
   if (v->dev) (void)hipFree(v->dev);
+  if (v->scratch) (void)hipFree(v->scratch);
   if (v->stream) (void)hipStreamDestroy(v->stream);
   if (v->helper_stream) (void)hipStreamDestroy(v->helper_stream);
+  for (hipEvent_t ev : v->helper_ev)
+    if (ev) (void)hipEventDestroy(ev);
   delete v;
 }
 } // namespace
@@ -486,7 +638,8 @@ int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, ui
       (e = hipStreamCreateWithFlags(&v->helper_stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipHostMalloc((void**)&v->mail, 2 * sizeof(SvcPost), hipHostMallocDefault)) != hipSuccess ||
       (e = hipHostMalloc((void**)&v->words, kWordsBytes, hipHostMallocDefault)) != hipSuccess ||
-      (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess) {
+      (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess ||
+      (e = hipMalloc((void**)&v->scratch, sizeof(u32x4) * 2 * 2 * kLinkFrames)) != hipSuccess) {
     const int rc = hip_err(ctx, e, "pn_service_open: allocation");
     svc_free(v);
     return rc;
@@ -504,6 +657,11 @@ int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, ui
 }
 
 int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results, uint32_t* post_id) {
+  return pn_service_post_linked(v, frames, n, results, nullptr, post_id);
+}
+
+int pn_service_post_linked(pn_service* v, const void* frames, uint32_t n, void* results, uint16_t* links,
+                           uint32_t* post_id) {
   if (!v) return set_err(nullptr, PN_EINVAL, "pn_service_post: service is NULL");
   pn_ctx* ctx = v->ctx;
   if (!ctx->tbl_dev) return set_err(ctx, PN_ENOTABLE, "pn_service_post: no conn table (call pn_set_conn_table)");
@@ -511,6 +669,8 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
     return set_err(ctx, PN_EINVAL, "pn_service_post: n must be in [1, PN_SERVICE_MAX_FRAMES], buffers set");
   if (((uintptr_t)frames & 15) || ((uintptr_t)results & 15))
     return set_err(ctx, PN_EINVAL, "pn_service_post: frames/results must be 16-byte aligned");
+  if (links && (n > PN_LINK_MAX_FRAMES || ((uintptr_t)links & 1)))
+    return set_err(ctx, PN_EINVAL, "pn_service_post_linked: n must be <= PN_LINK_MAX_FRAMES, links 2-byte aligned");
   // at most two posts outstanding: post k reuses the slot of post k - 2, which must be done
   const uint32_t done = svc_done(v);
   if ((int32_t)(v->seq - done) >= 2) return set_err(ctx, PN_EINVAL, "pn_service_post: two posts already outstanding");
@@ -524,15 +684,16 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
   // the fields and their check word first, then gen and seq = k, each a release store: the slot still holds post
   // k - 2 (done), so until gen and seq both read k it is not post k; and should the line's read be split into pieces
   // read at different times, a mix of two posts' fields fails the check and the kernel reads the slot again
-  p->n = n;
-  p->verify = ctx->verify_tcp ? 1u : 0u;
+  const bool verify = ctx->verify_tcp;
+  p->n = n | (verify ? kPostVerify : 0u) | (links ? kPostLinks : 0u);
   p->max_conn = ctx->max_conn;
   p->frames = (const uint8_t*)frames;
   p->out = (pn_result*)results;
   p->tbl = ctx->tbl_dev;
-  p->mask = ctx->mask;
+  p->links = links;
+  p->mask = (uint32_t)ctx->mask;
   p->n_entries = ctx->n_entries;
-  const uint32_t fpw = svc_fpw(n, p->verify != 0), helpers = svc_helpers(n, v->helpers_max);
+  const uint32_t fpw = svc_fpw(n, verify), helpers = svc_helpers(n, v->helpers_max);
   p->fpw = fpw | helpers << 8;
   const uint32_t act = svc_active(n, fpw, kLatWaves + helpers);
   // a large post's helpers first (they wait for wave 0 to publish it): should the launch fail, nothing was posted
@@ -541,7 +702,7 @@ int pn_service_post(pn_service* v, const void* frames, uint32_t n, void* results
     if (rc) return rc;
   }
   v->post_helpers[k & 1] = helpers;
-  v->post_words[k & 1] = act <= kDoneWords ? act : 1u;
+  v->post_words[k & 1] = (act <= kDoneWords && !links) ? act : 1u; // else done word 0 alone (svc_finish)
   v->tbl_post[ctx->cur] = k; // pn_set_conn_table waits for this post before it reuses the buffer
   v->tbl_used[ctx->cur] = true;
   p->check = svc_check(p, k);
@@ -590,6 +751,7 @@ int pn_service_close(pn_service* v) {
     const uint32_t k = v->seq + 1;
     SvcPost* p = v->mail + (k & 1);
     p->n = PN_SERVICE_STOP;
+    p->links = nullptr;
     v->post_words[k & 1] = 0;
     v->post_helpers[k & 1] = 0;
     p->check = svc_check(p, k);

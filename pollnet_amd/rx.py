@@ -124,11 +124,14 @@ _pn_match_streams = _sig("pn_match_streams", _i32, _vp, _vp, _u32, _u32, _u32, _
 _pn_service_open = _sig("pn_service_open", _i32, _vp, _u32, _u32, _u32, _c.POINTER(_vp))
 _pn_service_open_ex = _sig("pn_service_open_ex", _i32, _vp, _u32, _u32, _u32, _u32, _c.POINTER(_vp))
 _pn_service_post = _sig("pn_service_post", _i32, _vp, _vp, _u32, _vp, _vp)
+_pn_service_post_linked = _sig("pn_service_post_linked", _i32, _vp, _vp, _u32, _vp, _vp, _vp)
 _pn_service_wait = _sig("pn_service_wait", _i32, _vp, _u32)
 _pn_service_close = _sig("pn_service_close", _i32, _vp)
 PN_SERVICE_WAVES = 64
 PN_SERVICE_WAVES_PER_CU = 8
 PN_SERVICE_MAX_WAVES = 4096
+PN_LINK_MAX_FRAMES = 1024
+PN_LINK_MAX_CONNS = 4096
 PN_SERVICE_MAX_FRAMES = 1 << 20
 
 # The seeded workload generator lives in its own library (include/pollnet_amd_gen.h), outside
@@ -412,11 +415,16 @@ class RxService:
         self._h, self._ctx = h, ctx
         self._inflight = {}  # post id -> (frames, results): alive until the post completes
 
-    def post(self, frames, n: int, results) -> int:
-        """Non-blocking; returns the post's id (posts complete in order)."""
+    def post(self, frames, n: int, results, links=None) -> int:
+        """Non-blocking; returns the post's id (posts complete in order).  links (n u16, pinned host or device
+        memory): the post's chain links as well (pn_service_post_linked, n <= PN_LINK_MAX_FRAMES)."""
         pid = _u32(0)
-        _check(_pn_service_post(self._h, _ptr(frames), n, _ptr(results), _c.byref(pid)), self._ctx._h, "pn_service_post")
-        self._inflight[pid.value] = (frames, results)
+        if links is None:
+            rc = _pn_service_post(self._h, _ptr(frames), n, _ptr(results), _c.byref(pid))
+        else:
+            rc = _pn_service_post_linked(self._h, _ptr(frames), n, _ptr(results), _ptr(links), _c.byref(pid))
+        _check(rc, self._ctx._h, "pn_service_post")
+        self._inflight[pid.value] = (frames, results, links)
         return pid.value
 
     def wait(self, post_id: int = 0):
@@ -427,8 +435,8 @@ class RxService:
         for k in [k for k in self._inflight if ((last - k) & 0xFFFFFFFF) < 0x80000000]:
             del self._inflight[k]
 
-    def classify(self, frames, n: int, results):
-        self.post(frames, n, results)
+    def classify(self, frames, n: int, results, links=None):
+        self.post(frames, n, results, links)
         self.wait()
 
     def close(self):

@@ -17,7 +17,7 @@ step() {  # name, seconds, command...
   if fatal $rc; then echo "stopping after $name (rc $rc)"; tail -30 $OUT/$name.out; exit $rc; fi
   return 0
 }
-step service 300 python -u -m pytest tests/test_gpu_service.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
+step service 400 python -u -m pytest tests/test_gpu_links.py tests/test_gpu_service.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider
 tail -25 $OUT/service.out
 step tests 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider
 tail -3 $OUT/tests.out
@@ -32,3 +32,5 @@ for t in gpu reference twin; do
   python3 scripts/sample_report.py bench/bench_tcp_server $OUT/samp.$t --top 45 --lines > $OUT/profile_$t.txt 2>&1
 done
 head -40 $OUT/profile_gpu.txt
+step host_ab 400 bash scripts/host_ab.sh $TAG/ab 4 scratch_ab/srv_base scratch_ab/srv_A scratch_ab/srv_B
+cat $OUT/host_ab.out

@@ -51,17 +51,27 @@ struct OracleBackend {
   }
   std::vector<uint8_t> rx, tx;
   std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
+  std::vector<uint16_t> lk[2];     // links: each half's chain links (orc_chain_links), as the GPU's linked post
   uint32_t cap = 0;
   uint32_t tcap = 0;
+  bool links = false;
   const char* init(int, uint32_t rx_cap, uint32_t tx_cap, uint32_t = 0, uint32_t rx_halves = 1, uint32_t tx_halves = 1,
-                   bool = false) {
+                   bool = false, bool with_links = false) {
     cap = rx_cap;
     tcap = tx_cap;
+    links = with_links && rx_cap <= PN_LINK_MAX_FRAMES;
     rx.assign((size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1), 0);
     tx.assign((size_t)kStride * tx_cap * (tx_halves == 2 ? 2 : 1), 0);
-    recs[0].assign(rx_cap, pn_result{});
-    recs[1].assign(rx_cap, pn_result{});
+    for (int b = 0; b < 2; b++) {
+      recs[b].assign(rx_cap, pn_result{});
+      lk[b].assign(rx_cap, 0);
+    }
     return nullptr;
+  }
+  void chain(uint32_t half, uint32_t n, const pollnet_amd::ConnTable& t) {
+    if (links)
+      orc_chain_links(rxSlots(half), kStride, kFrameOff, n, recs[half].data(), t.maxConnCnt(), PN_LINK_MAX_FRAMES,
+                      PN_LINK_MAX_CONNS, lk[half].data());
   }
   uint8_t* rxSlots(uint32_t half = 0) { return rx.data() + (size_t)half * cap * kStride; }
   uint8_t* txSlots(uint32_t half = 0) { return tx.data() + (size_t)half * tcap * kStride; }
@@ -80,20 +90,27 @@ struct OracleBackend {
     if (verify) orc_classify_frame(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), r);
     else orc_classify_frame_release(eth, kStride - kFrameOff, e, ne, mask, t.maxConnCnt(), r);
   }
-  // sequential: each frame against the live table, just before its dispatch
+  // sequential: each frame against the live table, just before its dispatch (with links: the batch's links from its
+  // records against the table at the start, the GPU's snapshot -- the engine uses a link only while the table is the
+  // snapshot's, when the live records are those records)
   template <class F>
   const char* classify(uint32_t n, const pollnet_amd::ConnTable& t, F&& f) {
+    if (links) {
+      for (uint32_t i = 0; i < n; i++) one(rx.data() + (size_t)i * kStride + kFrameOff, t, &recs[0][i]);
+      chain(0, n, t);
+    }
     for (uint32_t i = 0; i < n; i++) {
       const uint8_t* eth = rx.data() + (size_t)i * kStride + kFrameOff;
       pn_result r;
       one(eth, t, &r);
-      f(keyOf(eth), r, eth);
+      f(keyOf(eth), r, eth, links ? lk[0][i] : (uint16_t)0);
     }
     return nullptr;
   }
   // pipelined: the whole half against the table as it is at launch (the GPU's snapshot)
   const char* launch(uint32_t half, uint32_t n, const pollnet_amd::ConnTable& t) {
     for (uint32_t i = 0; i < n; i++) one(rxSlots(half) + (size_t)i * kStride + kFrameOff, t, &recs[half][i]);
+    chain(half, n, t);
     return nullptr;
   }
   template <class F>
@@ -101,7 +118,7 @@ struct OracleBackend {
     for (uint32_t i = 0; i < n; i++) { // as GpuBackend: a hit's key is not computed (the engine derives it)
       const uint8_t* eth = rxSlots(half) + (size_t)i * kStride + kFrameOff;
       const pn_result& r = recs[half][i];
-      f((r.flags & (PN_F_HIT | PN_F_TW)) == PN_F_HIT ? 0 : keyOf(eth), r, eth);
+      f((r.flags & (PN_F_HIT | PN_F_TW)) == PN_F_HIT ? 0 : keyOf(eth), r, eth, links ? lk[half][i] : (uint16_t)0);
     }
     return nullptr;
   }

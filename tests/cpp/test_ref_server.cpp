@@ -47,6 +47,10 @@ struct ProdConf : RefConf {
 struct ProdConfResident : ProdConf {
   static const bool RxResident = true;
 };
+// ... with the chain links of each post and the in-order fast path they drive (Conf::RxLinks)
+struct ProdConfLinked : ProdConfResident {
+  static const bool RxLinks = true;
+};
 
 static const uint32_t kMaxPolls = 30000;
 
@@ -61,6 +65,7 @@ struct Transcript {
   std::string log;
   uint32_t polls = 0;
   std::vector<Client> clients;
+  uint64_t in_order = 0; // frames the product took through the in-order fast path (chain links)
 };
 
 static Transcript runRef(const std::vector<Client>& pop) {
@@ -118,6 +123,7 @@ static Transcript runProd(const std::vector<Client>& pop, bool drop_bad = true) 
   }
   t.out = srv->link().out;
   t.clients = srv->link().clients;
+  t.in_order = srv->inOrderFrames();
   return t;
 }
 
@@ -132,8 +138,10 @@ static int compare(const char* what, const Transcript& ref, const Transcript& p)
   while (same < ref.out.size() && same < p.out.size() && ref.out[same] == p.out[same]) same++;
   const bool frames_eq = same == ref.out.size() && same == p.out.size();
   const bool log_eq = ref.log == p.log;
-  std::printf("%s: %zu frames (reference %zu) %s, handler log %s (%zu B)\n", what, p.out.size(), ref.out.size(),
+  std::printf("%s: %zu frames (reference %zu) %s, handler log %s (%zu B)", what, p.out.size(), ref.out.size(),
               frames_eq ? "identical" : "DIFFERENT", log_eq ? "identical" : "DIFFERENT", ref.log.size());
+  if (p.in_order) std::printf(", %llu through the in-order fast path", (unsigned long long)p.in_order);
+  std::printf("\n");
   if (!frames_eq) {
     std::printf("  first difference at frame %zu\n", same);
     if (same < ref.out.size()) dumpFrame("reference", ref.out[same]);
@@ -367,6 +375,7 @@ int main(int argc, char** argv) {
   const uint32_t runs = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1;
   int fail = nic_queue_divergence() + rx_batch_divergence() + bad_checksum_divergence();
   if (gpu) fail += bad_checksum_divergence<GpuBackend>(" (GPU backend)");
+  uint64_t in_order_total = 0;
   for (g_seed = 0; g_seed < runs; g_seed++) {
     for (int chaos = 0; chaos < 2; chaos++) {
       std::printf("== %s population %u ==\n", chaos ? "chaos" : "peer", g_seed);
@@ -375,6 +384,10 @@ int main(int argc, char** argv) {
       if (ref.out.empty()) return 2;
       fail += coverage(ref);
       fail += compare("twin (sequential oracle backend) vs reference", ref, runProd<OracleBackend>(pop));
+      // the twin with chain links (orc_chain_links, as the resident service's linked posts): the in-order fast path
+      const Transcript tl = runProd<OracleBackend, ProdConfLinked>(pop);
+      fail += compare("twin with chain links vs reference", ref, tl);
+      in_order_total += tl.in_order;
       if (gpu) {
         fail += compare("GpuTcpServer (GPU backend) vs reference", ref, runProd<GpuBackend>(pop));
         fail += compare("GpuTcpServer (GPU backend, release path: no checksum verification) vs reference", ref,
@@ -383,9 +396,14 @@ int main(int argc, char** argv) {
                         runProd<GpuBackend, ProdConfResident>(pop));
         fail += compare("GpuTcpServer (GPU backend, resident service, release path) vs reference", ref,
                         runProd<GpuBackend, ProdConfResident>(pop, false));
+        fail += compare("GpuTcpServer (GPU backend, resident service, chain links) vs reference", ref,
+                        runProd<GpuBackend, ProdConfLinked>(pop));
+        fail += compare("GpuTcpServer (GPU backend, resident service, chain links, release path) vs reference", ref,
+                        runProd<GpuBackend, ProdConfLinked>(pop, false));
       }
     }
   }
+  if (!in_order_total) fail++, std::printf("FAIL: no frame took the in-order fast path\n");
   std::printf("%s\n", fail ? "FAIL" : "PASS");
   return fail ? 1 : 0;
 }

@@ -31,11 +31,11 @@ def csum(b: bytes, acc=0):
 
 def make_frame(src="10.0.0.2", sport=40000, dst="10.0.0.1", dport=1234, seq=0, ack=0, flags=0x18, payload=b"",
                ihl=5, doff=5, ip_opts=None, tcp_opts=None, tot_len=None, ether_type=0x0800, version=4, proto=6,
-               ttl=64, fix_ip=True, fix_tcp=True):
+               ttl=64, fix_ip=True, fix_tcp=True, window=0xFFFF):
     hl, th = 4 * ihl, 4 * doff
     ip_opts = ip_opts if ip_opts is not None else bytes([1] * max(0, hl - 20))
     tcp_opts = tcp_opts if tcp_opts is not None else bytes([1] * max(0, th - 20))
-    seg = struct.pack("!HHIIBBHHH", sport, dport, seq & 0xFFFFFFFF, ack & 0xFFFFFFFF, (doff & 15) << 4, flags, 0xFFFF, 0, 0)
+    seg = struct.pack("!HHIIBBHHH", sport, dport, seq & 0xFFFFFFFF, ack & 0xFFFFFFFF, (doff & 15) << 4, flags, window, 0, 0)
     seg += tcp_opts[: max(0, th - 20)] + payload
     real_len = max(hl, 20) + len(seg)
     tl = real_len if tot_len is None else tot_len

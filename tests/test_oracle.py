@@ -335,3 +335,63 @@ def test_unverified_record_is_full_record_less_tcp_verdict(cfg):
     exp["tcp_fold"] = 0xFFFF
     assert np.array_equal(got, exp)
     assert (full["flags"] & F.TRUNC).any() or cfg == 3
+
+
+# ---- chain links (orc_chain_links, the statement the GPU pass of pn_service_post_linked is checked against) ----
+
+def _chain(perturb=(), n_flows=4, per_flow=6, verify=True, unknown=(), tw=(), max_conn=1024, **kw):
+    import chainframes as cf
+    import pollnet_amd as pa
+
+    fr, flows = cf.build(n_flows, per_flow, perturb=perturb, unknown=unknown)
+    s = cf.slots_of(fr)
+    t = cf.table_for(pa, flows, max_conn=max_conn, tw=tw)
+    e, m = t.snapshot()
+    r = orc.classify_batch(s, STRIDE, FRAME_OFF, len(fr), e, m, t.max_conn_cnt, unverified=not verify)
+    return orc.chain_links(s, STRIDE, FRAME_OFF, len(fr), r, t.max_conn_cnt, **kw).reshape(per_flow, n_flows).T
+
+
+def test_chain_links_in_order_flows():
+    """Interleaved in-order flows: every segment but a flow's first links back to the flow's previous frame."""
+    got = _chain()
+    assert (got[:, 0] == 0).all() and (got[:, 1:] == 4).all()
+    single = _chain(n_flows=1, per_flow=40)  # one flow: each frame continues the one before it
+    assert single[0, 0] == 0 and (single[0, 1:] == 1).all()
+
+
+@pytest.mark.parametrize("kind", ["fin", "rst", "syn", "noack", "ack", "window", "dport", "pure_ack", "bad_ip"])
+def test_chain_links_broken_at_a_frame(kind):
+    """A frame TcpConn::onPack would not hand over as the next in-order segment with nothing else to do
+    (TcpConn.h:650-725): it gets no link, and neither does its successor (whose predecessor it is)."""
+    got = _chain(perturb=[(9, kind)])  # flow 1, segment 2
+    exp = np.full((4, 6), 4, np.uint16)
+    exp[:, 0] = 0
+    exp[1, 2] = exp[1, 3] = 0
+    assert np.array_equal(got, exp), (kind, got)
+
+
+def test_chain_links_hole_and_retransmission():
+    got = _chain(perturb=[(10, "hole")])  # flow 2, segment 2: 100 bytes past the next; the next frame is in order
+    assert list(got[2]) == [0, 4, 0, 0, 4, 4]  # the hole's successor does not continue the hole's frame
+    got = _chain(perturb=[(10, "retrans")])  # segment 2 repeats segment 1: its successor continues it again
+    assert list(got[2]) == [0, 4, 0, 4, 4, 4]
+
+
+def test_chain_links_tcp_verdict_by_path():
+    """A bad TCP checksum breaks the chain where the checksum is verified, not on the release path (no verdict)."""
+    assert list(_chain(perturb=[(9, "bad_tcp")])[1]) == [0, 4, 0, 0, 4, 4]
+    assert list(_chain(perturb=[(9, "bad_tcp")], verify=False)[1]) == [0, 4, 4, 4, 4, 4]
+
+
+def test_chain_links_skip_misses_and_time_wait():
+    """Frames of unknown or TIME_WAIT flows are in no chain and break none."""
+    got = _chain(unknown=(2,), tw=(3,))
+    assert (got[2] == 0).all() and (got[3] == 0).all()
+    assert (got[0, 1:] == 4).all() and (got[1, 1:] == 4).all()
+
+
+def test_chain_links_bounds():
+    """All 0 beyond the GPU pass's bounds: more frames than max_frames, or max_conn above max_conns."""
+    assert (_chain(max_frames=23) == 0).all()
+    assert (_chain(max_conn=8192) == 0).all()
+    assert (_chain(max_conn=4096) != 0).any()

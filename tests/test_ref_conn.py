@@ -44,7 +44,10 @@ def test_rx_conn_equals_reference_onpack():
 def test_server_twin_equals_reference_server():
     p = subprocess.run([_bin("test_ref_server"), "twin", "4"], capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert p.stdout.count("vs reference:") == 8, p.stdout
+    assert p.stdout.count("vs reference:") == 16, p.stdout
+    # round 6: the twin with the chain links (orc_chain_links): frames through the in-order fast path, identical
+    links = [l for l in p.stdout.splitlines() if l.startswith("twin with chain links vs reference:")]
+    assert len(links) == 8 and all("through the in-order fast path" in l for l in links), p.stdout
     assert "DIFFERENT" not in p.stdout and p.stdout.rstrip().endswith("PASS"), p.stdout
     # the intended differences, each shown: NIC-queue buffers (2 cases), frames per poll, bad checksums
     assert p.stdout.count("-> as documented") == 4, p.stdout
@@ -60,6 +63,9 @@ def test_gpu_server_equals_reference_server():
     # and with the classify in the resident service (Conf::RxResident, pn_service_*), both paths
     assert p.stdout.count("GpuTcpServer (GPU backend, resident service) vs reference") == 6, p.stdout
     assert p.stdout.count("GpuTcpServer (GPU backend, resident service, release path) vs reference") == 6, p.stdout
+    # and with the chain links of each post (Conf::RxLinks): the GPU's links drive the in-order fast path
+    res = [l for l in p.stdout.splitlines() if l.startswith("GpuTcpServer (GPU backend, resident service, chain links")]
+    assert len(res) == 12 and all("through the in-order fast path" in l for l in res), p.stdout
     assert "bad checksums (GPU backend):" in p.stdout and p.stdout.count("-> as documented") == 5, p.stdout
     assert "DIFFERENT" not in p.stdout and p.stdout.rstrip().endswith("PASS"), p.stdout
 
