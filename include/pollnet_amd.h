@@ -280,9 +280,11 @@ int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
  *   pn_service_close: waits for outstanding posts, stops the kernel, frees the service (before pn_close).
  * Post size.  Up to 4096 frames a post runs on the latency tier (a 64-frame post on one wave, no cross-wave step).
  * Above, the post also runs on helper waves, a grid launched with the post on a second stream of the service (in all
- * PN_SERVICE_WAVES_PER_CU waves per CU, 64-frame groups): the chip is not held while the service idles, and a
- * 1-Mi-frame post runs at pn_classify's rate (DESIGN.md §13 has the measured figures), so a caller need not switch
- * entry points by batch size.
+ * PN_SERVICE_WAVES_PER_CU waves per CU, 64-frame groups; the helpers take the post from their launch and wait for
+ * nothing): the chip is not held while the service idles.  Measured on MI355X (scripts/service_sizing.py, DESIGN.md
+ * §13): a 1-Mi-frame post of device-resident C2 frames, post to records complete, takes 1.15x pn_classify's launch
+ * to stream sync verified (0.300 vs 0.262 ms) and 1.27x on the release path (0.047 vs 0.037 ms); the latency tier
+ * alone (large_waves = PN_SERVICE_WAVES) takes 10x.
  * Timers.  After idle_ms (1..10000) without a post the kernel ends by itself; the next post (or wait) relaunches it.
  * A post in flight has its own limit (8 s from its acceptance): should one of its waves never finish, the kernel ends
  * and the host's next wait relaunches it, which runs the post again.  So the kernel always ends.
@@ -294,7 +296,7 @@ int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
  * Replaces the launch of the reference's per-poll work with its own busy-poll style (Core.h:494-498). */
 typedef struct pn_service pn_service;
 #define PN_SERVICE_WAVES 64u        /* the latency tier: every post of up to 4096 frames */
-#define PN_SERVICE_WAVES_PER_CU 8u  /* a large post's default wave count: this many per CU (2048 on a 256-CU MI355X) */
+#define PN_SERVICE_WAVES_PER_CU 12u /* a large post's default wave count: this many per CU (3072 on a 256-CU MI355X) */
 #define PN_SERVICE_MAX_WAVES 4096u
 #define PN_SERVICE_MAX_FRAMES (1u << 20)
 #define PN_SERVICE_STOP 0xFFFFFFFFu /* internal: the stop post */

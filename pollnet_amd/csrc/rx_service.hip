@@ -21,9 +21,10 @@
 // Large posts (round 6).  The resident kernel is the latency tier: kLatWaves (64) one-wave workgroups, which answer
 // every post of up to 4096 frames and leave the rest of the chip to other kernels while idle.  A post above that
 // also runs on helper waves: a grid the host launches with the post on a stream of its own (a launch's ~7 us is
-// nothing beside a large post's run).  The helpers wait for wave 0 to publish their post, take their share of its
-// groups as waves kLatWaves.. of it, count themselves done like the resident waves, and end.  The slot's fpw word
-// carries the helper count (bits 8+), so wave 0 knows the post's wave count.  Only vector memory operations
+// nothing beside a large post's run).  The helpers get the post in their arguments, take their share of its groups as
+// waves kLatWaves.. of it and end -- no wait, no count, no write-back of their own: the host takes the post as done
+// once the resident waves' done word and the helper grid's end are both there.  The slot's fpw word carries the
+// helper count (bits 8+), so wave 0 knows the post's wave count.  Only vector memory operations
 // (global loads / stores / one atomic add).
 #include <algorithm>
 #include <chrono>
@@ -287,14 +288,15 @@ __device__ __forceinline__ void svc_finish(const KArgsAux& a, uint16_t* links, u
 
 // a multi-wave post: count this wave done; the last one resets the count, completes the post through done word 0
 // when it has no per-wave words (svc_finish), and marks it done for wave 0 (every wave's records and chain entries
-// were made system-visible before its count: the count's order pairs them with what the last wave does next)
+// were made system-visible before its count: the count's order pairs them with what the last wave does next).  Only
+// the resident waves count (target = the post's waves in the tier); a large post's helpers run beside them.
 template <bool PASS>
-__device__ __forceinline__ void svc_count(SvcDev* dev, const KArgsAux& a, uint16_t* links, uint32_t act, uint32_t k,
-                                          uint32_t* done_word0, int lane) {
+__device__ __forceinline__ void svc_count(SvcDev* dev, const KArgsAux& a, uint16_t* links, uint32_t act,
+                                          uint32_t target, uint32_t k, uint32_t* done_word0, int lane) {
   uint32_t prev = 0;
   if (lane == 0) prev = atomicAdd(&dev->count, 1u);
   prev = __builtin_amdgcn_readfirstlane(prev);
-  if (prev == act - 1) {
+  if (prev == target - 1) { // the last of the post's resident waves (a large post's helpers do not count)
     if (lane == 0) dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
     if (act > kDoneWords || a.aux) svc_finish<PASS>(a, links, k, done_word0, lane);
     if (lane == 0) __hip_atomic_store(&dev->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -304,7 +306,8 @@ __device__ __forceinline__ void svc_count(SvcDev* dev, const KArgsAux& a, uint16
 // Wave 0 takes posts from the mailbox in order and publishes each with its wave count; a one-wave post it
 // classifies alone.  A post's waves other than 0 read it from the device copy, which wave 0 overwrites (two posts
 // later) only after every one of them counted itself done, so they always see it whole; the waves a post does not
-// run on only note it went by (from the published word alone: they may skip posts).
+// run on only note it went by (from the published word alone: they may skip posts).  The waves of a large post past
+// the tier's are the helper grid's, which needs none of this (rx_service_helper_kernel).
 // Timers: wave 0's idle limit runs from the end of the last post (or the launch); a post's limit from its
 // acceptance.  Every other wave ends on wave 0's word; its own limit is only a safety net, measured from the last post
 // it saw go by and longer than anything wave 0 can spend before publishing the next word (a post's limit, then idle).
@@ -377,7 +380,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       const KArgsAux a = svc_args(v, s, k);
       const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
       svc_run<MIS, COOP>(a, (nw & kPostVerify) != 0, a.aux != nullptr, w, act, k, s.done_words + w, lane);
-      if (act > 1) svc_count<true>(s.dev, a, svc_links(v), act, k, s.done_words, lane);
+      if (act > 1) svc_count<true>(s.dev, a, svc_links(v), act, act < W ? act : W, k, s.done_words, lane);
       else if (a.aux) svc_finish<true>(a, svc_links(v), k, s.done_words, lane);
     }
     if (w == 0) {
@@ -403,33 +406,13 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   }
 }
 
-// The helper waves of large post k: waves kLatWaves + blockIdx.x of it.  They wait for wave 0 to publish k (it does so
-// only once post k - 1 is done, so the device copy and the count are theirs), run their groups, count themselves done
-// and end.  They end at once on "idle" / "stop" or on a later post (the launch that published k is gone: the host
-// relaunches helpers with the kernel), and at their own limit, longer than anything wave 0 can take to publish k.
+// The helper waves of a large post: waves kLatWaves + blockIdx.x of it, with the post's arguments from the host (the
+// launch is issued with the post).  Their groups are theirs alone and nothing on the device waits for them: they run
+// as soon as they are scheduled, even before wave 0 has taken the post, and end; the host counts the post done once
+// their grid has ended (svc_post_done), and that end makes their records visible.
 template <int MIS, int COOP>
-__global__ __launch_bounds__(kWave) void rx_service_helper_kernel(SArgs s, uint32_t k) {
-  const int lane = threadIdx.x;
-  const uint32_t w = kLatWaves + blockIdx.x;
-  const uint64_t t0 = wall_clock64();
-  const uint64_t net = s.idle_ticks + 2 * s.post_ticks;
-  uint32_t act;
-  for (;;) {
-    const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t ck = __builtin_amdgcn_readfirstlane((uint32_t)c);
-    act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
-    if (ck == kSvcIdle || act == kSvcStop || (int32_t)(ck - k) > 0) return;
-    if (ck == k) break;
-    if (wall_clock64() - t0 > net) return;
-    __builtin_amdgcn_s_sleep(4);
-  }
-  if (w >= act) return; // never: the post's wave count includes every helper
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[k & 1]);
-  const uint32_t v = lane < 16 ? cp[lane] : 0u;
-  const KArgsAux a = svc_args(v, s, k); // never a linked post (at most kLinkFrames frames: the tier's alone)
-  svc_run<MIS, COOP, true>(a, (__builtin_amdgcn_readlane(v, 1) & kPostVerify) != 0, false, w, act, k, s.done_words, lane);
-  svc_count<false>(s.dev, a, nullptr, act, k, s.done_words, lane);
+__global__ __launch_bounds__(kWave) void rx_service_helper_kernel(KArgsAux a, uint32_t verify, uint32_t act) {
+  svc_run<MIS, COOP, true>(a, verify != 0, false, kLatWaves + blockIdx.x, act, 0, nullptr, threadIdx.x);
 }
 
 template <int MIS>
@@ -439,9 +422,9 @@ void launch_svc(bool coop, uint32_t waves, const SArgs& a, hipStream_t s) {
 }
 
 template <int MIS>
-void launch_helpers(bool coop, uint32_t helpers, const SArgs& a, uint32_t k, hipStream_t s) {
-  if (coop) hipLaunchKernelGGL((rx_service_helper_kernel<MIS, 1>), dim3(helpers), dim3(kWave), 0, s, a, k);
-  else hipLaunchKernelGGL((rx_service_helper_kernel<MIS, 0>), dim3(helpers), dim3(kWave), 0, s, a, k);
+void launch_helpers(bool coop, uint32_t helpers, const KArgsAux& a, uint32_t verify, uint32_t act, hipStream_t s) {
+  if (coop) hipLaunchKernelGGL((rx_service_helper_kernel<MIS, 1>), dim3(helpers), dim3(kWave), 0, s, a, verify, act);
+  else hipLaunchKernelGGL((rx_service_helper_kernel<MIS, 0>), dim3(helpers), dim3(kWave), 0, s, a, verify, act);
 }
 } // namespace
 
@@ -489,20 +472,35 @@ SArgs svc_sargs(const pn_service* v, uint32_t base) {
   return a;
 }
 
-// the helper grid of large post k, and the event its end completes (the post is done once both its done word and the
-// grid's end are: the helpers leave the write-back of their records to the end of their grid)
+// the helper grid of large post k (its fields already in slot k & 1), and the event its end completes: the post is
+// done once both its resident waves' done word and the grid's end are
 int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
-  const SArgs a = svc_sargs(v, 0);
+  const SvcPost* p = v->mail + (k & 1);
+  KArgsAux a;
+  a.n = p->n & kPostN;
+  a.fpw = p->fpw & 0xffu;
+  a.max_conn = p->max_conn;
+  a.frames = p->frames;
+  a.out = p->out;
+  a.tbl = p->tbl;
+  a.mask = p->mask;
+  a.n_entries = p->n_entries;
+  a.stride = v->stride;
+  a.ipa_off = (v->frame_off + 14) & ~15u;
+  a.avail = v->stride - v->frame_off;
+  a.offs = nullptr;
+  a.aux = nullptr;
+  const uint32_t verify = (p->n & kPostVerify) ? 1u : 0u, act = svc_active(a.n, a.fpw, kLatWaves + helpers);
   hipStream_t s = v->helper_stream;
   switch ((v->frame_off + 14) & 15) {
-    case 0: launch_helpers<0>(v->coop, helpers, a, k, s); break;
-    case 2: launch_helpers<2>(v->coop, helpers, a, k, s); break;
-    case 4: launch_helpers<4>(v->coop, helpers, a, k, s); break;
-    case 6: launch_helpers<6>(v->coop, helpers, a, k, s); break;
-    case 8: launch_helpers<8>(v->coop, helpers, a, k, s); break;
-    case 10: launch_helpers<10>(v->coop, helpers, a, k, s); break;
-    case 12: launch_helpers<12>(v->coop, helpers, a, k, s); break;
-    default: launch_helpers<14>(v->coop, helpers, a, k, s); break;
+    case 0: launch_helpers<0>(v->coop, helpers, a, verify, act, s); break;
+    case 2: launch_helpers<2>(v->coop, helpers, a, verify, act, s); break;
+    case 4: launch_helpers<4>(v->coop, helpers, a, verify, act, s); break;
+    case 6: launch_helpers<6>(v->coop, helpers, a, verify, act, s); break;
+    case 8: launch_helpers<8>(v->coop, helpers, a, verify, act, s); break;
+    case 10: launch_helpers<10>(v->coop, helpers, a, verify, act, s); break;
+    case 12: launch_helpers<12>(v->coop, helpers, a, verify, act, s); break;
+    default: launch_helpers<14>(v->coop, helpers, a, verify, act, s); break;
   }
   hipError_t e = hipGetLastError();
   if (e == hipSuccess && !v->helper_ev[k & 1]) e = hipEventCreateWithFlags(&v->helper_ev[k & 1], hipEventDisableTiming);
@@ -513,13 +511,10 @@ int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
 
 int svc_launch(pn_service* v, uint32_t base) {
   pn_ctx* ctx = v->ctx;
-  // the previous launch's helpers have ended (they end on its "idle" word) before the device state is reset under them
-  hipError_t e = hipStreamSynchronize(v->helper_stream);
-  if (e != hipSuccess) return hip_err(ctx, e, "pn_service: helper grids");
   SvcDev init{};
   init.cur = base;
   init.done = base;
-  e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
+  hipError_t e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(v->stream); // the previous launch has ended, the state is in place
   if (e != hipSuccess) return hip_err(ctx, e, "pn_service: device state");
   ++v->epoch;
@@ -536,14 +531,8 @@ int svc_launch(pn_service* v, uint32_t base) {
   }
   e = hipGetLastError();
   if (e != hipSuccess) return hip_err(ctx, e, "pn_service: launch");
-  v->running = true;
-  // posts issued but not completed (still in their slots) run again on this launch: their helpers with them
-  for (uint32_t k = base + 1; (int32_t)(v->seq - k) >= 0; ++k)
-    if (v->post_helpers[k & 1]) {
-      const int rc = svc_launch_helpers(v, k, v->post_helpers[k & 1]);
-      if (rc) return rc;
-    }
-  return PN_OK;
+  v->running = true; // posts issued but not completed (still in their slots) run again on this launch (their helper
+  return PN_OK;      // grids, independent of it, are not relaunched)
 }
 
 // post k (one of the last two) is complete once every done word it completes through holds k (or later): one per

@@ -128,7 +128,7 @@ _pn_service_post_linked = _sig("pn_service_post_linked", _i32, _vp, _vp, _u32, _
 _pn_service_wait = _sig("pn_service_wait", _i32, _vp, _u32)
 _pn_service_close = _sig("pn_service_close", _i32, _vp)
 PN_SERVICE_WAVES = 64
-PN_SERVICE_WAVES_PER_CU = 8
+PN_SERVICE_WAVES_PER_CU = 12
 PN_SERVICE_MAX_WAVES = 4096
 PN_LINK_MAX_FRAMES = 1024
 PN_LINK_MAX_CONNS = 4096
