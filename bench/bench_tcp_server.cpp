@@ -121,7 +121,7 @@ struct BenchLink {
   std::vector<uint32_t> cli_isn, srv_isn, sum_base; // sum_base: TCP sum of the data frame with seq = 0
   std::vector<uint8_t> payload = std::vector<uint8_t>(kPayload);
   uint64_t poll_no = 0;           // data polls so far
-  uint8_t* written[2] = {nullptr, nullptr}; // rings (halves, pipelined) whose slots hold full data frames
+  uint8_t* written[3] = {nullptr, nullptr, nullptr}; // rings (pipelined: 2 or 3) whose slots hold full data frames
   uint32_t written_n = 0;
   uint64_t acks = 0, rsts = 0, synacks = 0, other = 0;
   // echo workload: the peers acknowledge every byte the server sent them (their next frames carry it)
@@ -233,7 +233,7 @@ struct BenchLink {
     } else if (phase == Data) {
       const uint32_t per_flow = cap / n_flows;
       n = per_flow * n_flows;
-      if ((written[0] != slots && written[1] != slots) || written_n != n) { // first data poll: whole frames
+      if ((written[0] != slots && written[1] != slots && written[2] != slots) || written_n != n) { // whole frames
         for (uint32_t i = 0; i < n; i++) {
           const uint32_t f = i % n_flows;
           segtest::Seg s = seg(f, segtest::ACK | segtest::PSH, 0, 0);
@@ -246,8 +246,8 @@ struct BenchLink {
             sum_base[f] = (uint16_t)~c;
           }
         }
-        if (written_n != n) written[0] = written[1] = nullptr;
-        (written[0] ? written[1] : written[0]) = slots;
+        if (written_n != n) written[0] = written[1] = written[2] = nullptr;
+        (written[0] ? written[1] ? written[2] : written[1] : written[0]) = slots;
         written_n = n;
       }
       for (uint32_t i = 0; i < n; i++) { // seq, ack and checksum of segment k of flow f
@@ -351,8 +351,19 @@ struct TimedOracleBackend : OracleBackend {
   }
 };
 
+// The GPU backend with the host's wait for each batch's records timed (pipelined: ready() before the dispatch).
+struct TimedGpuBackend : GpuBackend {
+  double wait_s = 0;
+  const char* ready(uint32_t half) {
+    const auto t0 = Clock::now();
+    const char* e = GpuBackend::ready(half);
+    wait_s += secs(t0, Clock::now());
+    return e;
+  }
+};
+
 template <uint32_t kBatch, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false, bool kEcho = false,
-          bool kLinks = false>
+          bool kLinks = false, uint32_t kDepth = 1>
 struct Conf {
   static const uint32_t RecvBufSize = 65536;
   static const uint32_t MaxConns = 1024;
@@ -365,6 +376,7 @@ struct Conf {
   static const uint32_t TxBatch = kEcho ? 4 * kBatch : kBatch;
   static const uint32_t RxChunk = kChunk;
   static const bool RxPipeline = kPipe;
+  static const uint32_t RxPipelineDepth = kDepth; // with kPipe: polls a batch stays in flight (1 or 2)
   static const bool RxResident = kResident;
   static const bool RxLinks = kLinks; // with RxResident: the chain links and the in-order fast path
   struct UserData {};
@@ -375,6 +387,7 @@ struct Run {
   double ns_classify = -1, ns_dispatch = -1; // TimedOracleBackend: per frame, in launch() / collect()
   double in_order_share = -1;                 // frames through the in-order fast path (chain links), of all
   double echo_gbps = -1;                      // echo workload: payload bits the server sent back per second
+  double wait_us = -1;                        // TimedGpuBackend: host time per poll waiting for a batch's records
   bool ok = false;
   std::string err;
 };
@@ -382,10 +395,10 @@ struct Run {
 // verify = false: the checksum discard off, as the reference's release build runs (no checksum verified);
 // the GPU backend then classifies from each frame's header lines only (pn_set_verify)
 template <uint32_t kBatch, class Backend, uint32_t kChunk = 0, bool kPipe = false, bool kResident = false,
-          bool kEcho = false, bool kLinks = false>
+          bool kEcho = false, bool kLinks = false, uint32_t kDepth = 1>
 static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   Run out;
-  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident, kEcho, kLinks>, BenchLink, Backend>;
+  using Server = GpuTcpServer<Conf<kBatch, kChunk, kPipe, kResident, kEcho, kLinks, kDepth>, BenchLink, Backend>;
   auto srv = std::make_unique<Server>();
   srv->link().setup(n_flows);
   if (!srv->initWithLink("10.0.0.1", 1234)) {
@@ -413,16 +426,18 @@ static Run runOne(uint32_t n_flows, uint32_t polls, bool verify = true) {
   for (uint32_t p = 0; p < warm; p++) srv->poll(h);
   const uint64_t bytes0 = h.bytes, acks0 = link.acks, echo0 = link.echo_bytes;
   link.fill_s = 0;
-  pn_sampler::start(std::is_same_v<Backend, GpuBackend> ? "gpu" : "twin");
+  if constexpr (std::is_same_v<Backend, TimedGpuBackend>) srv->backend().wait_s = 0;
+  pn_sampler::start(std::is_base_of_v<GpuBackend, Backend> ? "gpu" : "twin");
   const auto t0 = Clock::now();
   for (uint32_t p = 0; p < polls; p++) srv->poll(h);
   const double t = secs(t0, Clock::now());
+  if constexpr (std::is_same_v<Backend, TimedGpuBackend>) out.wait_us = srv->backend().wait_s * 1e6 / polls;
   pn_sampler::stop();
   const uint64_t timed_bytes = h.bytes - bytes0;
   if (kEcho) out.echo_gbps = (link.echo_bytes - echo0) * 8.0 / t / 1e9;
   link.phase = BenchLink::Idle;
   // pipelined: the last batch is still in flight (echo: its replies leave a poll after their dispatch)
-  for (int k = 0; k < (kEcho ? 6 : 2); k++) srv->poll(h);
+  for (int k = 0; k < (kEcho ? 6 : 3); k++) srv->poll(h);
   const uint64_t frames = (uint64_t)polls * (kBatch / n_flows) * n_flows;
   out.mfps = frames / t / 1e6;
   out.us_poll = t * 1e6 / polls;
@@ -557,6 +572,12 @@ static std::string json(const Run& r) {
     std::snprintf(x, sizeof x, ", \"in_order_fast_path_share\": %.3f}", r.in_order_share);
     o += x;
   }
+  if (r.wait_us >= 0) {
+    o.pop_back();
+    char x[64];
+    std::snprintf(x, sizeof x, ", \"wait_us_per_poll\": %.3f}", r.wait_us);
+    o += x;
+  }
   if (r.echo_gbps >= 0) {
     o.pop_back();
     char x[96];
@@ -596,6 +617,18 @@ int main(int argc, char** argv) {
     leg("cpu_echo_512_release_path", runOne<512, OracleBackend, 0, false, false, true>(n_flows, polls, false));
 #ifdef PN_BENCH_REF
     leg("reference_server_echo_release_build", runRef(n_flows, polls, true));
+#endif
+  } else if (argc > 3 && std::strcmp(argv[3], "depth_ab") == 0) {
+    // the best leg pipelined one and two polls deep (Conf::RxPipelineDepth), the host's wait per poll timed, beside
+    // the reference's server
+    leg("gpu_rxbatch_512_pipelined_resident_release_path_timed",
+        runOne<512, TimedGpuBackend, 0, true, true>(n_flows, polls, false));
+    leg("gpu_rxbatch_512_pipelined2_resident_release_path_timed",
+        runOne<512, TimedGpuBackend, 0, true, true, false, false, 2>(n_flows, polls, false));
+    leg("gpu_rxbatch_512_pipelined2_resident_release_path",
+        runOne<512, GpuBackend, 0, true, true, false, false, 2>(n_flows, polls, false));
+#ifdef PN_BENCH_REF
+    leg("reference_server_release_build", runRef(n_flows, polls));
 #endif
   } else if (argc > 3 && std::strcmp(argv[3], "twin_timed") == 0) { // the host dispatch alone (profiling)
     leg("cpu_rxbatch_512_pipelined_release_path_timed", runOne<512, TimedOracleBackend, 0, true>(n_flows, polls, false));
@@ -667,7 +700,8 @@ int main(int argc, char** argv) {
   if (argc <= 3 || (std::strcmp(argv[3], "quick") != 0 && std::strcmp(argv[3], "release_pair") != 0 &&
                     std::strcmp(argv[3], "resident_pair") != 0 && std::strcmp(argv[3], "resident_pair_cold") != 0 &&
                     std::strcmp(argv[3], "resident_pair_l3") != 0 &&
-                    std::strcmp(argv[3], "twin_timed") != 0 && std::strcmp(argv[3], "echo") != 0)) {
+                    std::strcmp(argv[3], "twin_timed") != 0 && std::strcmp(argv[3], "echo") != 0 &&
+                    std::strcmp(argv[3], "depth_ab") != 0)) {
     leg("cpu_rxbatch_512", runOne<512, OracleBackend>(n_flows, polls));
     leg("cpu_rxbatch_512_release_path", runOne<512, OracleBackend>(n_flows, polls, false));
     leg("cpu_rxbatch_4096", runOne<4096, OracleBackend>(n_flows, polls / 4));

@@ -140,12 +140,13 @@ class GpuRx {
     if (hipSetDevice(device) != hipSuccess) return "hipSetDevice failed";
     if (hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking) != hipSuccess) return "hipStreamCreate failed";
     if (mode == Mode::ZeroCopy) {
-      if (hipHostMalloc((void**)&h_word_, 128, hipHostMallocDefault) != hipSuccess) return "hipHostMalloc(notify words) failed";
-      std::memset(h_word_, 0, 128);
+      if (hipHostMalloc((void**)&h_word_, 64 * kBufs, hipHostMallocDefault) != hipSuccess)
+        return "hipHostMalloc(notify words) failed";
+      std::memset(h_word_, 0, 64 * kBufs);
     }
     if (resident && mode == Mode::ZeroCopy && pn_service_open(ctx_, slot_stride, frame_off, resident_idle_ms, &svc_))
       return pn_last_error(ctx_);
-    for (int b = 0; b < 2; b++) {
+    for (uint32_t b = 0; b < kBufs; b++) {
       if (mode == Mode::Copy) {
         if (hipMalloc(&d_frames_[b], (size_t)slot_stride * max_batch) != hipSuccess) return "hipMalloc(frames) failed";
         if (hipMalloc(&d_res_[b], sizeof(pn_result) * (size_t)max_batch) != hipSuccess)
@@ -156,11 +157,11 @@ class GpuRx {
       if (mode == Mode::ZeroCopy &&
           hipHostMalloc(&h_offs_[b], sizeof(uint64_t) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
         return "hipHostMalloc(offsets) failed";
-      use_word_[b] = false;
+      use_word_[b] = waited_[b] = false;
       if (hipEventCreateWithFlags(&done_[b], hipEventDisableTiming) != hipSuccess) return "hipEventCreate failed";
     }
     links_ = links && svc_ && max_batch <= PN_LINK_MAX_FRAMES;
-    for (int b = 0; b < 2 && links_; b++)
+    for (uint32_t b = 0; b < kBufs && links_; b++)
       if (hipHostMalloc((void**)&h_links_[b], sizeof(uint16_t) * (size_t)max_batch, hipHostMallocDefault) != hipSuccess)
         return "hipHostMalloc(links) failed";
     return nullptr;
@@ -219,25 +220,34 @@ class GpuRx {
 
   // The two halves of pollBatch, for a caller that overlaps one batch's classify with other
   // host work (e.g. dispatching the previous batch): submit issues the classify of n <=
-  // max_batch slots into record buffer b (0 or 1; at most one batch per buffer in flight),
-  // complete waits for it and dispatches its records exactly as pollBatch does.  The slots
-  // must stay untouched in between.
+  // max_batch slots into record buffer b (0 .. kBufs - 1; at most one batch per buffer in flight),
+  // complete waits for it and dispatches its records exactly as pollBatch does; ready waits only
+  // (complete then dispatches at once).  The slots must stay untouched in between.
+  static constexpr uint32_t kBufs = 3;
   const char* submit(const uint8_t* host_slots, uint32_t n, uint32_t b) {
-    if (n > cap_ || b > 1) return "submit: n > max_batch or buffer > 1";
+    if (n > cap_ || b >= kBufs) return "submit: n > max_batch or buffer out of range";
     if (mode_ == Mode::ZeroCopy)
       if (const char* e = check_pinned(host_slots)) return e;
     const char* e = launch_at(host_slots, n, b);
     if (e) drain();
     return e;
   }
-  template <bool kHitKey = true, class RecvHandler, class TwHandler>
-  const char* complete(const uint8_t* host_slots, uint32_t n, uint32_t b, const ConnTable& table,
-                       RecvHandler&& recv_handler, TwHandler&& tw_handler) {
-    if (n > cap_ || b > 1) return "complete: n > max_batch or buffer > 1";
+  const char* ready(uint32_t b) {
+    if (b >= kBufs) return "ready: buffer out of range";
+    if (waited_[b]) return nullptr;
     if (const char* e = wait_done(b)) {
       drain();
       return e;
     }
+    waited_[b] = true;
+    return nullptr;
+  }
+  template <bool kHitKey = true, class RecvHandler, class TwHandler>
+  const char* complete(const uint8_t* host_slots, uint32_t n, uint32_t b, const ConnTable& table,
+                       RecvHandler&& recv_handler, TwHandler&& tw_handler) {
+    if (n > cap_ || b >= kBufs) return "complete: n > max_batch or buffer out of range";
+    if (const char* e = ready(b)) return e;
+    waited_[b] = false;
     auto eth_of = [&](uint32_t i) { return host_slots + (size_t)i * stride_ + off_; };
     walk<kHitKey>(h_res_[b], linked_[b] ? h_links_[b] : nullptr, 0, n, table, eth_of, recv_handler, tw_handler);
     return nullptr;
@@ -311,8 +321,10 @@ class GpuRx {
   }
   // After an error: nothing of this GpuRx left in flight (service posts waited for, the stream drained).
   void drain() {
-    for (uint32_t b = 0; b < 2; b++)
+    for (uint32_t b = 0; b < kBufs; b++) {
       if (post_[b]) (void)wait_done(b);
+      waited_[b] = false;
+    }
     (void)hipStreamSynchronize(stream_);
   }
   // Wait for buffer b's launch: its service post, its notify word, or its event.
@@ -327,7 +339,7 @@ class GpuRx {
   }
   // Issue the m slots at src into buffer b.
   const char* launch_at(const uint8_t* src, uint32_t m, uint32_t b) {
-    use_word_[b] = false;
+    use_word_[b] = waited_[b] = false;
     post_[b] = 0;
     linked_[b] = svc_ && links_;
     if (svc_) // resident service: a post, no launch
@@ -357,9 +369,9 @@ class GpuRx {
   void destruct() {
     if (svc_) (void)pn_service_close(svc_);
     svc_ = nullptr;
-    post_[0] = post_[1] = 0;
+    for (uint32_t b = 0; b < kBufs; b++) post_[b] = 0;
     if (stream_) (void)hipStreamSynchronize(stream_);
-    for (int b = 0; b < 2; b++) {
+    for (uint32_t b = 0; b < kBufs; b++) {
       if (done_[b]) (void)hipEventDestroy(done_[b]);
       if (h_res_[b]) (void)hipHostFree(h_res_[b]);
       if (h_offs_[b]) (void)hipHostFree(h_offs_[b]);
@@ -384,18 +396,19 @@ class GpuRx {
   pn_ctx* ctx_ = nullptr;
   hipStream_t stream_ = nullptr;
   Mode mode_ = Mode::Copy;
-  void* d_frames_[2] = {nullptr, nullptr};
-  pn_result* d_res_[2] = {nullptr, nullptr};
-  pn_result* h_res_[2] = {nullptr, nullptr};
-  uint64_t* h_offs_[2] = {nullptr, nullptr}; // ZeroCopy: pinned offsets the indexed kernel reads
-  hipEvent_t done_[2] = {nullptr, nullptr};
-  uint32_t* h_word_ = nullptr; // ZeroCopy: pinned notify words of buffers 0 and 1 (64 B apart)
-  uint32_t tok_[2] = {0, 0}, next_tok_ = 0;
-  bool use_word_[2] = {false, false};
+  void* d_frames_[kBufs] = {};
+  pn_result* d_res_[kBufs] = {};
+  pn_result* h_res_[kBufs] = {};
+  uint64_t* h_offs_[kBufs] = {}; // ZeroCopy: pinned offsets the indexed kernel reads
+  hipEvent_t done_[kBufs] = {};
+  uint32_t* h_word_ = nullptr; // ZeroCopy: pinned notify words of the buffers (64 B apart)
+  uint32_t tok_[kBufs] = {}, next_tok_ = 0;
+  bool use_word_[kBufs] = {};
+  bool waited_[kBufs] = {};      // buffer b's batch is complete (ready), not yet dispatched
   pn_service* svc_ = nullptr;       // resident classify service (ZeroCopy, init's `resident`)
-  uint16_t* h_links_[2] = {nullptr, nullptr}; // pinned: each buffer's chain links (init's `links`)
-  bool links_ = false, linked_[2] = {false, false}; // links on; buffer b's batch came with them
-  uint32_t post_[2] = {0, 0};       // buffer b's outstanding service post (0: none)
+  uint16_t* h_links_[kBufs] = {}; // pinned: each buffer's chain links (init's `links`)
+  bool links_ = false, linked_[kBufs] = {}; // links on; buffer b's batch came with them
+  uint32_t post_[kBufs] = {};       // buffer b's outstanding service post (0: none)
   uint32_t stride_ = 0, off_ = 0, cap_ = 0, max_conn_ = 0;
 };
 

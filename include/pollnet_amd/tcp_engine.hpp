@@ -79,6 +79,9 @@ PN_CONF_OPT(RxChunk, uint32_t, 0)           // frames per classify launch within
                                             // k+1 is on the GPU while chunk k is dispatched
 PN_CONF_OPT(RxPipeline, bool, false)        // throughput mode: a poll's frames are classified while the
                                             // previous poll's are dispatched (one poll of added latency)
+PN_CONF_OPT(RxPipelineDepth, uint32_t, 1)   // with RxPipeline: the polls a batch stays in flight before its
+                                            // dispatch, 1 or 2 (2: the GPU has two polls' host work to finish a
+                                            // batch in, one poll more of latency)
 PN_CONF_OPT(RxResident, bool, false)        // the classify runs in the resident service (pn_service_*): a post
                                             // per poll through pinned memory instead of a launch
 PN_CONF_OPT(RxLinks, bool, false)           // with RxResident: each post also returns its chain links
@@ -369,8 +372,8 @@ class GpuBackend {
   }
 
   // rx_chunk: frames per classify launch (a poll's frames go in chunks, the next one on the
-  // GPU while the host dispatches the current one; 0 = one launch per poll).  rx_halves = 2:
-  // two RX rings of rx_cap slots for launch/collect (one in flight while the other fills).
+  // GPU while the host dispatches the current one; 0 = one launch per poll).  rx_halves = 2 or 3:
+  // that many RX rings of rx_cap slots for launch/collect (one or two in flight while another fills).
   // tx_halves = 2: two TX batches (one filled on the GPU while the other is built).
   // links (with resident): the service returns each post's chain links, passed to f as a fourth argument
   const char* init(int device, uint32_t rx_cap, uint32_t tx_cap, uint32_t rx_chunk = 0, uint32_t rx_halves = 1,
@@ -388,7 +391,8 @@ class GpuBackend {
       return "hipStreamCreate(tx) failed";
     rx_cap_ = rx_cap;
     tx_cap_ = tx_cap;
-    const size_t rx_bytes = (size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1);
+    if (rx_halves < 1 || rx_halves > GpuRx::kBufs) return "rx_halves out of range";
+    const size_t rx_bytes = (size_t)kStride * rx_cap * rx_halves;
     const size_t tx_bytes = (size_t)kStride * tx_cap * (tx_halves == 2 ? 2 : 1);
     if (hipHostMalloc((void**)&rx_ring_, rx_bytes, hipHostMallocDefault) != hipSuccess)
       return "hipHostMalloc(rx ring) failed";
@@ -413,6 +417,8 @@ class GpuBackend {
   // device (syncTable); collect waits for it and calls f(key, rec, eth, link) in ring order (link: the frame's chain
   // link, 0 without links).
   const char* launch(uint32_t half, uint32_t n, const ConnTable&) { return rx_.submit(rxSlots(half), n, half); }
+  // wait for a launched half without dispatching it (collect then dispatches at once)
+  const char* ready(uint32_t half) { return rx_.ready(half); }
   template <class F>
   const char* collect(uint32_t half, uint32_t n, const ConnTable& t, F&& f) {
     return rx_.template complete<false>(
@@ -505,6 +511,9 @@ class TcpEngine {
   static constexpr uint32_t kRxChunk = srv_detail::opt_RxChunk<Conf>::value;
   static constexpr bool kRxPipeline = srv_detail::opt_RxPipeline<Conf>::value;
   static_assert(!(kRxPipeline && kRxChunk), "RxPipeline and RxChunk are alternatives");
+  static constexpr uint32_t kRxDepth = kRxPipeline ? srv_detail::opt_RxPipelineDepth<Conf>::value : 0;
+  static_assert(!kRxPipeline || kRxDepth == 1 || kRxDepth == 2, "RxPipelineDepth is 1 or 2");
+  static constexpr uint32_t kRxBufs = kRxDepth + 1; // RX rings: the one filling, the batches in flight
   static constexpr uint32_t kSendTimeoutMs = srv_detail::opt_SendTimeoutSec<Conf>::value * 1000;
   static constexpr uint32_t kRecvTimeoutMs = srv_detail::opt_RecvTimeoutSec<Conf>::value * 1000;
   static_assert(kSendBufCnt >= 4 && !(kSendBufCnt & (kSendBufCnt - 1)), "ConnSendBufCnt must be a power of 2");
@@ -760,7 +769,7 @@ class TcpEngine {
     }
     std::memcpy(local_mac_, link_.localMac(), 6);
     if (const char* e = table_.init(kMaxConn, kMaxTw, srv_detail::opt_ReferenceLiteralTable<Conf>::value)) return e;
-    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxPipeline ? 2 : 1,
+    if (const char* e = be_.init(srv_detail::opt_Device<Conf>::value, kRxBatch, kTxBatch, kRxChunk, kRxBufs,
                                  kRxPipeline ? 2 : 1, srv_detail::opt_RxResident<Conf>::value,
                                  srv_detail::opt_RxResident<Conf>::value && srv_detail::opt_RxLinks<Conf>::value))
       return e;
@@ -796,7 +805,8 @@ class TcpEngine {
       v.clear();
       v.reserve(kTxBatch);
     }
-    fl_n_[0] = fl_n_[1] = 0;
+    for (auto& f : fl_n_) f = 0;
+    fl_head_ = fl_cnt_ = 0;
     ++tver_;
     ready_ = true;
     return nullptr;
@@ -878,21 +888,30 @@ class TcpEngine {
     };
     if constexpr (kRxPipeline) {
       // launch this poll's frames; send what the previous poll built (its checksum fill ran
-      // meanwhile); dispatch the previous poll's frames while this poll's are classified; start
-      // the fill of what this poll built
+      // meanwhile); dispatch the oldest batch in flight -- launched kRxDepth polls ago, or any
+      // when no frames came -- while the newer ones are classified; start the fill of what this
+      // poll built.  At depth 2 the oldest batch is waited for before the launch: a resident
+      // service takes a post only with at most one other outstanding.
       if (n) {
+        if (kRxDepth == 2 && fl_cnt_ == 2)
+          if ((err_ = be_.ready(fl_head_))) return;
         if ((err_ = be_.launch(cur_, n, table_))) return;
         fl_n_[cur_] = n;
         fl_ver_[cur_] = tver_;
+        ++fl_cnt_;
       }
       completeTx();
-      const uint32_t prev = cur_ ^ 1;
-      if (const uint32_t m = fl_n_[prev]) {
-        fl_n_[prev] = 0;
-        disp_ver_ = fl_ver_[prev];
-        if (const char* e = be_.collect(prev, m, table_, frame)) err_ = e;
+      if (fl_cnt_ > (n ? kRxDepth : 0)) {
+        const uint32_t old = fl_head_, m = fl_n_[old];
+        fl_n_[old] = 0;
+        fl_head_ = old + 1 == kRxBufs ? 0 : old + 1;
+        --fl_cnt_;
+        disp_ver_ = fl_ver_[old];
+        if (const char* e = be_.ready(old)) err_ = e;
+        else if (const char* e2 = be_.collect(old, m, table_, frame)) err_ = e2;
       }
-      if (n) cur_ ^= 1;
+      cur_ = fl_head_ + fl_cnt_;
+      if (cur_ >= kRxBufs) cur_ -= kRxBufs;
       launchTx();
     } else {
       if (n) {
@@ -1513,8 +1532,9 @@ class TcpEngine {
   uint8_t local_mac_[6] = {};
   // table versions: tver_ counts table changes; synced_ver_ is the device snapshot's, disp_ver_
   // that of the records being dispatched; fl_* the pipelined batch in flight per ring half
-  uint64_t tver_ = 1, synced_ver_ = 0, disp_ver_ = 0, fl_ver_[2] = {0, 0};
-  uint32_t cur_ = 0, fl_n_[2] = {0, 0};
+  uint64_t tver_ = 1, synced_ver_ = 0, disp_ver_ = 0, fl_ver_[3] = {0, 0, 0};
+  // RX rings: cur_ is filling; fl_cnt_ batches in flight from fl_head_ on (pipelined), fl_n_ frames each
+  uint32_t cur_ = 0, fl_n_[3] = {0, 0, 0}, fl_head_ = 0, fl_cnt_ = 0;
   uint32_t tx_cur_ = 0, tx_fl_n_ = 0; // TX batch being built; frames of the other one in its fill (pipelined)
   uint8_t* tx_base_[2] = {nullptr, nullptr}; // be_.txSlots(half) + kFrameOff, set at init
   uint32_t tx_data_n_ = 0;            // payload-bearing frames in the batch being built

@@ -50,8 +50,8 @@ struct OracleBackend {
     return nullptr;
   }
   std::vector<uint8_t> rx, tx;
-  std::vector<pn_result> recs[2]; // pipelined: each half's records, classified at launch
-  std::vector<uint16_t> lk[2];     // links: each half's chain links (orc_chain_links), as the GPU's linked post
+  std::vector<pn_result> recs[3]; // pipelined: each ring's records, classified at launch
+  std::vector<uint16_t> lk[3];     // links: each ring's chain links (orc_chain_links), as the GPU's linked post
   uint32_t cap = 0;
   uint32_t tcap = 0;
   bool links = false;
@@ -60,9 +60,10 @@ struct OracleBackend {
     cap = rx_cap;
     tcap = tx_cap;
     links = with_links && rx_cap <= PN_LINK_MAX_FRAMES;
-    rx.assign((size_t)kStride * rx_cap * (rx_halves == 2 ? 2 : 1), 0);
+    if (rx_halves < 1 || rx_halves > 3) return "rx_halves out of range";
+    rx.assign((size_t)kStride * rx_cap * rx_halves, 0);
     tx.assign((size_t)kStride * tx_cap * (tx_halves == 2 ? 2 : 1), 0);
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < 3; b++) {
       recs[b].assign(rx_cap, pn_result{});
       lk[b].assign(rx_cap, 0);
     }
@@ -113,6 +114,7 @@ struct OracleBackend {
     chain(half, n, t);
     return nullptr;
   }
+  const char* ready(uint32_t) { return nullptr; } // classified at launch
   template <class F>
   const char* collect(uint32_t half, uint32_t n, const pollnet_amd::ConnTable&, F&& f) {
     for (uint32_t i = 0; i < n; i++) { // as GpuBackend: a hit's key is not computed (the engine derives it)

@@ -69,6 +69,13 @@ struct PeerConfResident : PeerConf {
 struct PeerConfPipeResident : PeerConfPipe {
   static const bool RxResident = true;
 };
+// pipelined two polls deep (Conf::RxPipelineDepth 2: three RX rings, two batches in flight)
+struct PeerConfPipe2 : PeerConfPipe {
+  static const uint32_t RxPipelineDepth = 2;
+};
+struct PeerConfPipe2Resident : PeerConfPipe2 {
+  static const bool RxResident = true;
+};
 
 template <class Backend, class Conf = PeerConf>
 struct Run {
@@ -281,6 +288,8 @@ int main(int argc, char** argv) {
     fail += scenario<PeerConfPipe>(gpu, pop, "pipelined RX (dispatch one poll later)");
     fail += scenario<PeerConfResident>(gpu, pop, "resident service, every poll");
     fail += scenario<PeerConfPipeResident>(gpu, pop, "resident service, pipelined RX");
+    fail += scenario<PeerConfPipe2>(gpu, pop, "pipelined RX two polls deep");
+    fail += scenario<PeerConfPipe2Resident>(gpu, pop, "resident service, pipelined RX two polls deep");
     if (g_seed == 0) fail += wrapper_admission(gpu, pop);
   }
   std::printf("%s\n", fail ? "FAIL" : "PASS");
