@@ -2,6 +2,7 @@
 // answered by the GPU into pinned host memory, the host spinning on the answer.
 //   launch:     one kernel launch per request (answers the value and ends) -- what pn_classify_notify pays
 //   resident:   one resident kernel polling the doorbell (pn_test_doorbell_echo), with / without s_sleep
+//   pipe_dK_gG: the pipelined poll (pn_test_doorbell_echo_pipe): K reads in flight, G x 64 clocks apart (round 6)
 // Prints one JSON line: median / p90 microseconds per round trip.   argv: iterations (2000)
 #include <hip/hip_runtime.h>
 
@@ -66,7 +67,34 @@ int main(int argc, char** argv) {
     __atomic_store_n(bell, 0xFFFFFFFFu, __ATOMIC_RELEASE); // stop
     if (hipStreamSynchronize(s) != hipSuccess) return 5;
     if (!ok) return 6;
-    stats(sl ? "resident_sleep" : "resident_spin", us, sl == 1);
+    stats(sl ? "resident_sleep" : "resident_spin", us, false);
+  }
+  // the pipelined poll: the host waits a random 0-3 us between requests, so a request lands at any phase of the polls
+  const struct { int depth; uint32_t gap; } grid[] = {{1, 0}, {2, 4}, {2, 8}, {4, 2}, {4, 4}, {4, 8}, {8, 1}, {8, 2}, {8, 4}};
+  uint32_t rnd = 12345;
+  const int n_grid = (int)(sizeof grid / sizeof grid[0]);
+  for (int g = 0; g < n_grid; g++) {
+    __atomic_store_n(bell, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(echo, 0u, __ATOMIC_RELEASE);
+    if (pn_test_doorbell_echo_pipe(bell, echo, 200, grid[g].depth, grid[g].gap, s)) return 3;
+    std::vector<double> us;
+    bool ok = true;
+    for (int i = 1; i <= iters + 50 && ok; i++) {
+      rnd = rnd * 1664525u + 1013904223u;
+      const auto tw = Clock::now() + std::chrono::nanoseconds((rnd >> 8) % 3000);
+      while (Clock::now() < tw) {
+      }
+      const auto t0 = Clock::now();
+      __atomic_store_n(bell, (uint32_t)i, __ATOMIC_RELEASE);
+      ok = spin(echo, (uint32_t)i);
+      if (i > 50) us.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t0).count());
+    }
+    __atomic_store_n(bell, 0xFFFFFFFFu, __ATOMIC_RELEASE); // stop
+    if (hipStreamSynchronize(s) != hipSuccess) return 5;
+    if (!ok) return 6;
+    char name[32];
+    std::snprintf(name, sizeof name, "pipe_d%d_g%u", grid[g].depth, grid[g].gap);
+    stats(name, us, g == n_grid - 1);
   }
   std::printf("}\n");
   (void)hipStreamDestroy(s);

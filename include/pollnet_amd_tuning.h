@@ -58,6 +58,11 @@ int pn_test_spin_wait(const uint32_t* go_host, uint32_t* done_host, uint32_t max
  * the current value and end.  sleep != 0: s_sleep between polls. */
 int pn_test_doorbell_echo(const uint32_t* bell_host, uint32_t* echo_host, uint32_t max_idle_ms, int once, int sleep,
                           void* stream);
+/* The same answered from a pipelined poll (round 6): `depth` (1, 2, 4 or 8) reads of *bell_host in flight, a new one
+ * issued `gap` x 64 clocks after the last, each checked when it returns -- a new value is seen within about one gap
+ * of its arrival instead of up to a whole PCIe read round trip.  Values must increase (stale reads are ignored). */
+int pn_test_doorbell_echo_pipe(const uint32_t* bell_host, uint32_t* echo_host, uint32_t max_idle_ms, int depth,
+                               uint32_t gap, void* stream);
 
 /* ---- A/B variants (built by default, TUNING=1; ids documented at their definitions) ---- */
 int pn_classify_variant(pn_ctx* ctx, const void* frames_dev, uint32_t slot_stride, uint32_t frame_off, uint32_t n,

@@ -65,6 +65,45 @@ __global__ __launch_bounds__(64) void doorbell_echo_kernel(const uint32_t* bell,
   }
 }
 
+// The doorbell answered from a pipelined poll: K relaxed system-scope reads of the bell's 64-B line in flight (lane
+// i reads word i & 15: the service mailbox's shape, no branch around the load), issued `gap` x 64 clocks apart; each is checked when it returns (the
+// value stays in a VGPR until its readlane, so the compiler waits for the oldest read only: vmcnt(K - 1)).  A new
+// value is seen about one gap after it lands rather than up to one read round trip later.  Reads issued before a value
+// arrived return older values: only a larger value counts.
+template <int K>
+__global__ __launch_bounds__(64) void doorbell_echo_pipe_kernel(const uint32_t* bell, uint32_t* echo,
+                                                                uint64_t max_idle_ticks, uint32_t gap) {
+  const int lane = threadIdx.x;
+  uint32_t last = 0;
+  uint64_t t_last = wall_clock64();
+  uint32_t q[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    q[j] = __hip_atomic_load(bell + (lane & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t g = 0; g < gap; ++g) __builtin_amdgcn_s_sleep(1);
+  }
+  // no return inside the loop: an exit path there makes the compiler drain every read at the loop head (vmcnt(0))
+  bool go = true;
+  while (go) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readlane(q[j], 0);
+      if (v == 0xFFFFFFFFu) {
+        go = false;
+      } else if ((int32_t)(v - last) > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        last = v;
+        if (lane == 0) __hip_atomic_store(echo, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        t_last = wall_clock64();
+      } else if (wall_clock64() - t_last > max_idle_ticks) {
+        go = false;
+      }
+      q[j] = __hip_atomic_load(bell + (lane & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      for (uint32_t g = 0; g < gap; ++g) __builtin_amdgcn_s_sleep(1);
+    }
+  }
+}
+
 // Read-only ceilings for the slot layout (no header work, no arithmetic): each wave
 // streams the first `bytes` of each of its 64 slots with the RX kernel's 1-KiB
 // buffer loads, 8 slots per batch.  STORE = 16 / 8: plus a per-slot record store
@@ -497,6 +536,27 @@ int pn_test_doorbell_echo(const uint32_t* bell_host, uint32_t* echo_host, uint32
                      (uint64_t)khz * max_idle_ms, (uint32_t)(once != 0), (uint32_t)(sleep != 0));
   e = hipGetLastError();
   return e == hipSuccess ? PN_OK : hip_err(nullptr, e, "doorbell_echo launch");
+}
+
+int pn_test_doorbell_echo_pipe(const uint32_t* bell_host, uint32_t* echo_host, uint32_t max_idle_ms, int depth,
+                               uint32_t gap, void* stream) {
+  if (!bell_host || !echo_host || max_idle_ms == 0 || max_idle_ms > 10000 || gap > 64 ||
+      (depth != 1 && depth != 2 && depth != 4 && depth != 8))
+    return set_err(nullptr, PN_EINVAL, "pn_test_doorbell_echo_pipe: bell/echo, max_idle_ms in [1, 10000], depth 1/2/4/8, gap <= 64");
+  int dev = 0, khz = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess || khz <= 0) return hip_err(nullptr, e, "wall clock rate");
+  const uint64_t t = (uint64_t)khz * max_idle_ms;
+  const hipStream_t s = (hipStream_t)stream;
+  switch (depth) {
+    case 1: hipLaunchKernelGGL(doorbell_echo_pipe_kernel<1>, dim3(1), dim3(64), 0, s, bell_host, echo_host, t, gap); break;
+    case 2: hipLaunchKernelGGL(doorbell_echo_pipe_kernel<2>, dim3(1), dim3(64), 0, s, bell_host, echo_host, t, gap); break;
+    case 4: hipLaunchKernelGGL(doorbell_echo_pipe_kernel<4>, dim3(1), dim3(64), 0, s, bell_host, echo_host, t, gap); break;
+    default: hipLaunchKernelGGL(doorbell_echo_pipe_kernel<8>, dim3(1), dim3(64), 0, s, bell_host, echo_host, t, gap);
+  }
+  e = hipGetLastError();
+  return e == hipSuccess ? PN_OK : hip_err(nullptr, e, "doorbell_echo_pipe launch");
 }
 
 int pn_calib_stream_read(pn_ctx* ctx, const void* src_dev, uint64_t bytes, void* sink_dev, void* stream) {
