@@ -205,4 +205,13 @@ ref:
 clean:
 	rm -f $(LIB) $(GEN_LIB) $(TUNING_LIB) $(ORACLE) oracle/_ref/*.so $(CPPTEST) $(RXCONNTEST) $(TCPRXTEST) $(TCPRXBENCH) $(LATBENCH) $(SRVBENCH) $(PINBENCH) $(SIGBENCH) $(STREAMBENCH) $(DOORBENCH) $(TXSMALLBENCH) $(RINGTEST) $(STREAMTEST) $(GPUSTREAMTEST) $(SERVERTEST) $(PEERTEST) $(CLISRVTEST) $(TXHOSTTEST) $(REFSERVERTEST) $(REFCONNTEST) $(REFCLIENTTEST)
 
-.PHONY: all ref clean
+.PHONY: all ref clean svc_trace
+
+# Measurement build of the service with its step clocks (-DPN_SVC_TRACE) and the driver that reads them; not in `all`
+svc_trace: ab_libs/trace/libpollnet_amd.so bench/svc_trace
+ab_libs/trace/libpollnet_amd.so: $(SRCS) $(HDRS) $(KHDRS)
+	mkdir -p ab_libs/trace
+	$(HIPCC) $(HIPFLAGS) -DPN_SVC_TRACE -shared -o $@ $(SRCS) -lpthread
+bench/svc_trace: bench/svc_trace.cpp ab_libs/trace/libpollnet_amd.so $(GEN_LIB)
+	$(HOSTHIP) -O2 -std=c++17 -Wall -o $@ $< -Lab_libs/trace -lpollnet_amd -Lpollnet_amd -lpollnet_amd_gen \
+	  -Wl,-rpath,'$$ORIGIN/../ab_libs/trace' -Wl,-rpath,'$$ORIGIN/../pollnet_amd'

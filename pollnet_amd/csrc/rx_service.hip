@@ -72,6 +72,21 @@ struct alignas(64) SvcDev { // device memory, set by the host before every launc
   SvcPost post[2];
 };
 
+// Measurement build only (-DPN_SVC_TRACE, bench/svc_trace.cpp): lane 0 of each wave stores the device wall clock at
+// the protocol's steps to pinned host memory (pn_svc_trace_set); compiled out of the product.  Plain stores: a step
+// before the wave's system fence reaches the host with the post, a later one only with the next post's fence.
+#ifdef PN_SVC_TRACE
+__device__ uint64_t* g_svc_trace = nullptr;
+#define SVC_T(w, i)                                                       \
+  do {                                                                    \
+    if (lane == 0 && (w) < 64) g_svc_trace[(w) * 8 + (i)] = wall_clock64(); \
+  } while (0)
+#else
+#define SVC_T(w, i) \
+  do {              \
+  } while (0)
+#endif
+
 struct SArgs {
   const SvcPost* mail;  // host: the two mailbox slots
   u32x4* scratch;       // device: per mailbox slot, kLinkFrames x 2 chain entries (kChainAux)
@@ -344,7 +359,9 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
+      SVC_T(0, 0);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
+      SVC_T(0, 1);
       t_acc = wall_clock64();
       const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
       if (nw == PN_SERVICE_STOP) {
@@ -357,6 +374,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[k & 1])[lane] = v;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)act << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        SVC_T(0, 2);
       }
       run = true;
     } else {
@@ -370,7 +388,9 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         continue;
       }
       if (w < act) { // this wave runs on post k: wave 0 waits for it before the next post, so k is current
+        SVC_T(w, 0);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        SVC_T(w, 1);
         const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[k & 1]);
         v = lane < 16 ? cp[lane] : 0u;
         run = true;
@@ -378,10 +398,13 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
     }
     if (run) { // one call site for every wave (the classify code is inlined once per path)
       const KArgsAux a = svc_args(v, s, k);
+      SVC_T(w, 5);
       const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
       svc_run<MIS, COOP>(a, (nw & kPostVerify) != 0, a.aux != nullptr, w, act, k, s.done_words + w, lane);
+      SVC_T(w, 6);
       if (act > 1) svc_count<true>(s.dev, a, svc_links(v), act, act < W ? act : W, k, s.done_words, lane);
       else if (a.aux) svc_finish<true>(a, svc_links(v), k, s.done_words, lane);
+      SVC_T(w, 7);
     }
     if (w == 0) {
       if (act == 1) { // one wave's work, done: let the others see it go by
@@ -400,6 +423,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
+      SVC_T(0, 4);
     }
     last = k;
     t0 = wall_clock64();
@@ -756,3 +780,11 @@ int pn_service_close(pn_service* v) {
 }
 
 } // extern "C"
+
+#ifdef PN_SVC_TRACE
+// measurement build only: where the service kernels store their step clocks (64 waves x 8 u64, pinned host memory);
+// set before pn_service_open
+extern "C" int pn_svc_trace_set(uint64_t* host_buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_svc_trace), &host_buf, sizeof host_buf) == hipSuccess ? PN_OK : PN_EHIP;
+}
+#endif
