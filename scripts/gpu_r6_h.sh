@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 6: the service's device line carries its own tag (no release fence on publish, none on `done`): the service
-# and link tests first, then the post round trips (bench_signal) of the previous library (ab_libs/old) and this one,
-# interleaved, and the device step clocks (svc_trace).   bash scripts/gpu_r6_h.sh <tag>
+# Round 6: a service A/B -- the service and link tests, the post round trips (bench_signal) of the previous library
+# (ab_libs/old) and this one, interleaved, and the device step clocks (svc_trace).  Used for the tagged-line publish
+# (r6h2) and the XCD-aware wave ranks (r6h3).   bash scripts/gpu_r6_h.sh <tag>
 set -o pipefail
 TAG=${1:-r6h2}
 OUT=gpurun_out/$TAG
