@@ -277,6 +277,9 @@ int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
  *     names the post.  Frames and results must stay valid until the post completes.
  *   pn_service_wait: spins until post post_id's records are visible to the host (as pn_classify_notify's word);
  *     posts complete in order; post_id 0 = the last post.
+ *   Post ids count up by one per post and wrap at 2^32: every value, 0 included, is a post's id (so "0 = the last
+ *     post" waits at least as long as the post named 0).  PN_SERVICE_FIRST_POST in the environment at open sets the
+ *     count's start (tests start it just below 2^32).
  *   pn_service_close: waits for outstanding posts, stops the kernel, frees the service (before pn_close).
  * Post size.  Up to 4096 frames a post runs on the latency tier (a 64-frame post on one wave, no cross-wave step).
  * Above, the post also runs on helper waves, a grid launched with the post on a second stream of the service (in all

@@ -322,17 +322,16 @@ class GpuRx {
   // After an error: nothing of this GpuRx left in flight (service posts waited for, the stream drained).
   void drain() {
     for (uint32_t b = 0; b < kBufs; b++) {
-      if (post_[b]) (void)wait_done(b);
+      if (posted_[b]) (void)wait_done(b);
       waited_[b] = false;
     }
     (void)hipStreamSynchronize(stream_);
   }
   // Wait for buffer b's launch: its service post, its notify word, or its event.
   const char* wait_done(uint32_t b) {
-    if (post_[b]) {
-      const uint32_t id = post_[b];
-      post_[b] = 0;
-      return pn_service_wait(svc_, id) ? pn_last_error(ctx_) : nullptr;
+    if (posted_[b]) {
+      posted_[b] = false;
+      return pn_service_wait(svc_, post_[b]) ? pn_last_error(ctx_) : nullptr;
     }
     if (use_word_[b]) return wait_word(&h_word_[16 * b], tok_[b], stream_);
     return hipEventSynchronize(done_[b]) == hipSuccess ? nullptr : "hipEventSynchronize failed";
@@ -340,12 +339,14 @@ class GpuRx {
   // Issue the m slots at src into buffer b.
   const char* launch_at(const uint8_t* src, uint32_t m, uint32_t b) {
     use_word_[b] = waited_[b] = false;
-    post_[b] = 0;
+    posted_[b] = false;
     linked_[b] = svc_ && links_;
-    if (svc_) // resident service: a post, no launch
-      return pn_service_post_linked(svc_, src, m, h_res_[b], links_ ? h_links_[b] : nullptr, &post_[b])
-                 ? pn_last_error(ctx_)
-                 : nullptr;
+    if (svc_) { // resident service: a post, no launch
+      if (pn_service_post_linked(svc_, src, m, h_res_[b], links_ ? h_links_[b] : nullptr, &post_[b]))
+        return pn_last_error(ctx_);
+      posted_[b] = true;
+      return nullptr;
+    }
     if (mode_ == Mode::ZeroCopy && m <= PN_NOTIFY_MAX_FRAMES) { // small batch: completion by a pinned word
       tok_[b] = ++next_tok_;
       if (pn_classify_notify(ctx_, src, stride_, off_, m, h_res_[b], stream_, &h_word_[16 * b], tok_[b]))
@@ -369,7 +370,7 @@ class GpuRx {
   void destruct() {
     if (svc_) (void)pn_service_close(svc_);
     svc_ = nullptr;
-    for (uint32_t b = 0; b < kBufs; b++) post_[b] = 0;
+    for (uint32_t b = 0; b < kBufs; b++) posted_[b] = false;
     if (stream_) (void)hipStreamSynchronize(stream_);
     for (uint32_t b = 0; b < kBufs; b++) {
       if (done_[b]) (void)hipEventDestroy(done_[b]);
@@ -408,7 +409,8 @@ class GpuRx {
   pn_service* svc_ = nullptr;       // resident classify service (ZeroCopy, init's `resident`)
   uint16_t* h_links_[kBufs] = {}; // pinned: each buffer's chain links (init's `links`)
   bool links_ = false, linked_[kBufs] = {}; // links on; buffer b's batch came with them
-  uint32_t post_[kBufs] = {};       // buffer b's outstanding service post (0: none)
+  uint32_t post_[kBufs] = {};       // buffer b's service post (every 32-bit id is one: the counter wraps)
+  bool posted_[kBufs] = {};         // ... and whether it is outstanding
   uint32_t stride_ = 0, off_ = 0, cap_ = 0, max_conn_ = 0;
 };
 

@@ -28,6 +28,7 @@
 // (global loads / stores / one atomic add).
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 
 #include "rx_classify.hpp"
 
@@ -60,8 +61,11 @@ constexpr uint32_t kLatFrames = kLatWaves * kFramesPerWave; // the largest post 
 constexpr uint32_t kPostLimitMs = 8000; // a post in flight (pn_service_wait gives up at 10 s)
 constexpr uint32_t kPostVerify = 1u << 30, kPostLinks = 1u << 29, kPostN = (1u << 21) - 1; // the n word
 constexpr uint32_t kLinkFrames = PN_LINK_MAX_FRAMES, kLinkConns = PN_LINK_MAX_CONNS;
-constexpr uint32_t kSvcIdle = 0xFFFFFFFFu; // published as the post when wave 0 ends for lack of posts
-constexpr uint32_t kSvcStop = 0xFFFFFFFFu; // published as the wave count of a stop post
+// Published in the wave-count half of `cur` (a real post runs on at most PN_SERVICE_MAX_WAVES): every 32-bit post id
+// is a valid post, the counter wraps (2^32 posts: 11 hours at 100k posts/s)
+constexpr uint32_t kSvcIdle = 0xFFFFFFFEu; // wave 0 ended: no post for idle_ms, or a post past its limit
+constexpr uint32_t kSvcStop = 0xFFFFFFFFu; // a stop post
+static_assert(PN_SERVICE_MAX_WAVES < kSvcIdle, "wave counts below the idle / stop marks");
 
 struct alignas(64) SvcDev { // device memory, set by the host before every launch
   uint64_t cur;             // wave 0 publishes (waves << 32) | post: the post and how many waves it runs on
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
           (uint32_t)__builtin_amdgcn_readlane(v, 14) != x) {
         if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
           if (lane == 0) {
-            __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           }
           return;
@@ -381,7 +385,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       k = __builtin_amdgcn_readfirstlane((uint32_t)c);
       act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
-      if (k == kSvcIdle || act == kSvcStop) return;
+      if (act >= kSvcIdle) return; // idle or stop
       if (k == last) {
         if (wall_clock64() - t0 > net) return; // a safety net: wave 0 always publishes kSvcIdle first
         __builtin_amdgcn_s_sleep(2);
@@ -414,7 +418,7 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
                k) {
           if (wall_clock64() - t_acc > s.post_ticks) { // a wave of the post never finished: give up, and say so
             if (lane == 0) {
-              __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+              __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
               __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             return;
@@ -657,9 +661,16 @@ int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, ui
     svc_free(v);
     return rc;
   }
+  // The post counter's start: 0, or PN_SERVICE_FIRST_POST from the environment (tests start it just below 2^32 to
+  // run the counter's wrap).  The done words and both slots hold it: neither slot reads as post first + 1 or + 2.
+  uint32_t first = 0;
+  if (const char* env = std::getenv("PN_SERVICE_FIRST_POST")) first = (uint32_t)std::strtoull(env, nullptr, 0);
   std::memset(v->mail, 0, 2 * sizeof(SvcPost));
   std::memset(v->words, 0, kWordsBytes);
-  const int rc = svc_launch(v, 0);
+  for (uint32_t w = 0; w < kDoneWords; ++w) v->words[w] = first;
+  for (int i = 0; i < 2; ++i) v->mail[i].gen = v->mail[i].seq = first;
+  v->seq = first;
+  const int rc = svc_launch(v, first);
   if (rc) {
     svc_free(v);
     return rc;

@@ -414,6 +414,7 @@ class RxService:
                "pn_service_open")
         self._h, self._ctx = h, ctx
         self._inflight = {}  # post id -> (frames, results): alive until the post completes
+        self._last = None  # the last post's id (ids wrap at 2^32: "the last" is not the largest)
 
     def post(self, frames, n: int, results, links=None) -> int:
         """Non-blocking; returns the post's id (posts complete in order).  links (n u16, pinned host or device
@@ -425,13 +426,16 @@ class RxService:
             rc = _pn_service_post_linked(self._h, _ptr(frames), n, _ptr(results), _ptr(links), _c.byref(pid))
         _check(rc, self._ctx._h, "pn_service_post")
         self._inflight[pid.value] = (frames, results, links)
+        self._last = pid.value
         return pid.value
 
     def wait(self, post_id: int = 0):
         """Until post post_id's records are visible (0: the last post)."""
         _check(_pn_service_wait(self._h, post_id), self._ctx._h, "pn_service_wait")
         # posts complete in order: every post up to the one waited for is done
-        last = post_id or max(self._inflight, default=0)
+        last = post_id or self._last
+        if last is None:
+            return
         for k in [k for k in self._inflight if ((last - k) & 0xFFFFFFFF) < 0x80000000]:
             del self._inflight[k]
 

@@ -515,3 +515,46 @@ def test_service_soak_large_posts_and_relaunches(torch, big):
             svc.close()
     finally:
         ctx.close()
+
+
+def test_service_post_ids_wrap(torch, big, monkeypatch):
+    """The post counter wraps at 2^32 (11 hours of posts at 100k a second): a service started just below it
+    (PN_SERVICE_FIRST_POST) takes posts 0xFFFFFFF1 .. 0x30 -- ids 0xFFFFFFFE and 0xFFFFFFFF (once the idle and stop
+    marks' values) and 0 included -- of every kind: one wave, the latency tier, helper grids, two outstanding, and idle
+    relaunches across the wrap.  Every post's records equal the oracle's."""
+    p, host, n = big
+    s = host.numpy().reshape(n, STRIDE)
+    table = pa.gen_conn_table(p)
+    m = 20000
+    exp = _expected(s[:m], m, table)
+    monkeypatch.setenv("PN_SERVICE_FIRST_POST", str(0xFFFFFFF0))
+    outs = [torch.zeros(m * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=2)
+        try:
+            sizes = [1, 64, 4096, m, 700]
+            ids, pending = [], []
+            for k in range(64):
+                size = sizes[k % len(sizes)]
+                o = k & 1
+                if pending and pending[0][1] == o:
+                    pid, oo, sz = pending.pop(0)
+                    svc.wait(pid)
+                    assert np.array_equal(outs[oo].numpy()[: sz * 16].view(pa.RESULT_DTYPE), exp[:sz]), (hex(pid), sz)
+                outs[o].zero_()
+                pid = svc.post(host, size, outs[o])
+                ids.append(pid)
+                pending.append((pid, o, size))
+                if k % 7 == 3:  # past idle_ms: the kernel ends, the next post relaunches it
+                    time.sleep(0.005)
+            for pid, oo, sz in pending:
+                svc.wait(pid)
+                assert np.array_equal(outs[oo].numpy()[: sz * 16].view(pa.RESULT_DTYPE), exp[:sz]), (hex(pid), sz)
+            assert ids[0] == 0xFFFFFFF1 and 0 in ids and 0xFFFFFFFF in ids and 0xFFFFFFFE in ids
+            assert all(((b - a) & 0xFFFFFFFF) == 1 for a, b in zip(ids, ids[1:]))
+        finally:
+            svc.close()
+    finally:
+        ctx.close()

@@ -42,10 +42,11 @@ def test_gpu_server_matches_twin(per_poll):
 PEER = os.path.join(ROOT, "tests", "cpp", "test_tcp_server_peer")
 
 
-def _peer(mode, populations=1):
+def _peer(mode, populations=1, env=None):
     if not os.path.exists(PEER):
         subprocess.run(["make", "-C", ROOT, "tests/cpp/test_tcp_server_peer"], check=True, capture_output=True)
-    return subprocess.run([PEER, mode, str(populations)], capture_output=True, text=True, timeout=300)
+    return subprocess.run([PEER, mode, str(populations)], capture_output=True, text=True, timeout=300,
+                          env=None if env is None else {**os.environ, **env})
 
 
 def test_server_twin_reactive_peers():
@@ -61,12 +62,22 @@ def test_server_twin_reactive_peers():
 
 @pytest.mark.gpu
 def test_gpu_server_reactive_peers_match_twin():
-    """The same on the GPU backend, 4 populations x 6 RX modes (every poll, latency budget,
-    chunks, pipelined, and the resident service every poll and pipelined): handler log and every TX frame
-    equal to the twin's in each run."""
+    """The same on the GPU backend, 4 populations x 8 RX modes (every poll, latency budget,
+    chunks, pipelined one and two polls deep, and the resident service every poll and pipelined one and two
+    polls deep): handler log and every TX frame equal to the twin's in each run."""
     p = _peer("gpu", 4)
     assert p.returncode == 0, p.stdout + p.stderr
-    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 24, p.stdout
+    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 32, p.stdout
+
+
+@pytest.mark.gpu
+def test_gpu_server_resident_post_ids_wrap():
+    """The resident-service modes with the service's post counter started 16 below 2^32 (PN_SERVICE_FIRST_POST):
+    every run's posts cross the wrap (post id 0 included, which GpuRx once took for "no post outstanding"), and the
+    handler log and every TX frame still equal the twin's."""
+    p = _peer("gpu", 1, env={"PN_SERVICE_FIRST_POST": str(0xFFFFFFF0)})
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 8, p.stdout
 
 
 CLISRV = os.path.join(ROOT, "tests", "cpp", "test_tcp_client_server")
