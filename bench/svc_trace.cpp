@@ -1,12 +1,12 @@
 // Where a resident-service post spends its time on the GPU (measurement build only: `make svc_trace` builds
 // ab_libs/trace/libpollnet_amd.so with -DPN_SVC_TRACE, whose service kernels store the device wall clock at each
 // step of the post protocol, and this driver against it).  Per post kind: the host's post-to-complete time and the
-// device steps relative to wave 0 seeing the post (medians over reps, µs):
-//   w0_acq     wave 0's acquire fence after the mailbox read matched
-//   w0_pub     + the device copy, release fence and cur store (multi-wave posts)
-//   oth_seen   the last of the post's other waves seeing cur;  oth_acq its acquire fence;  oth_args its copy read
-//   run_end    the last wave's classify + system fence + done word;  count_end  + its count (the done for wave 0)
-//   w0_next    wave 0 ready for the next post
+// device steps relative to wave 0 seeing the post (medians over reps, µs).  Round 6 protocol (every wave reads the
+// mailbox itself):
+//   w0_acq     wave 0's acquire fence after its mailbox read matched
+//   oth_seen   the last of the post's other waves seeing the post;  oth_acq its acquire fence;  oth_args its arguments
+//   run_end    the last wave's classify + system fence + done word;  count_end  + its count (counted posts)
+//   w0_pub, w0_next: steps of the round-5 protocol (wave 0's hand-off), -1 now
 //   argv: reps (300)
 #include <hip/hip_runtime.h>
 

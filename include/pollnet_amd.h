@@ -268,9 +268,10 @@ int pn_tx_fill_notify(pn_ctx* ctx, void* frames, uint32_t slot_stride, uint32_t 
 /* ---- resident classify service: no launch per batch (round 5) ----
  * pn_service_open launches a kernel that stays on the GPU (PN_SERVICE_WAVES one-wave workgroups on a stream of its
  * own, the latency tier) and classifies every batch the host posts afterwards, with the same code and records as
- * pn_classify on the layout given at open (strided slots).  A post is a few stores into pinned host memory that the
- * kernel polls, so a batch starts ~1-2 us after it is posted instead of a launch's ~7 us (bench/bench_doorbell;
- * DESIGN.md §13).
+ * pn_classify on the layout given at open (strided slots).  A post is one 64-B line the host writes into a mailbox
+ * that every wave of the kernel polls -- device memory written through the large BAR (pinned host memory on a device
+ * without one, or with PN_SERVICE_HOST_MAILBOX set in the environment at open) -- so a batch starts ~1-2 us after it
+ * is posted instead of a launch's ~7 us (bench/bench_doorbell).
  *   pn_service_post: frames (pinned host or device memory, 16-B aligned), n in [1, PN_SERVICE_MAX_FRAMES], results
  *     (pinned host or device memory, 16-B aligned).  The ctx's conn table and pn_set_verify setting at the post are
  *     used.  At most two posts outstanding (a third is refused, PN_EINVAL); non-blocking; *post_id (may be NULL)

@@ -3,28 +3,31 @@
 // rx_classify.hpp), without a launch per batch.  A launch costs ≈7 µs of host-to-GPU round trip; a resident wave
 // answering a doorbell ≈2.7 µs (bench/bench_doorbell, profiles/r05/latency/).
 //
-// Protocol.  Two mailbox slots of one 64-B line each (pinned host memory; post k uses slot k & 1).  The host
-// fills a slot's fields, then its first word (gen) and last word (seq) = k with release stores.  Wave 0 of
-// the kernel polls only the slot of the next post (one 64-B read per poll: 16 lanes x 4 B), accepts it when gen
-// and seq both read k, and publishes (waves << 32) | k in a device word: a post runs on one wave per group of
-// frames (at most all of them; svc_fpw sizes the groups).  A one-wave post wave 0 classifies alone; for a larger
-// one it first copies the slot to device memory, where the post's other waves read it.  Each wave of the post makes
-// its records system-visible and stores k to its own host done word -- the host waits on the words of the post's
-// waves, no cross-wave step on the way -- and then counts itself done on the device; the last resets the counter
-// and marks the post done for wave 0, which looks for post k + 1 only then.  A post on more waves than there are
-// done words (a large one, round 6) completes through the count alone: the last of its waves stores k to done word 0.
-// A stop post (n = PN_SERVICE_STOP) ends every wave.  Every wait has a device-wall-clock limit: after idle_ms without
-// a post wave 0 publishes "idle", stores the launch's epoch to the host's exit word and ends, and the others end on
-// seeing it (or at their own limit); the host relaunches on its next post.  A post in flight has a limit of its own
-// (kPostLimitMs from its acceptance, not the idle limit): should a wave of it never finish, wave 0 gives up the same
-// way, exit word included, and the host's relaunch runs the post again.  So the kernel always ends.
+// Protocol (round 6: every wave reads the mailbox itself).  Two mailbox slots of one 64-B line each, then a line
+// holding the exit flag; post k uses slot k & 1.  On a large-BAR device (MI355X) the mailbox is uncached device
+// memory that the host writes through the BAR, so a post lands in HBM and every wave of the kernel, on every XCD, sees
+// it with its own read of device memory -- no wave hands a post to the others.  (Without a large BAR the mailbox is
+// pinned host memory and the waves other than 0 poll it less often.)  The host writes a slot's fields and their check
+// word, store fence, then its first word (gen) and last word (seq) = k, store fence.  Each wave keeps the last post it
+// saw and reads both slots and the exit flag with one load (lanes 0-31: the slots, lane 32: the flag); it takes the
+// smallest post after its last one that a slot holds whole (gen = seq = k, the check word matching, so a read that
+// mixed two posts' words is refused).  A post runs on its first `act` waves (one per group of frames, at most all of
+// them; svc_fpw sizes the groups); the others note it went by.  A wave takes posts in order, so it never skips a post
+// it runs on: the host reuses post k's slot (for post k + 2) only once post k is complete.  Each wave of a post makes
+// its records system-visible and stores k to its own host done word; the host waits on the words of the post's waves.
+// A post completing through done word 0 alone -- a linked post (its chain pass runs after every wave's records) or a
+// large one (on more waves than there are done words) -- is counted on a per-slot device counter, and its last wave
+// completes it.  Posts k and k + 1 may run at once on different waves.  A stop post (n = PN_SERVICE_STOP) ends every
+// wave.  After idle_ms without a post wave 0 stores the launch's epoch to the exit flag and to the host's exit word and
+// ends; the others end on the flag (a safety limit of their own backs it); the host relaunches on its next post, and a
+// post the ended launch left incomplete runs again.  So the kernel always ends.
 // Large posts (round 6).  The resident kernel is the latency tier: kLatWaves (64) one-wave workgroups, which answer
 // every post of up to 4096 frames and leave the rest of the chip to other kernels while idle.  A post above that
 // also runs on helper waves: a grid the host launches with the post on a stream of its own (a launch's ~7 us is
 // nothing beside a large post's run).  The helpers get the post in their arguments, take their share of its groups as
 // waves kLatWaves.. of it and end -- no wait, no count, no write-back of their own: the host takes the post as done
 // once the resident waves' done word and the helper grid's end are both there.  The slot's fpw word carries the
-// helper count (bits 8+), so wave 0 knows the post's wave count.  Only vector memory operations
+// helper count (bits 8+), so the resident waves know the post's wave count.  Only vector memory operations
 // (global loads / stores / one atomic add).
 #include <algorithm>
 #include <chrono>
@@ -53,28 +56,24 @@ struct alignas(64) SvcPost { // one 64-B line: a mailbox slot (host) or its devi
 static_assert(sizeof(SvcPost) == 64, "one line per post");
 
 constexpr uint32_t kDoneWords = 64; // host words: one done word per wave of a post on at most this many waves,
+constexpr uint32_t kCountWords = 64; // then one per mailbox slot for counted posts (completed by their last wave),
 constexpr uint32_t kExitWord = 96;   // then the exit word on a line of its own
 constexpr uint32_t kWordsBytes = 512;
 constexpr uint32_t kLatWaves = PN_SERVICE_WAVES; // the latency tier: every post of up to 4096 frames runs on these
 static_assert(kLatWaves <= kDoneWords, "a latency-tier post completes through per-wave done words");
 constexpr uint32_t kLatFrames = kLatWaves * kFramesPerWave; // the largest post the tier takes alone
-constexpr uint32_t kPostLimitMs = 8000; // a post in flight (pn_service_wait gives up at 10 s)
+constexpr uint32_t kNetLimitMs = 8000; // waves other than 0: ended after 1.5 x idle_ms + this without a post, should
+                                       // wave 0's exit flag never come (pn_service_wait gives up at 10 s)
 constexpr uint32_t kPostVerify = 1u << 30, kPostLinks = 1u << 29, kPostN = (1u << 21) - 1; // the n word
 constexpr uint32_t kLinkFrames = PN_LINK_MAX_FRAMES, kLinkConns = PN_LINK_MAX_CONNS;
-// Published in the wave-count half of `cur` (a real post runs on at most PN_SERVICE_MAX_WAVES): every 32-bit post id
-// is a valid post, the counter wraps (2^32 posts: 11 hours at 100k posts/s)
-constexpr uint32_t kSvcIdle = 0xFFFFFFFEu; // wave 0 ended: no post for idle_ms, or a post past its limit
-constexpr uint32_t kSvcStop = 0xFFFFFFFFu; // a stop post
-static_assert(PN_SERVICE_MAX_WAVES < kSvcIdle, "wave counts below the idle / stop marks");
+constexpr uint32_t kMailBytes = 4096; // the mailbox allocation: slot 0, slot 1, the exit flag's line
+// Post ids count up by one and wrap (2^32 posts: 11 hours at 100k posts/s): every 32-bit value is a post's id, and
+// "after" is the wrap-aware order.  A stop post is marked by its n word.
 
 struct alignas(64) SvcDev { // device memory, set by the host before every launch
-  uint64_t cur;             // wave 0 publishes (waves << 32) | post: the post and how many waves it runs on
-  uint32_t pad0[14];
-  uint32_t count; // waves done with the current post
-  uint32_t done;  // the last multi-wave post every one of its waves finished
-  uint32_t pad1[14];
-  SvcPost post[2];
+  uint32_t count[2][16];    // per mailbox slot (one line each): the resident waves done with its post (counted posts)
 };
+constexpr uint32_t kExitFlag = 32; // the mailbox's word 32 (its third line): the epoch of the launch whose wave 0 ended
 
 // Measurement build only (-DPN_SVC_TRACE, bench/svc_trace.cpp): lane 0 of each wave stores the device wall clock at
 // the protocol's steps to pinned host memory (pn_svc_trace_set); compiled out of the product.  Plain stores: a step
@@ -92,16 +91,17 @@ __device__ uint64_t* g_svc_trace = nullptr;
 #endif
 
 struct SArgs {
-  const SvcPost* mail;  // host: the two mailbox slots
+  const SvcPost* mail;  // the two mailbox slots, then the exit flag's line (device memory, or pinned host)
   u32x4* scratch;       // device: per mailbox slot, kLinkFrames x 2 chain entries (kChainAux)
   uint32_t* done_words; // host: per wave, the last post it finished its groups of
   uint32_t* exit_word;  // host: the launch's epoch once it ended for lack of posts
   SvcDev* dev;
   uint64_t idle_ticks; // device wall clock
-  uint64_t post_ticks; // kPostLimitMs
+  uint64_t net_ticks;  // waves other than 0: their own limit without a post, should wave 0's flag never come
   uint32_t epoch;
   uint32_t last; // the post completed before this launch
   uint32_t stride, ipa_off, avail;
+  uint32_t poll_sleep; // waves other than 0: s_sleep between reads of the mailbox (1 in device memory)
 };
 
 // Frames per group (host, at the post).  The release path reads one header line per frame: 64 frames a wave, so a
@@ -135,22 +135,21 @@ inline uint32_t svc_helpers(uint32_t n, uint32_t max) {
   return std::min(groups - kLatWaves, max);
 }
 
-// a post's kernel arguments from its 64-B line held one word per lane (lanes 0-15, SvcPost's layout)
-__device__ __forceinline__ KArgsAux svc_args(uint32_t v, const SArgs& s, uint32_t k) {
+// a post's kernel arguments from its 64-B line held one word per lane (lanes b .. b + 15, SvcPost's layout)
+__device__ __forceinline__ KArgsAux svc_args(uint32_t v, uint32_t b, const SArgs& s, uint32_t k) {
   // readlane returns int: each word through uint32_t, or a low word with bit 31 set would sign-extend
-  auto u64 = [&](int lo) {
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, lo + 1) << 32) | (uint32_t)__builtin_amdgcn_readlane(v, lo);
-  };
+  auto w32 = [&](uint32_t i) { return (uint32_t)__builtin_amdgcn_readlane(v, b + i); };
+  auto u64 = [&](uint32_t lo) { return ((uint64_t)w32(lo + 1) << 32) | w32(lo); };
   KArgsAux a;
-  const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
+  const uint32_t nw = w32(1);
   a.n = nw & kPostN;
-  a.fpw = __builtin_amdgcn_readlane(v, 2) & 0xffu;
-  a.max_conn = __builtin_amdgcn_readlane(v, 3);
+  a.fpw = w32(2) & 0xffu;
+  a.max_conn = w32(3);
   a.frames = reinterpret_cast<const uint8_t*>(u64(4));
   a.out = reinterpret_cast<pn_result*>(u64(6));
   a.tbl = reinterpret_cast<const pn_conn_entry*>(u64(8));
-  a.mask = (uint32_t)__builtin_amdgcn_readlane(v, 12);
-  a.n_entries = __builtin_amdgcn_readlane(v, 13);
+  a.mask = w32(12);
+  a.n_entries = w32(13);
   a.stride = s.stride;
   a.ipa_off = s.ipa_off;
   a.avail = s.avail;
@@ -160,9 +159,9 @@ __device__ __forceinline__ KArgsAux svc_args(uint32_t v, const SArgs& s, uint32_
   return a;
 }
 
-__device__ __forceinline__ uint16_t* svc_links(uint32_t v) {
-  return reinterpret_cast<uint16_t*>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, 11) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane(v, 10));
+__device__ __forceinline__ uint16_t* svc_links(uint32_t v, uint32_t b) {
+  return reinterpret_cast<uint16_t*>(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(v, b + 11) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane(v, b + 10));
 }
 
 // ---- chain links (round 6): the in-order successor structure of a post, for the host's fast path ----
@@ -290,11 +289,12 @@ __device__ __forceinline__ void svc_run(const KArgsAux& a, bool verify, bool lin
     __hip_atomic_store(done_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The wave that completes a post through done word 0 alone (a post on more than kDoneWords waves, or a linked post):
-// a linked post's chain pass first, over the chain entries every wave of the post left in scratch; then k to done word
-// 0 once everything the post writes is visible to the host.
+// The wave that completes a counted post (on more than kDoneWords waves, or linked) through its slot's count word
+// (host words kCountWords + slot, never a wave's own done word: a wave may already run the next post): a linked post's
+// chain pass first, over the chain entries every wave of the post left in scratch; then k to the count word once
+// everything the post writes is visible to the host.
 template <bool PASS>
-__device__ __forceinline__ void svc_finish(const KArgsAux& a, uint16_t* links, uint32_t k, uint32_t* done_word0, int lane) {
+__device__ __forceinline__ void svc_finish(const KArgsAux& a, uint16_t* links, uint32_t k, uint32_t* count_word, int lane) {
   if constexpr (PASS) {
     if (a.aux) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // the other waves' chain entries
@@ -302,134 +302,95 @@ __device__ __forceinline__ void svc_finish(const KArgsAux& a, uint16_t* links, u
     }
   }
   __threadfence_system();
-  if (lane == 0) __hip_atomic_store(done_word0, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) __hip_atomic_store(count_word, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// a multi-wave post: count this wave done; the last one resets the count, completes the post through done word 0
-// when it has no per-wave words (svc_finish), and marks it done for wave 0 (every wave's records and chain entries
-// were made system-visible before its count: the count's order pairs them with what the last wave does next).  Only
-// the resident waves count (target = the post's waves in the tier); a large post's helpers run beside them.
+// a counted post (linked, or on more than kDoneWords waves): count this wave done on its slot's counter; the last of
+// the post's resident waves resets the counter (the slot's next post, k + 2, is issued only once k is complete) and
+// completes the post through done word 0 (svc_finish).  Every wave's records and chain entries were made
+// system-visible before its count, which pairs them with what the last wave does next.  A large post's helpers run
+// beside the resident waves and do not count.
 template <bool PASS>
-__device__ __forceinline__ void svc_count(SvcDev* dev, const KArgsAux& a, uint16_t* links, uint32_t act,
-                                          uint32_t target, uint32_t k, uint32_t* done_word0, int lane) {
+__device__ __forceinline__ void svc_count(uint32_t* count, const KArgsAux& a, uint16_t* links, uint32_t target, uint32_t k,
+                                          uint32_t* count_word, int lane) {
   uint32_t prev = 0;
-  if (lane == 0) prev = atomicAdd(&dev->count, 1u);
+  if (lane == 0) prev = atomicAdd(count, 1u);
   prev = __builtin_amdgcn_readfirstlane(prev);
-  if (prev == target - 1) { // the last of the post's resident waves (a large post's helpers do not count)
-    if (lane == 0) dev->count = 0u; // ordered before `done` by the release: wave 0 publishes the next post only after it
-    if (act > kDoneWords || a.aux) svc_finish<PASS>(a, links, k, done_word0, lane);
-    if (lane == 0) __hip_atomic_store(&dev->done, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev == target - 1) {
+    if (lane == 0) __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // before done word 0
+    svc_finish<PASS>(a, links, k, count_word, lane);
   }
 }
 
-// Wave 0 takes posts from the mailbox in order and publishes each with its wave count; a one-wave post it
-// classifies alone.  A post's waves other than 0 read it from the device copy, which wave 0 overwrites (two posts
-// later) only after every one of them counted itself done, so they always see it whole; the waves a post does not
-// run on only note it went by (from the published word alone: they may skip posts).  The waves of a large post past
-// the tier's are the helper grid's, which needs none of this (rx_service_helper_kernel).
-// Timers: wave 0's idle limit runs from the end of the last post (or the launch); a post's limit from its
-// acceptance.  Every other wave ends on wave 0's word; its own limit is only a safety net, measured from the last post
-// it saw go by and longer than anything wave 0 can spend before publishing the next word (a post's limit, then idle).
+// Every wave reads the mailbox itself (one load: lanes 0-31 the two slots, lane 32 the exit flag) and takes the posts
+// after the last one it saw, in order; it runs its groups of the posts it is one of the first `act` waves of.  Wave 0
+// ends after idle_ms without a post (the idle limit runs from the end of its last post, or the launch) and flags it;
+// the other waves end on the flag, or at their own limit.
 template <int MIS, int COOP>
 __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   const int lane = threadIdx.x;
   const uint32_t w = blockIdx.x, W = gridDim.x;
+  const uint32_t* mw = reinterpret_cast<const uint32_t*>(s.mail);
   uint32_t last = s.last;
   uint64_t t0 = wall_clock64();
-  const uint64_t net = s.idle_ticks + (s.idle_ticks >> 1) + s.post_ticks;
   chain_init(lane); // any wave of the tier may complete a linked post
   for (;;) {
-    uint32_t v = 0;         // the post's 64-B line, lane i holding word i (lanes 0-15)
-    uint32_t k = 0, act = 0; // the post and its wave count
-    bool run = false;       // this wave classifies groups of post k
-    uint64_t t_acc = 0;     // wave 0: when it accepted post k
-    if (w == 0) {
-      k = last + 1;
-      // the next post's slot, one 64-B read
-      const uint32_t* slot = reinterpret_cast<const uint32_t*>(s.mail + (k & 1));
-      v = lane < 16 ? __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-      uint32_t x = k; // the check word over words 1-13 (svc_check)
+    const uint32_t v = lane <= (int)kExitFlag ? __hip_atomic_load(mw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+    if (w != 0 && (uint32_t)__builtin_amdgcn_readlane(v, kExitFlag) == s.epoch) return; // wave 0 ended
+    // the earliest post after `last` that a slot holds whole
+    uint32_t k = 0;
+    bool found = false;
 #pragma unroll
-      for (int i = 1; i <= 13; i++) x ^= (uint32_t)__builtin_amdgcn_readlane(v, i);
-      if (__builtin_amdgcn_readlane(v, 0) != k || __builtin_amdgcn_readlane(v, 15) != k ||
-          (uint32_t)__builtin_amdgcn_readlane(v, 14) != x) {
+    for (uint32_t sl = 0; sl < 2; ++sl) {
+      const uint32_t q = __builtin_amdgcn_readlane(v, 16 * sl + 15);
+      uint32_t x = q; // the check word over words 1-13 (svc_check)
+#pragma unroll
+      for (uint32_t i = 1; i <= 13; i++) x ^= (uint32_t)__builtin_amdgcn_readlane(v, 16 * sl + i);
+      const bool whole = (uint32_t)__builtin_amdgcn_readlane(v, 16 * sl) == q &&
+                         (uint32_t)__builtin_amdgcn_readlane(v, 16 * sl + 14) == x && (q & 1) == sl;
+      if (whole && (int32_t)(q - last) > 0 && (!found || (int32_t)(q - k) < 0)) {
+        k = q;
+        found = true;
+      }
+    }
+    if (!found) {
+      if (w == 0) {
         if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
           if (lane == 0) {
-            __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(const_cast<uint32_t*>(mw) + kExitFlag, s.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           }
           return;
         }
         __builtin_amdgcn_s_sleep(1);
-        continue;
+      } else {
+        if (wall_clock64() - t0 > s.net_ticks) return; // a safety net: wave 0 always flags its end first
+        for (uint32_t i = 0; i < s.poll_sleep; ++i) __builtin_amdgcn_s_sleep(1);
       }
-      SVC_T(0, 0);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
-      SVC_T(0, 1);
-      t_acc = wall_clock64();
-      const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
-      if (nw == PN_SERVICE_STOP) {
-        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)kSvcStop << 32) | k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-      }
-      const uint32_t fw = __builtin_amdgcn_readlane(v, 2);
-      act = svc_active(nw & kPostN, fw & 0xffu, W + (fw >> 8));
-      if (act > 1) { // the post's other waves read it from the device copy
-        if (lane < 16) reinterpret_cast<uint32_t*>(&s.dev->post[k & 1])[lane] = v;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        if (lane == 0) __hip_atomic_store(&s.dev->cur, ((uint64_t)act << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        SVC_T(0, 2);
-      }
-      run = true;
-    } else {
-      const uint64_t c = __hip_atomic_load(&s.dev->cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      k = __builtin_amdgcn_readfirstlane((uint32_t)c);
-      act = __builtin_amdgcn_readfirstlane((uint32_t)(c >> 32));
-      if (act >= kSvcIdle) return; // idle or stop
-      if (k == last) {
-        if (wall_clock64() - t0 > net) return; // a safety net: wave 0 always publishes kSvcIdle first
-        __builtin_amdgcn_s_sleep(2);
-        continue;
-      }
-      if (w < act) { // this wave runs on post k: wave 0 waits for it before the next post, so k is current
-        SVC_T(w, 0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        SVC_T(w, 1);
-        const uint32_t* cp = reinterpret_cast<const uint32_t*>(&s.dev->post[k & 1]);
-        v = lane < 16 ? cp[lane] : 0u;
-        run = true;
-      }
+      continue;
     }
-    if (run) { // one call site for every wave (the classify code is inlined once per path)
-      const KArgsAux a = svc_args(v, s, k);
+    const uint32_t b = (k & 1) * 16; // the post's words: lanes b .. b + 15
+    const uint32_t nw = __builtin_amdgcn_readlane(v, b + 1);
+    if (nw == PN_SERVICE_STOP) return;
+    last = k;
+    const uint32_t fw = __builtin_amdgcn_readlane(v, b + 2);
+    const uint32_t act = svc_active(nw & kPostN, fw & 0xffu, W + (fw >> 8));
+    if (w < act) { // this wave runs on post k
+      SVC_T(w, 0);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); // the frames the host wrote before the post
+      SVC_T(w, 1);
+      const KArgsAux a = svc_args(v, b, s, k);
       SVC_T(w, 5);
-      const uint32_t nw = __builtin_amdgcn_readlane(v, 1);
-      svc_run<MIS, COOP>(a, (nw & kPostVerify) != 0, a.aux != nullptr, w, act, k, s.done_words + w, lane);
+      const bool linked = a.aux != nullptr;
+      svc_run<MIS, COOP>(a, (nw & kPostVerify) != 0, linked, w, act, k, s.done_words + w, lane);
       SVC_T(w, 6);
-      if (act > 1) svc_count<true>(s.dev, a, svc_links(v), act, act < W ? act : W, k, s.done_words, lane);
-      else if (a.aux) svc_finish<true>(a, svc_links(v), k, s.done_words, lane);
+      if (act > kDoneWords || linked) {
+        uint32_t* cw = s.done_words + kCountWords + (k & 1);
+        if (act == 1) svc_finish<true>(a, svc_links(v, b), k, cw, lane);
+        else svc_count<true>(&s.dev->count[k & 1][0], a, svc_links(v, b), act < W ? act : W, k, cw, lane);
+      }
       SVC_T(w, 7);
     }
-    if (w == 0) {
-      if (act == 1) { // one wave's work, done: let the others see it go by
-        if (lane == 0) __hip_atomic_store(&s.dev->cur, (1ull << 32) | k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else { // the next post only once every wave of this one is done (its device copy may then be reused)
-        while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(&s.dev->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) !=
-               k) {
-          if (wall_clock64() - t_acc > s.post_ticks) { // a wave of the post never finished: give up, and say so
-            if (lane == 0) {
-              __hip_atomic_store(&s.dev->cur, (uint64_t)kSvcIdle << 32, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-              __hip_atomic_store(s.exit_word, s.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            return;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-      SVC_T(0, 4);
-    }
-    last = k;
     t0 = wall_clock64();
   }
 }
@@ -464,10 +425,12 @@ struct pn_service {
   uint32_t helpers_max = 0;            // helper waves of a large post: its total wave count less the tier's
   uint32_t post_helpers[2] = {0, 0};   // helper waves of the last two posts (a relaunch launches them again)
   hipEvent_t helper_ev[2] = {nullptr, nullptr}; // the end of each one's helper grid: its records are visible then
-  uint64_t idle_ticks = 0, post_ticks = 0;
-  SvcPost* mail = nullptr;    // pinned host: 2 slots
+  uint64_t idle_ticks = 0, net_ticks = 0;
+  SvcPost* mail = nullptr;    // the two slots and the exit flag's line: device memory the host writes through the
+  bool mail_dev = false;      // large BAR (mail_dev), or pinned host memory; the host only ever stores to it
   uint32_t* words = nullptr;  // pinned host: [0, 64) the waves' done words, [kExitWord] exit (its own line)
-  uint32_t post_words[2] = {0, 0}; // done words of the last two posts (slot k & 1): whose words post k completes
+  uint32_t post_words[2] = {0, 0}; // the last two posts (slot k & 1): the waves whose done words post k completes
+                                   // through, or 0 for a counted post (its slot's count word)
   // the conn-table buffer each post captured (ctx->tbl_buf[b]): the last post that did, per buffer, so that
   // pn_set_conn_table waits for it before it overwrites or frees that buffer (svc_release_table)
   uint32_t tbl_post[2] = {0, 0};
@@ -475,7 +438,7 @@ struct pn_service {
   SvcDev* dev = nullptr;      // device
   u32x4* scratch = nullptr;   // device: the chain entries of linked posts, kLinkFrames x 2 per mailbox slot
   uint32_t seq = 0;           // last post issued
-  uint32_t epoch = 0;         // launches so far
+  uint32_t epoch = 0;         // launches so far (never 0: the exit flag's initial value)
   bool running = false;       // a launch that has not been seen to end
   bool coop = false;
 };
@@ -491,19 +454,52 @@ SArgs svc_sargs(const pn_service* v, uint32_t base) {
   a.exit_word = v->words + kExitWord;
   a.dev = v->dev;
   a.idle_ticks = v->idle_ticks;
-  a.post_ticks = v->post_ticks;
+  a.net_ticks = v->net_ticks;
   a.epoch = v->epoch;
   a.last = base;
   a.stride = v->stride;
   a.ipa_off = (v->frame_off + 14) & ~15u;
   a.avail = v->stride - v->frame_off;
+  a.poll_sleep = v->mail_dev ? 1u : 16u; // polls of host memory cross PCIe: fewer of them
   return a;
 }
 
-// the helper grid of large post k (its fields already in slot k & 1), and the event its end completes: the post is
-// done once both its resident waves' done word and the grid's end are
-int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
-  const SvcPost* p = v->mail + (k & 1);
+// x86 store fence: the mailbox's stores out of the write-combining buffer, in order (device memory through the BAR
+// is write-combined; for pinned host memory the fence costs little)
+inline void host_sfence() { asm volatile("sfence" ::: "memory"); }
+
+// Write post q into its slot.  Only stores: a read of device memory through the BAR would cost a PCIe round trip.
+// Device memory (write-combined): the whole 64-B line as two 32-B non-temporal stores and one fence, so it leaves the
+// write-combining buffer as one write (a read that still splits it fails the check word).  Pinned host memory, or a
+// CPU without AVX: words 1-14 (the fields and the check word), a fence, then gen and seq, a fence.
+void svc_publish(SvcPost* slot, const SvcPost& q, bool wc) {
+  static const bool avx = __builtin_cpu_supports("avx");
+  if (wc && avx) {
+    asm volatile(
+        "vmovdqu (%0), %%ymm0\n\t"
+        "vmovdqu 32(%0), %%ymm1\n\t"
+        "vmovntdq %%ymm0, (%1)\n\t"
+        "vmovntdq %%ymm1, 32(%1)\n\t"
+        "sfence\n\t"
+        "vzeroupper"
+        :
+        : "r"(&q), "r"(slot)
+        : "memory", "xmm0", "xmm1");
+    return;
+  }
+  volatile uint32_t* d = reinterpret_cast<volatile uint32_t*>(slot);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&q);
+  for (int i = 1; i <= 14; ++i) d[i] = w[i];
+  host_sfence();
+  d[0] = w[0];
+  d[15] = w[15];
+  host_sfence();
+}
+
+// the helper grid of large post k (its fields q), and the event its end completes: the post is done once both its
+// resident waves' done word and the grid's end are
+int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers, const SvcPost& q) {
+  const SvcPost* p = &q;
   KArgsAux a;
   a.n = p->n & kPostN;
   a.fpw = p->fpw & 0xffu;
@@ -539,13 +535,11 @@ int svc_launch_helpers(pn_service* v, uint32_t k, uint32_t helpers) {
 
 int svc_launch(pn_service* v, uint32_t base) {
   pn_ctx* ctx = v->ctx;
-  SvcDev init{};
-  init.cur = base;
-  init.done = base;
+  const SvcDev init{};
   hipError_t e = hipMemcpyAsync(v->dev, &init, sizeof(SvcDev), hipMemcpyHostToDevice, v->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(v->stream); // the previous launch has ended, the state is in place
   if (e != hipSuccess) return hip_err(ctx, e, "pn_service: device state");
-  ++v->epoch;
+  if (++v->epoch == 0) ++v->epoch;
   const SArgs a = svc_sargs(v, base);
   switch ((v->frame_off + 14) & 15) {
     case 0: launch_svc<0>(v->coop, kLatWaves, a, v->stream); break;
@@ -563,14 +557,24 @@ int svc_launch(pn_service* v, uint32_t base) {
   return PN_OK;      // grids, independent of it, are not relaunched)
 }
 
-// post k (one of the last two) is complete once every done word it completes through holds k (or later): one per
-// wave it ran on, or word 0 alone for a post on more than kDoneWords waves
-bool svc_post_done(const pn_service* v, uint32_t k) {
+// post k's own waves are done (k one of the last two posts): every done word it completes through holds k (or later),
+// one per wave it ran on or word 0 alone for a counted post, and its helper grid has ended
+bool svc_post_ran(const pn_service* v, uint32_t k) {
   const uint32_t words = v->post_words[k & 1];
+  if (words == 0 && (int32_t)(__atomic_load_n(v->words + kCountWords + (k & 1), __ATOMIC_ACQUIRE) - k) < 0) return false;
   for (uint32_t w = 0; w < words; ++w)
     if ((int32_t)(__atomic_load_n(v->words + w, __ATOMIC_ACQUIRE) - k) < 0) return false;
   if (v->post_helpers[k & 1] && hipEventQuery(v->helper_ev[k & 1]) != hipSuccess) return false; // (an error: not done)
   return true;
+}
+
+// post k is complete: it ran, and so did the post before it.  The waves take posts in order, but post k + 1 may run
+// on fewer waves than post k and finish first; completion stays in post order (the contract, and what lets the host
+// reuse post k's slot, counter and scratch for post k + 2).  Only the last two posts can be outstanding.
+bool svc_post_done(const pn_service* v, uint32_t k) {
+  if ((int32_t)(v->seq - k) >= 2) return true;
+  if (!svc_post_ran(v, k)) return false;
+  return k != v->seq || svc_post_ran(v, k - 1);
 }
 
 // the last completed post (posts complete in order)
@@ -586,7 +590,7 @@ void svc_free(pn_service* v) {
     auto& l = v->ctx->services;
     l.erase(std::remove(l.begin(), l.end(), v), l.end());
   }
-  if (v->mail) (void)hipHostFree(v->mail);
+  if (v->mail) (void)(v->mail_dev ? hipFree(v->mail) : hipHostFree(v->mail));
   if (v->words) (void)hipHostFree(v->words);
   if (v->dev) (void)hipFree(v->dev);
   if (v->scratch) (void)hipFree(v->scratch);
@@ -647,13 +651,18 @@ int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, ui
                                                                                       (uint32_t)cus * PN_SERVICE_WAVES_PER_CU));
   v->helpers_max = total - kLatWaves;
   v->idle_ticks = (uint64_t)khz * idle_ms;
-  v->post_ticks = (uint64_t)khz * kPostLimitMs;
+  v->net_ticks = v->idle_ticks + (v->idle_ticks >> 1) + (uint64_t)khz * kNetLimitMs;
   // the cooperative window needs a 16-B chunk before it inside the slot (frame_off >= 2); the frames' 16-B
   // alignment is checked per post
   v->coop = (slot_stride % 16) == 0 && ((frame_off + 14) & ~15u) >= 16;
+  // the mailbox in uncached device memory when the host can store to it through a large BAR
+  int large_bar = 0;
+  if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device) != hipSuccess) large_bar = 0;
+  v->mail_dev = large_bar != 0 && std::getenv("PN_SERVICE_HOST_MAILBOX") == nullptr;
   if ((e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&v->helper_stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = hipHostMalloc((void**)&v->mail, 2 * sizeof(SvcPost), hipHostMallocDefault)) != hipSuccess ||
+      (e = v->mail_dev ? hipExtMallocWithFlags((void**)&v->mail, kMailBytes, hipDeviceMallocUncached)
+                       : hipHostMalloc((void**)&v->mail, kMailBytes, hipHostMallocDefault)) != hipSuccess ||
       (e = hipHostMalloc((void**)&v->words, kWordsBytes, hipHostMallocDefault)) != hipSuccess ||
       (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess ||
       (e = hipMalloc((void**)&v->scratch, sizeof(u32x4) * 2 * 2 * kLinkFrames)) != hipSuccess) {
@@ -665,10 +674,17 @@ int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, ui
   // run the counter's wrap).  The done words and both slots hold it: neither slot reads as post first + 1 or + 2.
   uint32_t first = 0;
   if (const char* env = std::getenv("PN_SERVICE_FIRST_POST")) first = (uint32_t)std::strtoull(env, nullptr, 0);
-  std::memset(v->mail, 0, 2 * sizeof(SvcPost));
   std::memset(v->words, 0, kWordsBytes);
-  for (uint32_t w = 0; w < kDoneWords; ++w) v->words[w] = first;
-  for (int i = 0; i < 2; ++i) v->mail[i].gen = v->mail[i].seq = first;
+  for (uint32_t w = 0; w < kDoneWords + 2; ++w) v->words[w] = first; // the done and count words
+  {
+    SvcPost q{};
+    q.gen = q.seq = first;
+    q.check = ~svc_check(&q, first); // not a whole post either (and `first` is no post after the start)
+    for (int i = 0; i < 2; ++i) svc_publish(v->mail + i, q, v->mail_dev);
+    volatile uint32_t* flag = reinterpret_cast<volatile uint32_t*>(v->mail) + kExitFlag;
+    *flag = 0u; // no launch has epoch 0
+    host_sfence();
+  }
   v->seq = first;
   const int rc = svc_launch(v, first);
   if (rc) {
@@ -704,34 +720,34 @@ int pn_service_post_linked(pn_service* v, const void* frames, uint32_t n, void* 
     if (rc) return rc;
   }
   const uint32_t k = v->seq + 1;
-  SvcPost* p = v->mail + (k & 1);
-  // the fields and their check word first, then gen and seq = k, each a release store: the slot still holds post
-  // k - 2 (done), so until gen and seq both read k it is not post k; and should the line's read be split into pieces
-  // read at different times, a mix of two posts' fields fails the check and the kernel reads the slot again
+  // the post's line (svc_publish): the slot still holds post k - 2 (complete), so until gen and seq both read k it is
+  // not post k; and should a wave's read of the line be split into pieces read at different times, a mix of two
+  // posts' words fails the check and the wave reads the slot again
   const bool verify = ctx->verify_tcp;
-  p->n = n | (verify ? kPostVerify : 0u) | (links ? kPostLinks : 0u);
-  p->max_conn = ctx->max_conn;
-  p->frames = (const uint8_t*)frames;
-  p->out = (pn_result*)results;
-  p->tbl = ctx->tbl_dev;
-  p->links = links;
-  p->mask = (uint32_t)ctx->mask;
-  p->n_entries = ctx->n_entries;
+  SvcPost q{};
+  q.n = n | (verify ? kPostVerify : 0u) | (links ? kPostLinks : 0u);
+  q.max_conn = ctx->max_conn;
+  q.frames = (const uint8_t*)frames;
+  q.out = (pn_result*)results;
+  q.tbl = ctx->tbl_dev;
+  q.links = links;
+  q.mask = (uint32_t)ctx->mask;
+  q.n_entries = ctx->n_entries;
   const uint32_t fpw = svc_fpw(n, verify), helpers = svc_helpers(n, v->helpers_max);
-  p->fpw = fpw | helpers << 8;
+  q.fpw = fpw | helpers << 8;
   const uint32_t act = svc_active(n, fpw, kLatWaves + helpers);
-  // a large post's helpers first (they wait for wave 0 to publish it): should the launch fail, nothing was posted
+  // a large post's helpers first (nothing waits for them on the device): should the launch fail, nothing was posted
   if (helpers) {
-    const int rc = svc_launch_helpers(v, k, helpers);
+    const int rc = svc_launch_helpers(v, k, helpers, q);
     if (rc) return rc;
   }
   v->post_helpers[k & 1] = helpers;
-  v->post_words[k & 1] = (act <= kDoneWords && !links) ? act : 1u; // else done word 0 alone (svc_finish)
+  v->post_words[k & 1] = (act <= kDoneWords && !links) ? act : 0u; // else counted: its slot's count word (svc_finish)
   v->tbl_post[ctx->cur] = k; // pn_set_conn_table waits for this post before it reuses the buffer
   v->tbl_used[ctx->cur] = true;
-  p->check = svc_check(p, k);
-  __atomic_store_n(&p->gen, k, __ATOMIC_RELEASE);
-  __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
+  q.check = svc_check(&q, k);
+  q.gen = q.seq = k;
+  svc_publish(v->mail + (k & 1), q, v->mail_dev);
   v->seq = k;
   if (post_id) *post_id = k;
   return PN_OK;
@@ -773,14 +789,13 @@ int pn_service_close(pn_service* v) {
   int rc = svc_post_done(v, v->seq) ? PN_OK : pn_service_wait(v, 0);
   if (v->running && !svc_exited(v)) {
     const uint32_t k = v->seq + 1;
-    SvcPost* p = v->mail + (k & 1);
-    p->n = PN_SERVICE_STOP;
-    p->links = nullptr;
+    SvcPost q{};
+    q.n = PN_SERVICE_STOP;
     v->post_words[k & 1] = 0;
     v->post_helpers[k & 1] = 0;
-    p->check = svc_check(p, k);
-    __atomic_store_n(&p->gen, k, __ATOMIC_RELEASE);
-    __atomic_store_n(&p->seq, k, __ATOMIC_RELEASE);
+    q.check = svc_check(&q, k);
+    q.gen = q.seq = k;
+    svc_publish(v->mail + (k & 1), q, v->mail_dev);
     v->seq = k;
   }
   hipError_t e = hipStreamSynchronize(v->stream); // the kernel ends at the stop or its idle limit

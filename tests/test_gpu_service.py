@@ -558,3 +558,49 @@ def test_service_post_ids_wrap(torch, big, monkeypatch):
             svc.close()
     finally:
         ctx.close()
+
+
+def test_service_host_mailbox_fallback(torch, big, monkeypatch):
+    """Without a large BAR the mailbox is pinned host memory (PN_SERVICE_HOST_MAILBOX forces it here): the same
+    protocol, the waves reading the mailbox over PCIe.  Posts of every kind -- one wave, the latency tier, helper
+    grids, linked, two outstanding, idle relaunches -- give the oracle's records and links."""
+    p, host, n = big
+    s = host.numpy().reshape(n, STRIDE)
+    table = pa.gen_conn_table(p)
+    m = 20000
+    exp = _expected(s[:m], m, table)
+    links_exp = orc.chain_links(np.ascontiguousarray(s[:1000]), STRIDE, FRAME_OFF, 1000, exp[:1000], table.max_conn_cnt)
+    monkeypatch.setenv("PN_SERVICE_HOST_MAILBOX", "1")
+    outs = [torch.zeros(m * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    lk = [torch.zeros(1024, dtype=torch.int16).pin_memory() for _ in range(2)]
+    ctx = pa.RxContext(0)
+    try:
+        ctx.set_conn_table(table)
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF, idle_ms=2)
+        try:
+            sizes = [1, 64, 1000, 4096, m, 700]
+            pending = []
+            for k in range(48):
+                size = sizes[k % len(sizes)]
+                o = k & 1
+                if pending and pending[0][1] == o:
+                    pid, oo, sz, linked = pending.pop(0)
+                    svc.wait(pid)
+                    assert np.array_equal(outs[oo].numpy()[: sz * 16].view(pa.RESULT_DTYPE), exp[:sz]), (pid, sz)
+                    if linked:
+                        assert np.array_equal(lk[oo].numpy()[:sz].view(np.uint16), links_exp[:sz]), (pid, sz)
+                outs[o].zero_()
+                linked = size == 1000
+                pid = svc.post(host, size, outs[o], lk[o] if linked else None)
+                pending.append((pid, o, size, linked))
+                if k % 9 == 4:
+                    time.sleep(0.005)
+            for pid, oo, sz, linked in pending:
+                svc.wait(pid)
+                assert np.array_equal(outs[oo].numpy()[: sz * 16].view(pa.RESULT_DTYPE), exp[:sz]), (pid, sz)
+                if linked:
+                    assert np.array_equal(lk[oo].numpy()[:sz].view(np.uint16), links_exp[:sz]), (pid, sz)
+        finally:
+            svc.close()
+    finally:
+        ctx.close()
