@@ -659,10 +659,14 @@ int pn_service_open_ex(pn_ctx* ctx, uint32_t slot_stride, uint32_t frame_off, ui
   int large_bar = 0;
   if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, ctx->device) != hipSuccess) large_bar = 0;
   v->mail_dev = large_bar != 0 && std::getenv("PN_SERVICE_HOST_MAILBOX") == nullptr;
+  if (v->mail_dev && hipExtMallocWithFlags((void**)&v->mail, kMailBytes, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError(); // no uncached device memory: the mailbox in pinned host memory
+    v->mail = nullptr;
+    v->mail_dev = false;
+  }
   if ((e = hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking)) != hipSuccess ||
       (e = hipStreamCreateWithFlags(&v->helper_stream, hipStreamNonBlocking)) != hipSuccess ||
-      (e = v->mail_dev ? hipExtMallocWithFlags((void**)&v->mail, kMailBytes, hipDeviceMallocUncached)
-                       : hipHostMalloc((void**)&v->mail, kMailBytes, hipHostMallocDefault)) != hipSuccess ||
+      (!v->mail && (e = hipHostMalloc((void**)&v->mail, kMailBytes, hipHostMallocDefault)) != hipSuccess) ||
       (e = hipHostMalloc((void**)&v->words, kWordsBytes, hipHostMallocDefault)) != hipSuccess ||
       (e = hipMalloc((void**)&v->dev, sizeof(SvcDev))) != hipSuccess ||
       (e = hipMalloc((void**)&v->scratch, sizeof(u32x4) * 2 * 2 * kLinkFrames)) != hipSuccess) {
