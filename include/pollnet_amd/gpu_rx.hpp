@@ -125,7 +125,7 @@ class GpuRx {
   // frame_off = sizeof(RecvBuf) + receive_prefix_len in the reference); max_batch:
   // the chunk pollBatch() classifies per launch (two chunks are in flight at once).
   // resident (ZeroCopy only): the chunks go to the resident classify service (pn_service_*: one launch, then a post
-  // per chunk through pinned memory) instead of a launch each; resident_idle_ms: how long it stays without a post.
+  // per chunk through its mailbox) instead of a launch each; resident_idle_ms: how long it stays without a post.
   // links (resident, max_batch <= PN_LINK_MAX_FRAMES): each post also returns its chain links
   // (pn_service_post_linked), handed to a recv_handler that takes a fifth argument.
   const char* init(int device, uint32_t slot_stride, uint32_t frame_off, uint32_t max_batch, Mode mode = Mode::Copy,

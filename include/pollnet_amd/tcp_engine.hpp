@@ -83,7 +83,7 @@ PN_CONF_OPT(RxPipelineDepth, uint32_t, 1)   // with RxPipeline: the polls a batc
                                             // dispatch, 1 or 2 (2: the GPU has two polls' host work to finish a
                                             // batch in, one poll more of latency)
 PN_CONF_OPT(RxResident, bool, false)        // the classify runs in the resident service (pn_service_*): a post
-                                            // per poll through pinned memory instead of a launch
+                                            // per poll through its mailbox instead of a launch
 PN_CONF_OPT(RxLinks, bool, false)           // with RxResident: each post also returns its chain links
                                             // (pn_service_post_linked) and a frame that continues its connection's
                                             // previous one takes the in-order fast path.  Off by default: the GPU's

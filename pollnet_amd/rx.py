@@ -402,7 +402,8 @@ def wire_bytes(slots: np.ndarray, slot_stride: int, frame_off: int, n: int) -> i
 
 
 class RxService:
-    """The resident classify service (pn_service_*): one launch, then batches posted through pinned host memory
+    """The resident classify service (pn_service_*): one launch, then batches posted through a mailbox in device memory
+    (the large BAR; pinned host memory without one)
     and classified by the kernel already on the GPU.  Frames / results: pinned host or device memory.
     large_waves: a large post's wave count (pn_service_open_ex; 0 = the default, PN_SERVICE_WAVES_PER_CU per CU).
     Each post's frames and results objects are held until the post is waited for (or the service closed): the
