@@ -1001,7 +1001,9 @@ def summary(out):
                                                   g(sec, "small_batch_latency", "zero_copy", "64", "service_us")],
             "zero_copy_64_release_us_notify_vs_service": [
                 g(sec, "small_batch_latency", "zero_copy_release_path", "64", "signal_us"),
-                g(sec, "small_batch_latency", "zero_copy_release_path", "64", "service_us")]})
+                g(sec, "small_batch_latency", "zero_copy_release_path", "64", "service_us")],
+            "service_release_device_us_64_512_1024": [
+                g(sec, "small_batch_latency", "resident_release_path", m, "service_us") for m in ("64", "512", "1024")]})
     if cpu:
         s.update({"cpu_ref_gbit_per_s": cpu.get("value"), "cpu_ref_min_max": [cpu.get("min"), cpu.get("max")],
                   "cpu_ref_cores": cpu.get("cores"), "cpu_ref_consistent_with_sweep": cpu.get("consistent_with_sweep"),
