@@ -9,11 +9,14 @@
 // it with its own read of device memory -- no wave hands a post to the others.  (Without a large BAR the mailbox is
 // pinned host memory and the waves other than 0 poll it less often.)  The host writes a slot's fields and their check
 // word, store fence, then its first word (gen) and last word (seq) = k, store fence.  Each wave keeps the last post it
-// saw and reads both slots and the exit flag with one load (lanes 0-31: the slots, lane 32: the flag); it takes the
-// smallest post after its last one that a slot holds whole (gen = seq = k, the check word matching, so a read that
-// mixed two posts' words is refused).  A post runs on its first `act` waves (one per group of frames, at most all of
+// saw and reads both slots and the exit flag with one load (lanes 0-31: the slots, lane 32: the flag); it waits for the
+// next post, last + 1, in that post's slot, whole (gen = seq = k, the check word matching, so a read that mixed two
+// posts' words is refused) -- never taking a later post from the other slot first, since its read of the next post's
+// slot may be the older one.  A slot holding a later post means the next post was complete without this wave: the wave
+// was not one of its waves and passes it.  A post runs on its first `act` waves (one per group of frames, at most all of
 // them; svc_fpw sizes the groups); the others note it went by.  A wave takes posts in order, so it never skips a post
-// it runs on: the host reuses post k's slot (for post k + 2) only once post k is complete.  Each wave of a post makes
+// it runs on: the host reuses post k's slot (for post k + 2) only once post k is complete (a wave that took post k + 1
+// from the other slot before post k would store done word k + 1 without having run post k).  Each wave of a post makes
 // its records system-visible and stores k to its own host done word; the host waits on the words of the post's waves.
 // A post completing through done word 0 alone -- a linked post (its chain pass runs after every wave's records) or a
 // large one (on more waves than there are done words) -- is counted on a per-slot device counter, and its last wave
@@ -337,23 +340,16 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
   for (;;) {
     const uint32_t v = lane <= (int)kExitFlag ? __hip_atomic_load(mw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
     if (w != 0 && (uint32_t)__builtin_amdgcn_readlane(v, kExitFlag) == s.epoch) return; // wave 0 ended
-    // the earliest post after `last` that a slot holds whole
-    uint32_t k = 0;
-    bool found = false;
+    // the next post, k = last + 1, in its slot k & 1 -- and only there: a wave never passes over a post it may run on
+    // (an earlier read of the other slot could be older than this one's)
+    const uint32_t k = last + 1;
+    const uint32_t b = (k & 1) * 16; // the slot's words: lanes b .. b + 15
+    const uint32_t q = __builtin_amdgcn_readlane(v, b + 15);
+    uint32_t x = q; // the check word over words 1-13 (svc_check)
 #pragma unroll
-    for (uint32_t sl = 0; sl < 2; ++sl) {
-      const uint32_t q = __builtin_amdgcn_readlane(v, 16 * sl + 15);
-      uint32_t x = q; // the check word over words 1-13 (svc_check)
-#pragma unroll
-      for (uint32_t i = 1; i <= 13; i++) x ^= (uint32_t)__builtin_amdgcn_readlane(v, 16 * sl + i);
-      const bool whole = (uint32_t)__builtin_amdgcn_readlane(v, 16 * sl) == q &&
-                         (uint32_t)__builtin_amdgcn_readlane(v, 16 * sl + 14) == x && (q & 1) == sl;
-      if (whole && (int32_t)(q - last) > 0 && (!found || (int32_t)(q - k) < 0)) {
-        k = q;
-        found = true;
-      }
-    }
-    if (!found) {
+    for (uint32_t i = 1; i <= 13; i++) x ^= (uint32_t)__builtin_amdgcn_readlane(v, b + i);
+    const bool whole = (uint32_t)__builtin_amdgcn_readlane(v, b) == q && (uint32_t)__builtin_amdgcn_readlane(v, b + 14) == x;
+    if (!whole || (int32_t)(q - k) < 0) { // post k is not there yet
       if (w == 0) {
         if (wall_clock64() - t0 > s.idle_ticks) { // no post for idle_ms: end, and say so
           if (lane == 0) {
@@ -369,7 +365,11 @@ __global__ __launch_bounds__(kWave) void rx_service_kernel(SArgs s) {
       }
       continue;
     }
-    const uint32_t b = (k & 1) * 16; // the post's words: lanes b .. b + 15
+    if (q != k) { // the slot already holds a later post: post k was complete without this wave, which was not one of
+      last = k;   // its waves (the host reuses a slot only once its post is complete)
+      t0 = wall_clock64();
+      continue;
+    }
     const uint32_t nw = __builtin_amdgcn_readlane(v, b + 1);
     if (nw == PN_SERVICE_STOP) return;
     last = k;

@@ -604,3 +604,61 @@ def test_service_host_mailbox_fallback(torch, big, monkeypatch):
             svc.close()
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("mailbox", ["device", "host"])
+def test_service_ring_reuse_with_table_changes(torch, monkeypatch, mailbox):
+    """The drop-in server's pattern, as a soak: a pinned ring of two halves, each rewritten by the CPU with other frames
+    once its previous post is done, two posts outstanding, conn-table changes with a post in flight, both paths, random
+    sizes.  Every post's records equal the oracle's for the frames and table it was posted with -- with the mailbox in
+    device memory and in pinned host memory (PN_SERVICE_HOST_MAILBOX)."""
+    if mailbox == "host":
+        monkeypatch.setenv("PN_SERVICE_HOST_MAILBOX", "1")
+    rng = np.random.default_rng(0x7AB1E)
+    m = 512
+    p = pa.rx.GenParams.for_config(3)
+    sets = [_frames(3, m, first=m * i)[1] for i in range(8)]
+    t0 = pa.gen_conn_table(p)
+    t1 = pa.gen_conn_table(p)
+    for i in range(0, 64, 3):
+        t1.delete(_flow_key(sets[0], i))
+    tables = [t0, t1]
+    exp = {(si, ti, v): _expected(sets[si], m, tables[ti], verify=v) for si in range(8) for ti in range(2)
+           for v in (True, False)}
+    assert not np.array_equal(exp[(0, 0, True)], exp[(0, 1, True)])
+    ring = torch.zeros(2 * m * STRIDE, dtype=torch.uint8).pin_memory()
+    ring_np = ring.numpy().reshape(2 * m, STRIDE)
+    outs = [torch.zeros(m * 16, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    ctx = pa.RxContext(0)
+    try:
+        ti = 0
+        ctx.set_conn_table(tables[ti])
+        svc = pa.RxService(ctx, STRIDE, FRAME_OFF)
+        try:
+            pending = {}  # half -> (post id, set, table, n, verify)
+            for it in range(600):
+                h = it & 1
+                if h in pending:
+                    pid, si, tj, n, v = pending.pop(h)
+                    svc.wait(pid)
+                    got = outs[h].numpy()[: n * 16].view(pa.RESULT_DTYPE)
+                    assert np.array_equal(got, exp[(si, tj, v)][:n]), (it, pid, si, tj, n, v)
+                si = int(rng.integers(0, 8))
+                ring_np[h * m:(h + 1) * m] = sets[si]
+                if rng.random() < 0.15:  # a table change with the other half's post in flight
+                    ti ^= 1
+                    ctx.set_conn_table(tables[ti])
+                v = bool(rng.random() < 0.5)
+                ctx.set_verify(v)
+                n = int(rng.integers(1, m + 1))
+                outs[h].zero_()
+                pid = svc.post(ring[h * m * STRIDE:], n, outs[h])
+                pending[h] = (pid, si, ti, n, v)
+            for h, (pid, si, tj, n, v) in pending.items():
+                svc.wait(pid)
+                got = outs[h].numpy()[: n * 16].view(pa.RESULT_DTYPE)
+                assert np.array_equal(got, exp[(si, tj, v)][:n]), ("tail", pid, si, tj, n, v)
+        finally:
+            svc.close()
+    finally:
+        ctx.close()

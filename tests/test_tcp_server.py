@@ -80,6 +80,15 @@ def test_gpu_server_resident_post_ids_wrap():
     assert p.stdout.count("gpu: handler log identical, TX frames identical") == 8, p.stdout
 
 
+@pytest.mark.gpu
+def test_gpu_server_resident_host_mailbox():
+    """The resident-service modes with the service's mailbox in pinned host memory (PN_SERVICE_HOST_MAILBOX: the
+    path a device without a large BAR takes): handler log and every TX frame equal to the twin's."""
+    p = _peer("gpu", 1, env={"PN_SERVICE_HOST_MAILBOX": "1"})
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert p.stdout.count("gpu: handler log identical, TX frames identical") == 8, p.stdout
+
+
 CLISRV = os.path.join(ROOT, "tests", "cpp", "test_tcp_client_server")
 
 
