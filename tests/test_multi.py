@@ -416,3 +416,28 @@ def test_shared_host_ring_refuses_what_does_not_fit():
     assert "GiB" in room_for(1 << 50)
     with pytest.raises(RuntimeError, match="no shared host ring"):
         SharedHostRing(None, 0, 1, 1 << 40, 2048)
+
+
+def test_server_rounds_median_legs():
+    """bench.py's server placements run in rounds; each leg is reported from its median round with every round's
+    rate beside it, `delivered_ok` only if every round delivered, and the summary takes the hot pair from them."""
+    import importlib.util
+    import sys
+
+    sys.path.insert(0, ROOT)
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    leg = "gpu_rxbatch_512_pipelined_resident_release_path"
+    ref = "reference_server_release_build"
+    rows = [{leg: {"mframes_per_s": g, "mframes_per_s_server_only": g + 10}, ref: {"mframes_per_s": r,
+             "mframes_per_s_server_only": r + 10}, "delivered_ok": ok}
+            for g, r, ok in ((58.0, 54.0, True), (12.0, 53.0, True), (61.0, 55.0, True))]
+    m = bench.median_legs(rows)
+    assert m[leg]["mframes_per_s"] == 58.0 and m[leg]["rounds_mframes_per_s"] == [58.0, 12.0, 61.0]
+    assert m[ref]["mframes_per_s"] == 54.0 and m["delivered_ok"] is True and m["rounds"] == 3
+    rows[1]["delivered_ok"] = False
+    assert bench.median_legs(rows)["delivered_ok"] is False
+    s = bench.summary({"value": 1.0, "unit": "Gbit/s", "n_gpus": 1, "secondary": {"tcp_server_poll": {"hot": m}}})
+    assert s["server_hot_pair_median3_mfps"] == [58.0, 54.0]
+    assert s["server_hot_frames_resident_vs_reference_mfps"] == [68.0, 64.0]
